@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of Isaac-Velocity-Flat-H12_12dof-v0 random-action rollouts, 4096 envs per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = one ManagerBasedRLEnv.step of every env on the GPU (4 physics steps x 2 inner integration
+steps, delayed PD, contact, sensor, rewards, terminations, resets, commands, 450-float observations).
+Actions ~ N(0,1) are pre-generated and resident in HBM before timing.  Envs shard across ranks
+(4096 per GPU, weak scaling, RNG keyed by global env id); no collective inside the timed region.
+
+Rank 0 prints ONE JSON line with the contract fields plus `roofline` (dominant kernel, measured with
+HIP events on the env's stream) and `cpu_baseline` (the CPU oracle on host cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
+
+METRIC = "env-steps/sec at 4096 envs, Velocity-Flat-H12_12dof, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=500)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--envs", type=int, default=4096, help="envs per GPU (the metric is quoted at 4096)")
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc-file", type=str, default=None,
+                   help="JSON with per-launch HBM bytes from a rocprofv3 --pmc run (fills roofline.traffic)")
+    p.add_argument("--profile-only", action="store_true", help="timed loop only (for rocprofv3 runs)")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The CPU oracle (C, fp64, OpenMP over envs) on this host, bounded sample of the same workload."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+    from h12env import H12FlatEnvCfg
+    from h12env.model import build_model
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    n = 4096
+    cfg = H12FlatEnvCfg()
+    cfg.scene.num_envs = n
+    env = O.OracleEnv(build_model(), cfg.to_c(), n)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.normal(size=(8, n, 12)).astype(np.float32)
+    env.step(acts[0], 1, n_threads=threads)  # warm
+    t0 = time.perf_counter()
+    steps = 0
+    while time.perf_counter() - t0 < seconds:
+        env.step(acts[steps % 8], steps + 2, n_threads=threads)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/h12_oracle.c (fp64, OpenMP) on {n} envs x {steps} env steps "
+                      f"({dt:.1f} s) of the same random-action Flat-H12 workload, {threads} host threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+
+    from h12env import H12FlatEnvCfg
+    from h12env.env import H12VelocityEnv
+
+    n = args.envs
+    cfg = H12FlatEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = str(dev)
+    env = H12VelocityEnv(cfg, env_offset=rank * n)
+    env.reset()
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    K, W = args.steps, args.warmup
+    pool = min(K + W, 256)
+    actions = torch.randn(pool, n, 12, device=dev, generator=g)  # resident in HBM before timing
+
+    for i in range(W):
+        env.step(actions[i % pool])
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        env.step(actions[(W + i) % pool])
+    barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if args.profile_only:
+        if rank == 0:
+            print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * dt / K}))
+        return
+
+    # per-launch kernel duration with HIP events on the env's stream (separate pass, so the timed
+    # region above is not perturbed by event records)
+    stream = torch.cuda.current_stream(dev)
+    M = min(K, 200)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(M)]
+    for i in range(M):
+        ev[i][0].record(stream)
+        env.step(actions[i % pool])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+    kern_ms_avg = sum(kern_ms) / len(kern_ms)
+    bytes_env, flops_env = env.step_cost()
+
+    value = world * n * K / dt
+    if rank == 0:
+        achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
+        traffic = None
+        if args.pmc_file and Path(args.pmc_file).exists():
+            traffic = json.loads(Path(args.pmc_file).read_text()).get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": 1e3 * dt / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: N(0,1) random actions, reset distribution of the Flat task (seeded)",
+            "config": {
+                "workload": "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X",
+                "envs_per_gpu": n,
+                "global_envs": n * world,
+                "decimation": cfg.decimation,
+                "physics_dt": cfg.sim.dt,
+                "inner_steps": cfg.sim.inner_steps,
+                "parallelism": f"env-shard x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "step_kernel",
+                "kernel_ms_avg": kern_ms_avg,
+                "kernel_ms_p50": kern_ms[len(kern_ms) // 2],
+                "algorithmic_bytes_per_env_step": bytes_env,
+                "valu_flops_per_env_step": flops_env,
+                "valu_tflops": flops_env * n / (kern_ms_avg * 1e-3) / 1e12,
+                "valu_frac": flops_env * n / (kern_ms_avg * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+            },
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

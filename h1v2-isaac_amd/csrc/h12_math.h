@@ -1,0 +1,176 @@
+// h12_math.h — fp32 device helpers for the H1-2 env kernels (CDNA4 / gfx950).
+//
+// Spatial-vector conventions (Featherstone): motion m = (w; v), force f = (n; f), 6-vectors with the
+// angular part first.  Every H1-2 leg joint turns about a coordinate axis of its parent frame and
+// carries no fixed rotation (MJCF h12_12dof.xml:71-134), so every per-link transform is "rotate about
+// axis A by q, then shift by r" and all rotations below are templated on the axis.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define H12_DEV __device__ __forceinline__
+
+namespace h12 {
+
+// out = R_A(q) * in   (child coords -> parent axes); c = cos q, s = sin q
+template <int A>
+H12_DEV void rot(float c, float s, const float* in, float* out) {
+  float x = in[0], y = in[1], z = in[2];
+  if constexpr (A == 0) { out[0] = x; out[1] = c * y - s * z; out[2] = s * y + c * z; }
+  else if constexpr (A == 1) { out[0] = c * x + s * z; out[1] = y; out[2] = -s * x + c * z; }
+  else { out[0] = c * x - s * y; out[1] = s * x + c * y; out[2] = z; }
+}
+// out = R_A(q)^T * in (parent axes -> child coords)
+template <int A>
+H12_DEV void rotT(float c, float s, const float* in, float* out) { rot<A>(c, -s, in, out); }
+
+H12_DEV void cross(const float* a, const float* b, float* o) {
+  float t0 = a[1] * b[2] - a[2] * b[1];
+  float t1 = a[2] * b[0] - a[0] * b[2];
+  float t2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+H12_DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// 3x3 rotation from unit quaternion (w x y z); R maps body -> world
+H12_DEV void quat_R(const float* q, float R[3][3]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - w * z); R[0][2] = 2.f * (x * z + w * y);
+  R[1][0] = 2.f * (x * y + w * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - w * x);
+  R[2][0] = 2.f * (x * z - w * y); R[2][1] = 2.f * (y * z + w * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+H12_DEV void mv(const float R[3][3], const float* v, float* o) {
+  float t0 = R[0][0] * v[0] + R[0][1] * v[1] + R[0][2] * v[2];
+  float t1 = R[1][0] * v[0] + R[1][1] * v[1] + R[1][2] * v[2];
+  float t2 = R[2][0] * v[0] + R[2][1] * v[1] + R[2][2] * v[2];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+H12_DEV void mtv(const float R[3][3], const float* v, float* o) {
+  float t0 = R[0][0] * v[0] + R[1][0] * v[1] + R[2][0] * v[2];
+  float t1 = R[0][1] * v[0] + R[1][1] * v[1] + R[2][1] * v[2];
+  float t2 = R[0][2] * v[0] + R[1][2] * v[1] + R[2][2] * v[2];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+// R <- R * R_A(q)  (world rotation of a child frame)
+template <int A>
+H12_DEV void rmul_axis(float R[3][3], float c, float s) {
+  for (int i = 0; i < 3; ++i) {
+    float row[3] = {R[i][0], R[i][1], R[i][2]}, o[3];
+    // row * R_A = (R_A^T row^T)^T
+    rotT<A>(c, s, row, o);
+    R[i][0] = o[0]; R[i][1] = o[1]; R[i][2] = o[2];
+  }
+}
+
+// Articulated-body inertia I = [[A, B], [B^T, C]] with A, C symmetric (xx yy zz xy xz yz).
+struct AInertia {
+  float A[6];
+  float B[3][3];
+  float C[6];
+};
+H12_DEV float sget(const float* S, int i, int j) {
+  // symmetric accessor, indices resolved at compile time after unrolling
+  if (i == j) return S[i];
+  int a = i < j ? i : j, b = i < j ? j : i;
+  return (a == 0) ? (b == 1 ? S[3] : S[4]) : S[5];
+}
+H12_DEV void sym_full(const float* S, float M[3][3]) {
+  M[0][0] = S[0]; M[1][1] = S[1]; M[2][2] = S[2];
+  M[0][1] = M[1][0] = S[3]; M[0][2] = M[2][0] = S[4]; M[1][2] = M[2][1] = S[5];
+}
+H12_DEV void full_sym(const float M[3][3], float* S) {
+  S[0] = M[0][0]; S[1] = M[1][1]; S[2] = M[2][2]; S[3] = M[0][1]; S[4] = M[0][2]; S[5] = M[1][2];
+}
+// I * m for a 6-vector m = (w; v):  (A w + B v ; B^T w + C v)
+H12_DEV void ai_mul(const AInertia& I, const float* m, float* o) {
+  const float* w = m;
+  const float* v = m + 3;
+  for (int i = 0; i < 3; ++i) {
+    o[i] = sget(I.A, i, 0) * w[0] + sget(I.A, i, 1) * w[1] + sget(I.A, i, 2) * w[2] +
+           I.B[i][0] * v[0] + I.B[i][1] * v[1] + I.B[i][2] * v[2];
+    o[3 + i] = I.B[0][i] * w[0] + I.B[1][i] * w[1] + I.B[2][i] * w[2] +
+               sget(I.C, i, 0) * v[0] + sget(I.C, i, 1) * v[1] + sget(I.C, i, 2) * v[2];
+  }
+}
+// rigid-body inertia at the body origin from (Ibar = I_origin (sym), mc = m*c, m)
+H12_DEV void ai_rigid(AInertia& I, const float* Ibar, const float* mc, float m) {
+  for (int i = 0; i < 6; ++i) I.A[i] = Ibar[i];
+  // B = m [c]x
+  I.B[0][0] = 0.f; I.B[0][1] = -mc[2]; I.B[0][2] = mc[1];
+  I.B[1][0] = mc[2]; I.B[1][1] = 0.f; I.B[1][2] = -mc[0];
+  I.B[2][0] = -mc[1]; I.B[2][1] = mc[0]; I.B[2][2] = 0.f;
+  I.C[0] = I.C[1] = I.C[2] = m;
+  I.C[3] = I.C[4] = I.C[5] = 0.f;
+}
+H12_DEV void ai_add(AInertia& I, const AInertia& J) {
+  for (int i = 0; i < 6; ++i) { I.A[i] += J.A[i]; I.C[i] += J.C[i]; }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) I.B[i][j] += J.B[i][j];
+}
+// rotate every block into parent axes: X_rot^T I X_rot with E^T = R_A(q)
+template <int A>
+H12_DEV void ai_rotate(AInertia& I, float c, float s) {
+  float M[3][3], T[3][3];
+  // A block: R A R^T
+  sym_full(I.A, M);
+  for (int j = 0; j < 3; ++j) { float col[3] = {M[0][j], M[1][j], M[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
+  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); M[i][0] = o[0]; M[i][1] = o[1]; M[i][2] = o[2]; }
+  full_sym(M, I.A);
+  sym_full(I.C, M);
+  for (int j = 0; j < 3; ++j) { float col[3] = {M[0][j], M[1][j], M[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
+  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); M[i][0] = o[0]; M[i][1] = o[1]; M[i][2] = o[2]; }
+  full_sym(M, I.C);
+  // B block: R B R^T
+  for (int j = 0; j < 3; ++j) { float col[3] = {I.B[0][j], I.B[1][j], I.B[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
+  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); I.B[i][0] = o[0]; I.B[i][1] = o[1]; I.B[i][2] = o[2]; }
+}
+// shift the reference point from the child origin to the parent origin (child origin at r in
+// parent coords, parent axes): A += S + S^T - T rx, B += T, with T = rx C, S = rx B^T.
+H12_DEV void ai_shift(AInertia& I, const float* r) {
+  float Cf[3][3], T[3][3], S[3][3];
+  sym_full(I.C, Cf);
+  for (int j = 0; j < 3; ++j) { float col[3] = {Cf[0][j], Cf[1][j], Cf[2][j]}, o[3]; cross(r, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
+  // S = rx B^T : column j of B^T is row j of B
+  for (int j = 0; j < 3; ++j) { float col[3] = {I.B[j][0], I.B[j][1], I.B[j][2]}, o[3]; cross(r, col, o); S[0][j] = o[0]; S[1][j] = o[1]; S[2][j] = o[2]; }
+  // (T rx)_ij = T_i . rx_col_j ; rx = [[0,-rz,ry],[rz,0,-rx],[-ry,rx,0]]
+  auto trx = [&](int i, int j) {
+    float rxc0 = (j == 0) ? 0.f : (j == 1 ? -r[2] : r[1]);
+    float rxc1 = (j == 0) ? r[2] : (j == 1 ? 0.f : -r[0]);
+    float rxc2 = (j == 0) ? -r[1] : (j == 1 ? r[0] : 0.f);
+    return T[i][0] * rxc0 + T[i][1] * rxc1 + T[i][2] * rxc2;
+  };
+  I.A[0] += 2.f * S[0][0] - trx(0, 0);
+  I.A[1] += 2.f * S[1][1] - trx(1, 1);
+  I.A[2] += 2.f * S[2][2] - trx(2, 2);
+  I.A[3] += S[0][1] + S[1][0] - trx(0, 1);
+  I.A[4] += S[0][2] + S[2][0] - trx(0, 2);
+  I.A[5] += S[1][2] + S[2][1] - trx(1, 2);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) I.B[i][j] += T[i][j];
+}
+
+// Philox4x32-10 (same streams as oracle/h12_oracle.c)
+H12_DEV void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t y0 = hi1 ^ c1 ^ k0;
+    uint32_t y2 = hi0 ^ c3 ^ k1;
+    c1 = lo1;
+    c3 = lo0;
+    c0 = y0;
+    c2 = y2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+H12_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+H12_DEV float uab(uint32_t x, float a, float b) { return a + (b - a) * u01(x); }
+
+// lane-pair exchange (lanes 2e and 2e+1 hold the two legs of env e)
+H12_DEV float pair_swap(float x) { return __shfl_xor(x, 1); }
+H12_DEV int pair_swap_i(int x) { return __shfl_xor(x, 1); }
+
+}  // namespace h12

@@ -1,0 +1,1258 @@
+// h12env.hip — MI355X (gfx950) implementation of the Isaac-Velocity-Flat-H12_12dof-v0 env step.
+//
+// One fused kernel per env step: delayed explicit PD (h12.py:58-112) -> decimation x inner_steps x
+// (penalty contact + Featherstone ABA over the 13-body tree + semi-implicit Euler) -> contact sensor
+// (history 3, air time) -> terminations -> 12 reward terms -> masked in-kernel resets -> command
+// update -> observation frame + 10-frame history (ManagerBasedRLEnv.step, cat_env.py:95-193).
+//
+// Thread mapping: a LANE PAIR per env (lanes 2e, 2e+1 of a wave64 own the left / right leg).
+// Mirror lanes: the H1-2 right leg is the exact mirror image of the left one about the pelvis
+// xz-plane, so the right-leg lane runs the very same code and literal constants in MIRRORED
+// coordinates (y -> -y; x/z joint angles negated).  The two legs meet only at the floating base:
+// each lane un-mirrors its leg's articulated inertia / bias force, one DPP lane swap exchanges them,
+// and both lanes solve the same 6x6 base system (fixed left+right summation order keeps the two
+// copies bit-identical).  State is structure-of-arrays so each field access of a wave is one
+// contiguous segment; the 450-float observation rows are written cooperatively through LDS so each
+// wave stores its 32 consecutive rows as one contiguous, coalesced block.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "../../include/h12env.h"
+#include "h12_math.h"
+#include "h12_model_gen.h"
+
+using namespace h12;
+
+namespace {
+
+constexpr int NJ = H12_NJ;
+constexpr int NL = 6;               // links per leg
+constexpr int ENVS_PER_BLOCK = 32;  // 64 lanes = 32 lane pairs
+constexpr int BLOCK = 64;
+// joint axes per leg link: hip yaw z, hip pitch y, hip roll x, knee y, ankle pitch y, ankle roll x
+constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
+
+thread_local char g_err[512] = "";
+int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return set_err(H12_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+// ------------------------------------------------------------------ runtime parameters (kernarg)
+struct KParams {
+  float kp[NL], kd[NL], elim[NL], dimpl[NL];  // per leg link (leg-symmetric)
+  int dgroup[NL];
+  float g;
+  int mode, fix_base, decimation, inner, max_len, min_delay, max_delay, use_fl;
+  int corrupt, ill_knees, ill_torso;
+  float dt, h, step_dt, action_scale, soft_f;
+  float ck, cc, fk, fc, mus, mud, lk, lc, cthr;
+  float cmd_T, cmd_x0, cmd_x1, cmd_y0, cmd_y1, cmd_w0, cmd_w1, cmd_h0, cmd_h1;
+  float rel_stand, rel_head, head_k;
+  float rx0, rx1, ry0, ry1, ryaw0, ryaw1, root_z;
+  float n_w, n_g, n_q, n_qd;
+  float rew_w[H12_NREW];
+  float std2_inv, air_thr;
+  uint32_t seed_lo, seed_hi;
+};
+static_assert(sizeof(KParams) < 1024, "kernarg budget");
+
+struct Workspace {
+  float* F;    // [H12_NF_FLOAT][n]
+  int32_t* I;  // [H12_NF_INT][n]
+  int n;
+};
+
+enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3 };
+
+// joint-angle sign of leg link k in the lane's frame (x / z joints flip under the y-mirror)
+H12_DEV float jsign(int k, float sg) { return AX[k] == 1 ? 1.f : sg; }
+// soft joint limits (ArticulationCfg.soft_joint_pos_limit_factor) in the left-leg frame
+H12_DEV float soft_lo(const KParams& P, int k) {
+  return 0.5f * (h12m::QLO[k] + h12m::QHI[k]) - 0.5f * (h12m::QHI[k] - h12m::QLO[k]) * P.soft_f;
+}
+H12_DEV float soft_hi(const KParams& P, int k) {
+  return 0.5f * (h12m::QLO[k] + h12m::QHI[k]) + 0.5f * (h12m::QHI[k] - h12m::QLO[k]) * P.soft_f;
+}
+
+// ------------------------------------------------------------------ per-lane simulation state
+struct Base {               // shared floating base, REAL coordinates (identical in both lanes)
+  float pos[3], quat[4], vlin[3], wang[3];
+};
+struct Leg {                // this lane's leg in the lane frame (mirrored for the right leg)
+  float q[NL], qd[NL];
+  float anc[H12_NFOOT_PTS][2];
+  int cmask;                // 4 bits: sole sphere (lane-frame index) in contact
+};
+struct Forces {             // net contact force of this lane's bodies (lane world frame)
+  float foot[3], knee[3], torso[3];
+};
+
+// one penalty contact (sphere centre pl in body coords, body world pose Rb/pb, body spatial velocity
+// vb in body coords); adds the body-frame spatial force into f[6]; anchored stiction for sole spheres
+template <bool ANCHOR>
+H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
+                            const float* pl, float rad, float* f, float* fw, float* anc, bool was_in) {
+  float xw[3];
+  mv(Rb, pl, xw);
+  xw[0] += pb[0]; xw[1] += pb[1]; xw[2] += pb[2];
+  float depth = rad - xw[2];
+  if (!(depth > 0.f)) return false;
+  float vl[3];
+  cross(vb, pl, vl);
+  vl[0] += vb[3]; vl[1] += vb[4]; vl[2] += vb[5];
+  float vw[3];
+  mv(Rb, vl, vw);
+  float fn = P.ck * depth - P.cc * vw[2];
+  if (!(fn > 0.f)) return false;
+  float ft0, ft1;
+  if constexpr (ANCHOR) {
+    float ax = was_in ? anc[0] : xw[0], ay = was_in ? anc[1] : xw[1];
+    ft0 = -P.fk * (xw[0] - ax) - P.fc * vw[0];
+    ft1 = -P.fk * (xw[1] - ay) - P.fc * vw[1];
+    float ftn = sqrtf(ft0 * ft0 + ft1 * ft1);
+    if (ftn > P.mus * fn) {
+      float sc = P.mud * fn / ftn;
+      ft0 *= sc;
+      ft1 *= sc;
+      ax = xw[0] + ft0 / P.fk;
+      ay = xw[1] + ft1 / P.fk;
+    }
+    anc[0] = ax;
+    anc[1] = ay;
+  } else {
+    ft0 = -P.fc * vw[0];
+    ft1 = -P.fc * vw[1];
+    float ftn = sqrtf(ft0 * ft0 + ft1 * ft1), cap = P.mud * fn;
+    if (ftn > cap) { float sc = cap / ftn; ft0 *= sc; ft1 *= sc; }
+  }
+  float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
+  mtv(Rb, Fw, fl);
+  cross(pl, fl, nl);
+  f[0] += nl[0]; f[1] += nl[1]; f[2] += nl[2];
+  f[3] += fl[0]; f[4] += fl[1]; f[5] += fl[2];
+  fw[0] += Fw[0]; fw[1] += Fw[1]; fw[2] += Fw[2];
+  return true;
+}
+
+H12_DEV void quat_integrate(float* q, const float* w, float h) {
+  float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  if (wn > 0.f) {
+    float half = 0.5f * wn * h, sh, ch;
+    sincosf(half, &sh, &ch);
+    sh /= wn;
+    float r[4] = {ch, w[0] * sh, w[1] * sh, w[2] * sh};
+    float o[4] = {q[0] * r[0] - q[1] * r[1] - q[2] * r[2] - q[3] * r[3],
+                  q[0] * r[1] + q[1] * r[0] + q[2] * r[3] - q[3] * r[2],
+                  q[0] * r[2] - q[1] * r[3] + q[2] * r[0] + q[3] * r[1],
+                  q[0] * r[3] + q[1] * r[2] - q[2] * r[1] + q[3] * r[0]};
+    float inv = rsqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
+    q[0] = o[0] * inv; q[1] = o[1] * inv; q[2] = o[2] * inv; q[3] = o[3] * inv;
+  }
+}
+
+// Solve the 6x6 SPD system I x = b (LDL^T, fully unrolled)
+H12_DEV void solve6(const AInertia& I, const float* b, float* x) {
+  float M[6][6];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      M[i][j] = sget(I.A, i, j);
+      M[i][3 + j] = I.B[i][j];
+      M[3 + i][j] = I.B[j][i];
+      M[3 + i][3 + j] = sget(I.C, i, j);
+    }
+  float L[6][6], D[6], Dinv[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float d = M[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+    D[j] = d;
+    Dinv[j] = 1.f / d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      float t = M[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k] * D[k];
+      L[i][j] = t * Dinv[j];
+    }
+  }
+  float y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= L[i][k] * y[k];
+    y[i] = t;
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float t = y[i] * Dinv[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) t -= L[k][i] * x[k];
+    x[i] = t;
+  }
+}
+
+// ---- ABA pass 1 for leg link LINK: velocity, velocity-product accel, bias force, world pose
+template <int LINK>
+H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], float* v, float (&cb)[NL][6], float (&pA)[NL][6],
+                        float (&R)[3][3], float* p) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  float s, c;
+  sincosf(lg.q[LINK], &s, &c);
+  cs[LINK][0] = c;
+  cs[LINK][1] = s;
+  float t[3], wl[3], vl[3];
+  cross(r, v, t);
+  float lin[3] = {v[3] - t[0], v[4] - t[1], v[5] - t[2]};
+  rotT<A>(c, s, v, wl);
+  rotT<A>(c, s, lin, vl);
+  float qd = lg.qd[LINK];
+  wl[A] += qd;
+  v[0] = wl[0]; v[1] = wl[1]; v[2] = wl[2]; v[3] = vl[0]; v[4] = vl[1]; v[5] = vl[2];
+  // c = v x (e_A qd)
+  float e[3] = {0.f, 0.f, 0.f};
+  e[A] = qd;
+  cross(wl, e, cb[LINK]);
+  cross(vl, e, cb[LINK] + 3);
+  // bias force v x* (I v) with I = (Ibar, m c, m)
+  const float* Ibar = h12m::IBAR[LINK];
+  const float* mc = h12m::MC[LINK];
+  const float m = h12m::M[LINK];
+  float n[3], f[3], a1[3], a2[3];
+  for (int i = 0; i < 3; ++i) n[i] = sget(Ibar, i, 0) * wl[0] + sget(Ibar, i, 1) * wl[1] + sget(Ibar, i, 2) * wl[2];
+  cross(mc, vl, a1);
+  n[0] += a1[0]; n[1] += a1[1]; n[2] += a1[2];
+  cross(mc, wl, a2);
+  f[0] = m * vl[0] - a2[0]; f[1] = m * vl[1] - a2[1]; f[2] = m * vl[2] - a2[2];
+  float x1[3], x2[3], x3[3];
+  cross(wl, n, x1);
+  cross(vl, f, x2);
+  cross(wl, f, x3);
+  pA[LINK][0] = x1[0] + x2[0]; pA[LINK][1] = x1[1] + x2[1]; pA[LINK][2] = x1[2] + x2[2];
+  pA[LINK][3] = x3[0]; pA[LINK][4] = x3[1]; pA[LINK][5] = x3[2];
+  // world pose of the link frame
+  float Rr[3];
+  mv(R, r, Rr);
+  p[0] += Rr[0]; p[1] += Rr[1]; p[2] += Rr[2];
+  rmul_axis<A>(R, c, s);
+}
+
+// ---- ABA pass 2 for leg link LINK (leaf -> root), leaves the result expressed at the parent origin
+template <int LINK>
+H12_DEV void link_pass2(const KParams& P, const float (&cs)[NL][2], const float (&cb)[NL][6], const float (&pA)[NL][6],
+                        const float* tau, AInertia& IA, float* pAcc, float (&U)[NL][6], float (&Dinv)[NL],
+                        float (&u)[NL], float h) {
+  constexpr int A = AX[LINK];
+  float Ua[3] = {sget(IA.A, 0, A), sget(IA.A, 1, A), sget(IA.A, 2, A)};
+  float Ul[3] = {IA.B[A][0], IA.B[A][1], IA.B[A][2]};
+  float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK];
+  float di = 1.f / D;
+  float uu = tau[LINK] - pAcc[A];
+  U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
+  U[LINK][3] = Ul[0]; U[LINK][4] = Ul[1]; U[LINK][5] = Ul[2];
+  Dinv[LINK] = di;
+  u[LINK] = uu;
+  // Ia = IA - U U^T / D
+  float Uad[3] = {Ua[0] * di, Ua[1] * di, Ua[2] * di};
+  float Uld[3] = {Ul[0] * di, Ul[1] * di, Ul[2] * di};
+  IA.A[0] -= Ua[0] * Uad[0]; IA.A[1] -= Ua[1] * Uad[1]; IA.A[2] -= Ua[2] * Uad[2];
+  IA.A[3] -= Ua[0] * Uad[1]; IA.A[4] -= Ua[0] * Uad[2]; IA.A[5] -= Ua[1] * Uad[2];
+  IA.C[0] -= Ul[0] * Uld[0]; IA.C[1] -= Ul[1] * Uld[1]; IA.C[2] -= Ul[2] * Uld[2];
+  IA.C[3] -= Ul[0] * Uld[1]; IA.C[4] -= Ul[0] * Uld[2]; IA.C[5] -= Ul[1] * Uld[2];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * Uld[j];
+  // pa = pA + Ia c + U u / D
+  float Ic[6];
+  ai_mul(IA, cb[LINK], Ic);
+  float ud = uu * di;
+  float pa[6];
+  for (int i = 0; i < 3; ++i) {
+    pa[i] = pAcc[i] + Ic[i] + Ua[i] * ud;
+    pa[3 + i] = pAcc[3 + i] + Ic[3 + i] + Ul[i] * ud;
+  }
+  // to the parent: rotate into parent axes, then shift the reference point by r
+  float c = cs[LINK][0], s = cs[LINK][1];
+  const float* r = h12m::R[LINK];
+  ai_rotate<A>(IA, c, s);
+  ai_shift(IA, r);
+  float nr[3], fr[3], rf[3];
+  rot<A>(c, s, pa, nr);
+  rot<A>(c, s, pa + 3, fr);
+  cross(r, fr, rf);
+  pAcc[0] = nr[0] + rf[0]; pAcc[1] = nr[1] + rf[1]; pAcc[2] = nr[2] + rf[2];
+  pAcc[3] = fr[0]; pAcc[4] = fr[1]; pAcc[5] = fr[2];
+  if constexpr (LINK > 0) {
+    AInertia Rg;
+    ai_rigid(Rg, h12m::IBAR[LINK - 1], h12m::MC[LINK - 1], h12m::M[LINK - 1]);
+    ai_add(IA, Rg);
+    for (int i = 0; i < 6; ++i) pAcc[i] += pA[LINK - 1][i];
+  }
+}
+
+// ---- ABA pass 3 for leg link LINK (root -> leaf)
+template <int LINK>
+H12_DEV void link_pass3(const float (&cs)[NL][2], const float (&cb)[NL][6], const float (&U)[NL][6],
+                        const float (&Dinv)[NL], const float (&u)[NL], float* a, float* qdd) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  float c = cs[LINK][0], s = cs[LINK][1];
+  float t[3];
+  cross(r, a, t);
+  float lin[3] = {a[3] - t[0], a[4] - t[1], a[5] - t[2]};
+  float w[3], l[3];
+  rotT<A>(c, s, a, w);
+  rotT<A>(c, s, lin, l);
+  a[0] = w[0] + cb[LINK][0]; a[1] = w[1] + cb[LINK][1]; a[2] = w[2] + cb[LINK][2];
+  a[3] = l[0] + cb[LINK][3]; a[4] = l[1] + cb[LINK][4]; a[5] = l[2] + cb[LINK][5];
+  float ua = 0.f;
+  for (int i = 0; i < 6; ++i) ua += U[LINK][i] * a[i];
+  float x = (u[LINK] - ua) * Dinv[LINK];
+  qdd[LINK] = x;
+  a[A] += x;
+}
+
+// spatial sign of the y-mirror for component i of a motion / force 6-vector (ang x,y,z, lin x,y,z)
+H12_DEV float s6(int i, float sg) { return (i % 2 == 0) ? sg : 1.f; }
+
+// One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
+// lane's 6 joints (lane frame).  Adds this lane's contact forces * wgt into fr.
+H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
+                        float wgt) {
+  const float sg = leg ? -1.f : 1.f;
+  float R0[3][3];
+  quat_R(b.quat, R0);
+  float vb[3];
+  mtv(R0, b.vlin, vb);
+  // base quantities in the lane frame: R' = M R M, v' = s6 * v, p' = M p
+  const float mm[3] = {1.f, sg, 1.f};
+  float R[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i][j] = mm[i] * mm[j] * R0[i][j];
+  float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+  float v[6];
+  for (int i = 0; i < 6; ++i) v[i] = s6(i, sg) * v0[i];
+  float p[3] = {b.pos[0], sg * b.pos[1], b.pos[2]};
+  float cs[NL][2], cb[NL][6], pA[NL][6];
+  float Rk[3][3], pk[3], vk[6];
+  link_pass1<0>(lg, cs, v, cb, pA, R, p);
+  link_pass1<1>(lg, cs, v, cb, pA, R, p);
+  link_pass1<2>(lg, cs, v, cb, pA, R, p);
+  link_pass1<3>(lg, cs, v, cb, pA, R, p);
+  for (int i = 0; i < 3; ++i) { pk[i] = p[i]; for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j]; }
+  for (int i = 0; i < 6; ++i) vk[i] = v[i];
+  link_pass1<4>(lg, cs, v, cb, pA, R, p);
+  link_pass1<5>(lg, cs, v, cb, pA, R, p);
+
+  // ---- contacts: external forces are subtracted from the bias forces
+  {
+    float fext[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int nmask = 0;
+#pragma unroll
+    for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+      bool was = (lg.cmask >> q) & 1;
+      if (contact_sphere<true>(P, R, p, v, h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was)) nmask |= 1 << q;
+    }
+    lg.cmask = nmask;
+    for (int i = 0; i < 6; ++i) pA[5][i] -= fext[i];
+  }
+  {
+    float w0[3], w1[3];
+    mv(Rk, h12m::KNEE0, w0);
+    mv(Rk, h12m::KNEE1, w1);
+    const float* pl = (w0[2] <= w1[2]) ? h12m::KNEE0 : h12m::KNEE1;
+    float fk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float tmp[3] = {0.f, 0.f, 0.f};
+    float dummy[2];
+    contact_sphere<false>(P, Rk, pk, vk, pl, h12m::KNEE_R, fk, tmp, dummy, false);
+    for (int i = 0; i < 6; ++i) pA[3][i] -= fk[i];
+    fr.knee[0] += wgt * tmp[0]; fr.knee[1] += wgt * tmp[1]; fr.knee[2] += wgt * tmp[2];
+  }
+  // ---- joint torques for this inner step: actuator + limit penalty (+ MuJoCo passive)
+  float tau[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    float q = lg.q[k], qd = lg.qd[k];
+    float t = tau_pd[k];
+    if (q > h12m::QHI[k]) t += fminf(0.f, -P.lk * (q - h12m::QHI[k]) - P.lc * qd);
+    else if (q < h12m::QLO[k]) t += fmaxf(0.f, -P.lk * (q - h12m::QLO[k]) - P.lc * qd);
+    t -= P.dimpl[k] * qd;
+    if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
+    tau[k] = t;
+  }
+  // ---- pass 2 (leaf -> root)
+  AInertia IA;
+  ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
+  float pAcc[6];
+  for (int i = 0; i < 6; ++i) pAcc[i] = pA[5][i];
+  float U[NL][6], Dinv[NL], u[NL];
+  link_pass2<5>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<4>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<3>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<2>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<1>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<0>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
+  }
+  IA.A[3] *= sg; IA.A[5] *= sg;  // xy, yz of the angular block (s = (sg,1,sg))
+  IA.C[3] *= sg; IA.C[5] *= sg;  // xy, yz of the linear block (s = (1,sg,1))
+  for (int i = 0; i < 6; ++i) pAcc[i] *= s6(i, sg);
+  // ---- lane 0 adds the base body: rigid inertia, bias force, torso-box contact
+  float ag[6] = {0.f, 0.f, 0.f, -P.g * R0[2][0], -P.g * R0[2][1], -P.g * R0[2][2]};
+  if (leg == 0) {
+    AInertia Rg;
+    ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
+    ai_add(IA, Rg);
+    float hb[6];
+    ai_mul(Rg, v0, hb);
+    float x1[3], x2[3], x3[3];
+    cross(v0, hb, x1);
+    cross(v0 + 3, hb + 3, x2);
+    cross(v0, hb + 3, x3);
+    pAcc[0] += x1[0] + x2[0]; pAcc[1] += x1[1] + x2[1]; pAcc[2] += x1[2] + x2[2];
+    pAcc[3] += x3[0]; pAcc[4] += x3[1]; pAcc[5] += x3[2];
+    float corner[3];
+    for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+    float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float tmp[3] = {0.f, 0.f, 0.f};
+    float dummy[2];
+    contact_sphere<false>(P, R0, b.pos, v0, corner, 0.f, ft, tmp, dummy, false);
+    for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
+    fr.torso[0] += wgt * tmp[0]; fr.torso[1] += wgt * tmp[1]; fr.torso[2] += wgt * tmp[2];
+  }
+  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
+  AInertia IB;
+  float pB[6];
+  {
+    auto comb = [&](float x) {
+      float y = pair_swap(x);
+      return leg ? (y + x) : (x + y);
+    };
+    for (int i = 0; i < 6; ++i) { IB.A[i] = comb(IA.A[i]); IB.C[i] = comb(IA.C[i]); pB[i] = comb(pAcc[i]); }
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) IB.B[i][j] = comb(IA.B[i][j]);
+  }
+  float a0[6];
+  if (P.fix_base) {
+    for (int i = 0; i < 6; ++i) a0[i] = -ag[i];
+  } else {
+    float rhs[6] = {-pB[0], -pB[1], -pB[2], -pB[3], -pB[4], -pB[5]};
+    solve6(IB, rhs, a0);
+  }
+  // ---- pass 3 (root -> leaf) in the lane frame
+  float a[6];
+  for (int i = 0; i < 6; ++i) a[i] = s6(i, sg) * a0[i];
+  float qdd[NL];
+  link_pass3<0>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<1>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<2>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<3>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<4>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<5>(cs, cb, U, Dinv, u, a, qdd);
+  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates
+  if (!P.fix_base) {
+    float nd[6];
+    for (int i = 0; i < 6; ++i) nd[i] = a0[i] + ag[i];
+    float wxv[3];
+    cross(b.wang, vb, wxv);
+    float al[3] = {nd[3] + wxv[0], nd[4] + wxv[1], nd[5] + wxv[2]}, aw[3];
+    mv(R0, al, aw);
+    for (int i = 0; i < 3; ++i) { b.vlin[i] += h * aw[i]; b.wang[i] += h * nd[i]; }
+    for (int i = 0; i < 3; ++i) b.pos[i] += h * b.vlin[i];
+    quat_integrate(b.quat, b.wang, h);
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    lg.qd[k] += h * qdd[k];
+    lg.q[k] += h * lg.qd[k];
+  }
+}
+
+// ------------------------------------------------------------------ state load / store
+H12_DEV float ldf(const Workspace& W, int f, int e) { return W.F[(size_t)f * W.n + e]; }
+H12_DEV void stf(const Workspace& W, int f, int e, float x) { W.F[(size_t)f * W.n + e] = x; }
+
+struct EnvSt {
+  Base b;
+  Leg lg;                         // lane frame
+  float act[NL], act1[NL];        // a_t, a_{t-1} of this leg (lane frame)
+  float cmd[3], heading, cmd_time;
+  float air, con, last_air, last_con;  // this lane's foot
+  float epsum[H12_NREW];
+  int eplen, lag[3], since_reset, is_heading, is_standing;
+};
+
+H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
+  const float sg = leg ? -1.f : 1.f;
+  for (int i = 0; i < 3; ++i) s.b.pos[i] = ldf(W, H12_F_POS + i, e);
+  for (int i = 0; i < 4; ++i) s.b.quat[i] = ldf(W, H12_F_QUAT + i, e);
+  for (int i = 0; i < 3; ++i) s.b.vlin[i] = ldf(W, H12_F_VLIN + i, e);
+  for (int i = 0; i < 3; ++i) s.b.wang[i] = ldf(W, H12_F_WANG + i, e);
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    float js = jsign(k, sg);
+    s.lg.q[k] = js * ldf(W, H12_F_Q + NL * leg + k, e);
+    s.lg.qd[k] = js * ldf(W, H12_F_QD + NL * leg + k, e);
+    s.act[k] = js * ldf(W, H12_F_ACT + NL * leg + k, e);
+    s.act1[k] = js * ldf(W, H12_F_ACT_PREV + NL * leg + k, e);
+  }
+  int pk = W.I[(size_t)H12_I_PACK * W.n + e];
+  int cm = (pk >> (13 + 4 * leg)) & 0xF;
+  s.lg.cmask = 0;
+#pragma unroll
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+    int qr = leg ? (q ^ 1) : q;  // mirrored sole sphere q is real sphere q^1
+    s.lg.anc[q][0] = ldf(W, H12_F_ANCHOR + 8 * leg + 2 * qr, e);
+    s.lg.anc[q][1] = sg * ldf(W, H12_F_ANCHOR + 8 * leg + 2 * qr + 1, e);
+    s.lg.cmask |= ((cm >> qr) & 1) << q;
+  }
+  for (int i = 0; i < 3; ++i) s.cmd[i] = ldf(W, H12_F_CMD + i, e);
+  s.heading = ldf(W, H12_F_HEADING, e);
+  s.cmd_time = ldf(W, H12_F_CMD_TIME, e);
+  s.air = ldf(W, H12_F_AIR + leg, e);
+  s.con = ldf(W, H12_F_CONTACT + leg, e);
+  s.last_air = ldf(W, H12_F_LAST_AIR + leg, e);
+  s.last_con = ldf(W, H12_F_LAST_CONTACT + leg, e);
+  for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
+  s.eplen = W.I[(size_t)H12_I_EPLEN * W.n + e];
+  for (int g = 0; g < 3; ++g) s.lag[g] = (pk >> (3 * g)) & 7;
+  s.since_reset = (pk >> 9) & 3;
+  s.is_heading = (pk >> 11) & 1;
+  s.is_standing = (pk >> 12) & 1;
+}
+
+H12_DEV void store_env(const Workspace& W, int e, int leg, const EnvSt& s) {
+  const float sg = leg ? -1.f : 1.f;
+  if (leg == 0) {
+    for (int i = 0; i < 3; ++i) stf(W, H12_F_POS + i, e, s.b.pos[i]);
+    for (int i = 0; i < 4; ++i) stf(W, H12_F_QUAT + i, e, s.b.quat[i]);
+    for (int i = 0; i < 3; ++i) stf(W, H12_F_VLIN + i, e, s.b.vlin[i]);
+    for (int i = 0; i < 3; ++i) stf(W, H12_F_WANG + i, e, s.b.wang[i]);
+    for (int i = 0; i < 3; ++i) stf(W, H12_F_CMD + i, e, s.cmd[i]);
+    stf(W, H12_F_HEADING, e, s.heading);
+    stf(W, H12_F_CMD_TIME, e, s.cmd_time);
+    for (int t = 0; t < H12_NREW; ++t) stf(W, H12_F_EPSUM + t, e, s.epsum[t]);
+    W.I[(size_t)H12_I_EPLEN * W.n + e] = s.eplen;
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    float js = jsign(k, sg);
+    stf(W, H12_F_Q + NL * leg + k, e, js * s.lg.q[k]);
+    stf(W, H12_F_QD + NL * leg + k, e, js * s.lg.qd[k]);
+    stf(W, H12_F_ACT + NL * leg + k, e, js * s.act[k]);
+    stf(W, H12_F_ACT_PREV + NL * leg + k, e, js * s.act1[k]);
+  }
+  int cm_real = 0;
+#pragma unroll
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+    int qr = leg ? (q ^ 1) : q;
+    stf(W, H12_F_ANCHOR + 8 * leg + 2 * qr, e, s.lg.anc[q][0]);
+    stf(W, H12_F_ANCHOR + 8 * leg + 2 * qr + 1, e, sg * s.lg.anc[q][1]);
+    cm_real |= ((s.lg.cmask >> q) & 1) << qr;
+  }
+  stf(W, H12_F_AIR + leg, e, s.air);
+  stf(W, H12_F_CONTACT + leg, e, s.con);
+  stf(W, H12_F_LAST_AIR + leg, e, s.last_air);
+  stf(W, H12_F_LAST_CONTACT + leg, e, s.last_con);
+  int cm_other = pair_swap_i(cm_real);
+  if (leg == 0) {
+    int pk = 0;
+    for (int g = 0; g < 3; ++g) pk |= (s.lag[g] & 7) << (3 * g);
+    pk |= (s.since_reset & 3) << 9;
+    pk |= (s.is_heading & 1) << 11;
+    pk |= (s.is_standing & 1) << 12;
+    pk |= (cm_real & 0xF) << 13;
+    pk |= (cm_other & 0xF) << 17;
+    W.I[(size_t)H12_I_PACK * W.n + e] = pk;
+  }
+}
+
+// ------------------------------------------------------------------ MDP pieces
+H12_DEV void rng(const KParams& P, uint32_t g, uint32_t lo, uint32_t hi, int stream, int block, uint32_t out[4]) {
+  philox(P.seed_lo, P.seed_hi, g, lo, ((uint32_t)stream << 16) | (uint32_t)block, hi, out);
+}
+
+H12_DEV float wrap_pi(float x) {
+  const float TWO_PI = 6.283185307179586f, PI_F = 3.141592653589793f;
+  float r = fmodf(x, TWO_PI);
+  if (r < 0.f) r += TWO_PI;
+  return r > PI_F ? r - TWO_PI : r;
+}
+
+// UniformVelocityCommand._resample_command (upstream; in-repo twin utils/mdp/commands.py:19-59)
+H12_DEV void cmd_resample(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi) {
+  uint32_t r0[4], r1[4];
+  rng(P, g, lo, hi, ST_CMD, 0, r0);
+  rng(P, g, lo, hi, ST_CMD, 1, r1);
+  s.cmd[0] = uab(r0[0], P.cmd_x0, P.cmd_x1);
+  s.cmd[1] = uab(r0[1], P.cmd_y0, P.cmd_y1);
+  s.cmd[2] = uab(r0[2], P.cmd_w0, P.cmd_w1);
+  s.heading = uab(r0[3], P.cmd_h0, P.cmd_h1);
+  s.is_heading = u01(r1[0]) <= P.rel_head;
+  s.is_standing = u01(r1[1]) <= P.rel_stand;
+  s.cmd_time = P.cmd_T;
+}
+
+// UniformVelocityCommand._update_command (heading control, standing envs)
+H12_DEV void cmd_update(const KParams& P, EnvSt& s) {
+  if (s.is_heading) {
+    float R[3][3];
+    quat_R(s.b.quat, R);
+    float hw = atan2f(R[1][0], R[0][0]);
+    float w = P.head_k * wrap_pi(s.heading - hw);
+    s.cmd[2] = fminf(fmaxf(w, P.cmd_w0), P.cmd_w1);
+  }
+  if (s.is_standing) s.cmd[0] = s.cmd[1] = s.cmd[2] = 0.f;
+}
+
+// _reset_idx: scene reset (delay lags, sensors), reset events, manager resets (cat_env.py:195-248)
+H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi) {
+  uint32_t r0[4], r1[4];
+  rng(P, g, lo, hi, ST_RESET, 0, r0);
+  rng(P, g, lo, hi, ST_RESET, 1, r1);
+  s.b.pos[0] = uab(r0[0], P.rx0, P.rx1);
+  s.b.pos[1] = uab(r0[1], P.ry0, P.ry1);
+  s.b.pos[2] = P.root_z;
+  float yaw = uab(r0[2], P.ryaw0, P.ryaw1);
+  float sy, cy;
+  sincosf(0.5f * yaw, &sy, &cy);
+  s.b.quat[0] = cy; s.b.quat[1] = 0.f; s.b.quat[2] = 0.f; s.b.quat[3] = sy;
+  for (int i = 0; i < 3; ++i) { s.b.vlin[i] = 0.f; s.b.wang[i] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    // reset_joints_by_scale (x1.0) clamped to the soft limits, in the lane frame
+    s.lg.q[k] = fminf(fmaxf(h12m::Q0[k], soft_lo(P, k)), soft_hi(P, k));
+    s.lg.qd[k] = 0.f;
+    s.act[k] = 0.f;
+    s.act1[k] = 0.f;
+  }
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) { s.lg.anc[q][0] = 0.f; s.lg.anc[q][1] = 0.f; }
+  s.lg.cmask = 0;
+  uint32_t span = (uint32_t)(P.max_delay - P.min_delay + 1);
+  s.lag[0] = P.min_delay + (int)(r0[3] % span);
+  s.lag[1] = P.min_delay + (int)(r1[0] % span);
+  s.lag[2] = P.min_delay + (int)(r1[1] % span);
+  s.since_reset = 0;
+  s.air = s.con = s.last_air = s.last_con = 0.f;
+  for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = 0.f;
+  s.eplen = 0;
+  cmd_resample(P, s, g, lo, hi);
+}
+
+// this lane's part of the new observation frame -> LDS row fr (45 floats, real coordinates)
+H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi, float* fr) {
+  const float sg = leg ? -1.f : 1.f;
+  float noise[32];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    uint32_t r[4];
+    rng(P, g, lo, hi, ST_OBS, b, r);
+    for (int a = 0; a < 4; ++a) noise[4 * b + a] = u01(r[a]);
+  }
+  auto nz = [&](int t, float nmax) { return P.corrupt ? (-nmax + 2.f * nmax * noise[t]) : 0.f; };
+  if (leg == 0) {
+    float R[3][3];
+    quat_R(s.b.quat, R);
+    for (int a = 0; a < 3; ++a) fr[a] = s.b.wang[a] + nz(a, P.n_w);
+    for (int a = 0; a < 3; ++a) fr[3 + a] = -R[2][a] + nz(3 + a, P.n_g);
+    for (int a = 0; a < 3; ++a) fr[6 + a] = s.cmd[a];
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    float js = jsign(k, sg);
+    int j = NL * leg + k;
+    fr[9 + j] = js * (s.lg.q[k] - h12m::Q0[k]) + nz(6 + j, P.n_q);
+    fr[21 + j] = js * s.lg.qd[k] + nz(18 + j, P.n_qd);
+    fr[33 + j] = js * s.act[k];
+  }
+}
+
+// cooperative, coalesced write of the block's observation rows: shifted previous row + new frame
+H12_DEV void write_obs_block(const float* obs_prev, float* obs, int e0, int n_rows, const float* lds_frame,
+                             const int* lds_fill, const int* lds_write) {
+  const int total = n_rows * H12_NOBS;
+  const size_t base = (size_t)e0 * H12_NOBS;
+  for (int idx = threadIdx.x; idx < total; idx += BLOCK) {
+    int row = idx / H12_NOBS;
+    int col = idx - row * H12_NOBS;
+    if (!lds_write[row]) continue;
+    // column -> (term, history slot, component): term blocks of 30, 30, 30, 120, 120, 120 floats
+    int off, fo, d;
+    if (col < 90) { int t = col / 30; off = 30 * t; fo = 3 * t; d = 3; }
+    else { int t = (col - 90) / 120; off = 90 + 120 * t; fo = 9 + 12 * t; d = 12; }
+    int rel = col - off;
+    int hh = rel / d;
+    int a = rel - hh * d;
+    float v;
+    if (lds_fill[row] || hh == H12_NHIST - 1) v = lds_frame[row * H12_OBS_FRAME + fo + a];
+    else v = obs_prev[base + idx + d];
+    obs[base + idx] = v;
+  }
+}
+
+// ------------------------------------------------------------------ kernels
+struct StepArgs {
+  const float* actions;
+  const float* obs_prev;
+  float* obs;
+  float* rew;
+  uint8_t* term;
+  uint8_t* trunc;
+  float* log_acc;
+  float* applied_torque;
+  float* foot_force;
+  const uint8_t* reset_mask;
+  const float* q_ref;  // physics-only hook
+  int64_t env_offset;
+  uint32_t lo, hi;
+  int n_substeps;
+};
+
+__global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
+  __shared__ int s_fill[ENVS_PER_BLOCK];
+  __shared__ int s_write[ENVS_PER_BLOCK];
+  const int lane_pair = threadIdx.x >> 1;
+  const int leg = threadIdx.x & 1;
+  const float sg = leg ? -1.f : 1.f;
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e = e0 + lane_pair;
+  const bool active = e < W.n;
+  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
+  const uint32_t g = (uint32_t)(A.env_offset + e);
+  if (active) {
+    EnvSt s;
+    load_env(W, e, leg, s);
+    // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
+    float a_t[NL], a_t1[NL], a_t2[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      a_t[k] = jsign(k, sg) * A.actions[(size_t)e * NJ + NL * leg + k];
+      a_t1[k] = s.act[k];
+      a_t2[k] = s.act1[k];
+      s.act1[k] = s.act[k];
+      s.act[k] = a_t[k];
+    }
+    const int dec = P.decimation;
+    float tau_app[NL], jacc[NL];
+    float fmax_knee = 0.f, fmax_torso = 0.f, fmax_foot = 0.f, flast_foot = 0.f;
+    const float wgt = 1.f / (float)P.inner;
+    for (int st = 0; st < dec; ++st) {
+      float tau[NL];
+      if (P.mode == H12_MODE_ISAACLAB) {
+        // DelayedPDActuator: delayed target = CircularBuffer[lag] with lag clamped to pushes-1
+        int npush = s.since_reset * dec + st + 1;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          int L = min(s.lag[P.dgroup[k]], npush - 1);
+          float a = (L <= st) ? a_t[k] : ((L <= st + dec) ? a_t1[k] : a_t2[k]);
+          float tgt = h12m::Q0[k] + P.action_scale * a;
+          float v = P.kp[k] * (tgt - s.lg.q[k]) + P.kd[k] * (0.f - s.lg.qd[k]);
+          tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          float tgt = h12m::Q0[k] + P.action_scale * a_t[k];
+          float v = P.kp[k] * (tgt - s.lg.q[k]) - P.kd[k] * s.lg.qd[k];
+          tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
+        }
+      }
+      float qd0[NL];
+      for (int k = 0; k < NL; ++k) qd0[k] = s.lg.qd[k];
+      Forces fr = {};
+      for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr, wgt);
+      for (int k = 0; k < NL; ++k) { tau_app[k] = tau[k]; jacc[k] = (s.lg.qd[k] - qd0[k]) / P.dt; }
+      // ContactSensor._update_buffers_impl: air / contact time (threshold 1 N, elapsed = dt)
+      float fn = sqrtf(fr.foot[0] * fr.foot[0] + fr.foot[1] * fr.foot[1] + fr.foot[2] * fr.foot[2]) * wgt;
+      bool is_c = fn > P.cthr;
+      bool first_c = (s.air > 0.f) && is_c;
+      bool first_d = (s.con > 0.f) && !is_c;
+      if (first_c) s.last_air = s.air + P.dt;
+      s.air = is_c ? 0.f : s.air + P.dt;
+      if (first_d) s.last_con = s.con + P.dt;
+      s.con = is_c ? s.con + P.dt : 0.f;
+      flast_foot = fn;
+      if (st >= dec - 3) {  // net_forces_w_history (history_length 3)
+        fmax_foot = fmaxf(fmax_foot, fn);
+        fmax_knee = fmaxf(fmax_knee, sqrtf(fr.knee[0] * fr.knee[0] + fr.knee[1] * fr.knee[1] + fr.knee[2] * fr.knee[2]));
+        fmax_torso = fmaxf(fmax_torso, sqrtf(fr.torso[0] * fr.torso[0] + fr.torso[1] * fr.torso[1] + fr.torso[2] * fr.torso[2]));
+      }
+    }
+    s.eplen += 1;
+    // ---- terminations: time_out, illegal_contact (pair-combined)
+    const bool tout = s.eplen >= P.max_len;
+    int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
+    const int term = ill | pair_swap_i(ill);
+    // ---- rewards on the pre-reset state
+    float R[3][3];
+    quat_R(s.b.quat, R);
+    float ww[3];
+    mv(R, s.b.wang, ww);
+    float cw[3], wxc[3];
+    mv(R, h12m::BASE_COM, cw);
+    cross(ww, cw, wxc);
+    float vcom[3] = {s.b.vlin[0] + wxc[0], s.b.vlin[1] + wxc[1], s.b.vlin[2] + wxc[2]};
+    float yaw = atan2f(R[1][0], R[0][0]);
+    float sy, cy;
+    sincosf(yaw, &sy, &cy);
+    float vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
+    float terms[H12_NREW];
+    float ex = s.cmd[0] - vy0, ey = s.cmd[1] - vy1, ew = s.cmd[2] - ww[2];
+    terms[H12_R_TRACK_LIN_VEL_XY] = expf(-(ex * ex + ey * ey) * P.std2_inv);
+    terms[H12_R_TRACK_ANG_VEL_Z] = expf(-(ew * ew) * P.std2_inv);
+    terms[H12_R_ANG_VEL_XY_L2] = s.b.wang[0] * s.b.wang[0] + s.b.wang[1] * s.b.wang[1];
+    float st_ = 0.f, sa_ = 0.f, sr_ = 0.f, sl_ = 0.f, sd_ = 0.f;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      st_ += tau_app[k] * tau_app[k];
+      sa_ += jacc[k] * jacc[k];
+      float dr = s.act[k] - s.act1[k];
+      sr_ += dr * dr;
+    }
+#pragma unroll
+    for (int k = 4; k < 6; ++k) {  // ankle pitch / roll soft limits (symmetric under the mirror)
+      float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
+      sl_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
+    }
+    sd_ = fabsf(s.lg.q[0] - h12m::Q0[0]) + fabsf(s.lg.q[2] - h12m::Q0[2]);  // hip yaw, hip roll
+    auto psum = [&](float x) {
+      float y = pair_swap(x);
+      return leg ? (y + x) : (x + y);
+    };
+    terms[H12_R_DOF_TORQUES_L2] = psum(st_);
+    terms[H12_R_DOF_ACC_L2] = psum(sa_);
+    terms[H12_R_ACTION_RATE_L2] = psum(sr_);
+    {
+      float con_o = pair_swap(s.con), air_o = pair_swap(s.air);
+      float conL = leg ? con_o : s.con, conR = leg ? s.con : con_o;
+      float airL = leg ? air_o : s.air, airR = leg ? s.air : air_o;
+      int incL = conL > 0.f, incR = conR > 0.f;
+      float mL = incL ? conL : airL, mR = incR ? conR : airR;
+      float r = ((incL + incR) == 1) ? fminf(mL, mR) : 0.f;
+      r = fminf(r, P.air_thr);
+      float cn = sqrtf(s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1]);
+      terms[H12_R_FEET_AIR_TIME] = cn > 0.1f ? r : 0.f;
+    }
+    terms[H12_R_FLAT_ORIENTATION_L2] = R[2][0] * R[2][0] + R[2][1] * R[2][1];
+    terms[H12_R_DOF_POS_LIMITS] = psum(sl_);
+    terms[H12_R_TERMINATION] = term ? 1.f : 0.f;
+    {
+      // feet_slide: |v_xy| of the foot COM (lane frame; the norm is mirror-invariant) where max_h |F| > 1
+      float fs = 0.f;
+      if (fmax_foot > 1.0f) {
+        const float mm[3] = {1.f, sg, 1.f};
+        float Rf[3][3];
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) Rf[i][j] = mm[i] * mm[j] * R[i][j];
+        float vb[3];
+        mtv(R, s.b.vlin, vb);
+        float v6[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
+        for (int i = 0; i < 6; ++i) v6[i] *= s6(i, sg);
+        float csd[NL][2], cbd[NL][6], pAd[NL][6], pd[3] = {0.f, 0.f, 0.f};
+        link_pass1<0>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        link_pass1<1>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        link_pass1<2>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        link_pass1<3>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        link_pass1<4>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        link_pass1<5>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        float vc[3], vw[3];
+        cross(v6, h12m::COM[5], vc);
+        vc[0] += v6[3]; vc[1] += v6[4]; vc[2] += v6[5];
+        mv(Rf, vc, vw);
+        fs = sqrtf(vw[0] * vw[0] + vw[1] * vw[1]);
+      }
+      terms[H12_R_FEET_SLIDE] = psum(fs);
+    }
+    terms[H12_R_JOINT_DEV_HIP] = psum(sd_);
+    float r = 0.f;
+#pragma unroll
+    for (int t = 0; t < H12_NREW; ++t) {
+      float v = terms[t] * P.rew_w[t] * P.step_dt;
+      r += v;
+      s.epsum[t] += v;
+    }
+    const bool reset = term || tout;
+    if (leg == 0) {
+      A.rew[e] = r;
+      A.term[e] = (uint8_t)term;
+      A.trunc[e] = (uint8_t)tout;
+    }
+    if (A.applied_torque)
+      for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau_app[k];
+    if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
+    // ---- episode log: wave-reduced, one atomic per value per wave that saw a reset
+    if (A.log_acc) {
+      const bool mine = reset && leg == 0;
+      if (__ballot(mine)) {
+        float lv[15];
+        for (int t = 0; t < H12_NREW; ++t) lv[t] = mine ? s.epsum[t] : 0.f;
+        lv[12] = mine ? 1.f : 0.f;
+        lv[13] = (mine && tout) ? 1.f : 0.f;
+        lv[14] = (mine && term) ? 1.f : 0.f;
+        for (int t = 0; t < 15; ++t) {
+          float x = lv[t];
+          for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+          lv[t] = x;
+        }
+        if ((threadIdx.x & 63) == 0)
+          for (int t = 0; t < 15; ++t) atomicAdd(&A.log_acc[t], lv[t]);
+      }
+    }
+    if (reset) env_reset(P, s, leg, g, A.lo, A.hi);
+    else s.since_reset = min(s.since_reset + 1, 2);
+    // ---- CommandTerm.compute(step_dt)
+    s.cmd_time -= P.step_dt;
+    if (s.cmd_time <= 0.f) cmd_resample(P, s, g, A.lo, A.hi);
+    cmd_update(P, s);
+    // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
+    obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
+    if (leg == 0) {
+      s_fill[lane_pair] = reset ? 1 : 0;
+      s_write[lane_pair] = 1;
+    }
+    store_env(W, e, leg, s);
+  }
+  __syncthreads();
+  if (n_rows > 0) write_obs_block(A.obs_prev, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+}
+
+__global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, StepArgs A) {
+  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
+  __shared__ int s_fill[ENVS_PER_BLOCK];
+  __shared__ int s_write[ENVS_PER_BLOCK];
+  const int lane_pair = threadIdx.x >> 1;
+  const int leg = threadIdx.x & 1;
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e = e0 + lane_pair;
+  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
+  if (leg == 0) { s_write[lane_pair] = 0; s_fill[lane_pair] = 1; }
+  __syncthreads();
+  if (e < W.n && (!A.reset_mask || A.reset_mask[e])) {
+    const uint32_t g = (uint32_t)(A.env_offset + e);
+    EnvSt s;
+    load_env(W, e, leg, s);
+    env_reset(P, s, leg, g, A.lo, A.hi);
+    obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
+    if (leg == 0) s_write[lane_pair] = 1;
+    store_env(W, e, leg, s);
+  }
+  __syncthreads();
+  if (n_rows > 0) write_obs_block(A.obs, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+}
+
+// parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
+__global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, StepArgs A) {
+  const int lane_pair = threadIdx.x >> 1;
+  const int leg = threadIdx.x & 1;
+  const float sg = leg ? -1.f : 1.f;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + lane_pair;
+  if (e >= W.n) return;
+  EnvSt s;
+  load_env(W, e, leg, s);
+  float qr[NL];
+  for (int k = 0; k < NL; ++k) qr[k] = jsign(k, sg) * A.q_ref[(size_t)e * NJ + NL * leg + k];
+  const float wgt = 1.f / (float)P.inner;
+  for (int st = 0; st < A.n_substeps; ++st) {
+    float tau[NL];
+    for (int k = 0; k < NL; ++k) {
+      float v = P.kp[k] * (qr[k] - s.lg.q[k]) - P.kd[k] * s.lg.qd[k];
+      tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
+    }
+    Forces fr = {};
+    for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr, wgt);
+  }
+  store_env(W, e, leg, s);
+}
+
+// ------------------------------------------------------------------ host side
+struct Handle {
+  KParams P;
+  Workspace W;
+  bool own;
+  int device;
+  int64_t env_offset;
+  uint64_t reset_calls;
+  double flops_per_env;
+};
+
+bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
+
+// the kernel compiles the H1-2 model in (h12_model_gen.h); refuse any other model
+int check_model(const h12env_model* m) {
+  for (int leg = 0; leg < 2; ++leg)
+    for (int k = 0; k < NL; ++k) {
+      int j = NL * leg + k;
+      int want_parent = k == 0 ? -1 : j - 1;
+      if (m->parent[j] != want_parent || m->axis[j] != AX[k])
+        return set_err(H12_E_ARG, "model joint %d: tree/axis differ from the compiled H1-2 model", j);
+      float my = leg ? -1.f : 1.f;
+      float js = AX[k] == 1 ? 1.f : my;
+      bool ok = close(m->joint_pos[j][0], h12m::R[k][0]) && close(m->joint_pos[j][1], my * h12m::R[k][1]) &&
+                close(m->joint_pos[j][2], h12m::R[k][2]) && close(m->link_mass[j], h12m::M[k]) &&
+                close(m->link_com[j][0], h12m::COM[k][0]) && close(m->link_com[j][1], my * h12m::COM[k][1]) &&
+                close(m->link_com[j][2], h12m::COM[k][2]) && close(m->armature[j], h12m::ARM[k]) &&
+                close(m->damping[j], h12m::DAMP[k]) && close(m->q_default[j], js * h12m::Q0[k]) &&
+                close(fminf(js * m->q_lower[j], js * m->q_upper[j]), h12m::QLO[k]) &&
+                close(fmaxf(js * m->q_lower[j], js * m->q_upper[j]), h12m::QHI[k]);
+      if (!ok) return set_err(H12_E_ARG, "model joint %d differs from the compiled H1-2 model (regenerate h12_model_gen.h)", j);
+    }
+  if (!close(m->base_mass, h12m::BASE_M) || !close(m->base_com[0], h12m::BASE_COM[0]) ||
+      !close(m->base_com[2], h12m::BASE_COM[2]) || !close(m->foot_radius, h12m::FOOT_R) ||
+      !close(m->knee_radius, h12m::KNEE_R))
+    return set_err(H12_E_ARG, "base / contact geometry differs from the compiled H1-2 model");
+  return 0;
+}
+
+int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
+  memset(&P, 0, sizeof P);
+  if (int rc = check_model(m)) return rc;
+  if (c->decimation < 1 || c->inner_steps < 1 || !(c->physics_dt > 0)) return set_err(H12_E_ARG, "bad decimation/inner_steps/dt");
+  if (c->mode != H12_MODE_ISAACLAB && c->mode != H12_MODE_MUJOCO) return set_err(H12_E_ARG, "bad mode %d", c->mode);
+  if (c->min_delay < 0 || c->max_delay < c->min_delay || c->max_delay > 7 || c->max_delay > 2 * c->decimation)
+    return set_err(H12_E_ARG, "delay range [%d,%d] unsupported", c->min_delay, c->max_delay);
+  for (int k = 0; k < NL; ++k) {
+    if (c->delay_group[k] != c->delay_group[NL + k] || c->delay_group[k] < 0 || c->delay_group[k] > 2)
+      return set_err(H12_E_ARG, "delay groups must be leg-symmetric and in 0..2");
+    if (c->kp[k] != c->kp[NL + k] || c->kd[k] != c->kd[NL + k] || c->effort_limit[k] != c->effort_limit[NL + k])
+      return set_err(H12_E_ARG, "gains must be leg-symmetric");
+  }
+  if (!(c->friction_k > 0)) return set_err(H12_E_ARG, "friction_k must be > 0");
+  const bool mj = c->mode == H12_MODE_MUJOCO;
+  for (int k = 0; k < NL; ++k) {
+    P.kp[k] = c->kp[k];
+    P.kd[k] = c->kd[k];
+    P.elim[k] = mj ? m->mj_frc_limit[k] : c->effort_limit[k];
+    P.dimpl[k] = mj ? m->damping[k] : 0.f;
+    P.dgroup[k] = c->delay_group[k];
+  }
+  P.g = m->gravity;
+  P.mode = c->mode;
+  P.fix_base = c->fix_base;
+  P.decimation = c->decimation;
+  P.inner = c->inner_steps;
+  P.max_len = c->max_episode_length;
+  P.min_delay = c->min_delay;
+  P.max_delay = c->max_delay;
+  P.use_fl = c->use_frictionloss;
+  P.corrupt = c->enable_corruption;
+  P.ill_knees = c->illegal_contact_knees;
+  P.ill_torso = c->illegal_contact_torso;
+  P.dt = c->physics_dt;
+  P.h = c->physics_dt / (float)c->inner_steps;
+  P.step_dt = c->physics_dt * (float)c->decimation;
+  P.action_scale = c->action_scale;
+  P.soft_f = c->soft_limit_factor;
+  P.ck = c->contact_k; P.cc = c->contact_c; P.fk = c->friction_k; P.fc = c->friction_c;
+  P.mus = c->mu_static; P.mud = c->mu_dynamic; P.lk = c->limit_k; P.lc = c->limit_c;
+  P.cthr = c->contact_threshold;
+  P.cmd_T = c->cmd_resample_time;
+  P.cmd_x0 = c->cmd_lin_x[0]; P.cmd_x1 = c->cmd_lin_x[1];
+  P.cmd_y0 = c->cmd_lin_y[0]; P.cmd_y1 = c->cmd_lin_y[1];
+  P.cmd_w0 = c->cmd_ang_z[0]; P.cmd_w1 = c->cmd_ang_z[1];
+  P.cmd_h0 = c->cmd_heading[0]; P.cmd_h1 = c->cmd_heading[1];
+  P.rel_stand = c->rel_standing_envs; P.rel_head = c->rel_heading_envs; P.head_k = c->heading_stiffness;
+  P.rx0 = c->reset_x[0]; P.rx1 = c->reset_x[1]; P.ry0 = c->reset_y[0]; P.ry1 = c->reset_y[1];
+  P.ryaw0 = c->reset_yaw[0]; P.ryaw1 = c->reset_yaw[1];
+  P.root_z = m->root_height;
+  P.n_w = c->noise_ang_vel; P.n_g = c->noise_gravity; P.n_q = c->noise_joint_pos; P.n_qd = c->noise_joint_vel;
+  for (int t = 0; t < H12_NREW; ++t) P.rew_w[t] = c->rew_w[t];
+  P.std2_inv = 1.f / (c->track_std * c->track_std);
+  P.air_thr = c->air_time_threshold;
+  P.seed_lo = (uint32_t)c->seed;
+  P.seed_hi = (uint32_t)(c->seed >> 32);
+  return 0;
+}
+
+int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
+
+}  // namespace
+
+// ================================================================== C-ABI
+extern "C" {
+
+int h12env_abi_version(void) { return H12ENV_ABI_VERSION; }
+const char* h12env_last_error(void) { return g_err; }
+
+int h12env_config_default(h12env_config* c) {
+  if (!c) return set_err(H12_E_ARG, "null config");
+  memset(c, 0, sizeof *c);
+  c->abi_version = H12ENV_ABI_VERSION;
+  c->mode = H12_MODE_ISAACLAB;
+  c->physics_dt = 0.005f;
+  c->decimation = 4;
+  c->inner_steps = 2;
+  c->max_episode_length = 1000;
+  c->action_scale = 0.5f;
+  const float kp[6] = {200, 200, 200, 300, 40, 40}, kd[6] = {2.5f, 2.5f, 2.5f, 4, 2, 2};
+  const float E[6] = {220, 220, 220, 360, 45, 45};
+  const int grp[6] = {0, 0, 0, 1, 2, 2};
+  for (int j = 0; j < H12_NJ; ++j) {
+    c->kp[j] = kp[j % 6]; c->kd[j] = kd[j % 6]; c->effort_limit[j] = E[j % 6]; c->delay_group[j] = grp[j % 6];
+  }
+  c->min_delay = 0; c->max_delay = 5;
+  c->contact_k = 3e4f; c->contact_c = 100.f; c->friction_k = 3e4f; c->friction_c = 100.f;
+  c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1000.f; c->limit_c = 2.f; c->contact_threshold = 1.f;
+  c->cmd_resample_time = 10.f;
+  c->cmd_lin_x[0] = 0.f; c->cmd_lin_x[1] = 1.f; c->cmd_lin_y[0] = -0.5f; c->cmd_lin_y[1] = 0.5f;
+  c->cmd_ang_z[0] = -1.f; c->cmd_ang_z[1] = 1.f;
+  c->cmd_heading[0] = -3.14159265f; c->cmd_heading[1] = 3.14159265f;
+  c->rel_standing_envs = 0.02f; c->rel_heading_envs = 1.f; c->heading_stiffness = 0.5f;
+  c->reset_x[0] = -0.5f; c->reset_x[1] = 0.5f; c->reset_y[0] = -0.5f; c->reset_y[1] = 0.5f;
+  c->reset_yaw[0] = -3.14f; c->reset_yaw[1] = 3.14f;
+  c->enable_corruption = 1;
+  c->noise_ang_vel = 0.2f; c->noise_gravity = 0.05f; c->noise_joint_pos = 0.01f; c->noise_joint_vel = 1.5f;
+  const float w[H12_NREW] = {1.0f, 1.0f, -0.05f, -2e-6f, -1e-7f, -0.005f, 0.75f, -1.0f, -1.0f, -200.f, -0.25f, -0.2f};
+  for (int t = 0; t < H12_NREW; ++t) c->rew_w[t] = w[t];
+  c->track_std = 0.5f; c->air_time_threshold = 0.4f; c->soft_limit_factor = 0.9f;
+  c->illegal_contact_knees = 1; c->illegal_contact_torso = 1;
+  c->seed = 42;
+  return 0;
+}
+
+size_t h12env_state_bytes(int n_envs) {
+  if (n_envs <= 0) return 0;
+  return (size_t)(H12_NF_FLOAT + H12_NF_INT) * sizeof(float) * (size_t)n_envs;
+}
+
+int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_envs, int64_t env_offset, int device,
+                  void* state_dev, h12env** out) {
+  if (!model || !cfg || !out) return set_err(H12_E_ARG, "null argument");
+  *out = nullptr;
+  if (n_envs <= 0) return set_err(H12_E_ARG, "n_envs must be > 0 (got %d)", n_envs);
+  if (env_offset < 0 || env_offset + (int64_t)n_envs > (int64_t)0xFFFFFFFFll)
+    return set_err(H12_E_ARG, "global env ids must fit in 32 bits");
+  if (cfg->abi_version != H12ENV_ABI_VERSION)
+    return set_err(H12_E_ARG, "config abi %d != %d", cfg->abi_version, H12ENV_ABI_VERSION);
+  Handle* h = new (std::nothrow) Handle();
+  if (!h) return set_err(H12_E_ALLOC, "host allocation failed");
+  if (int rc = build_params(model, cfg, h->P)) { delete h; return rc; }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { delete h; return set_err(H12_E_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); }
+  size_t bytes = h12env_state_bytes(n_envs);
+  h->own = state_dev == nullptr;
+  if (h->own) {
+    e = hipMalloc(&state_dev, bytes);
+    if (e != hipSuccess) { delete h; return set_err(H12_E_ALLOC, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e)); }
+    e = hipMemset(state_dev, 0, bytes);
+    if (e != hipSuccess) { (void)hipFree(state_dev); delete h; return set_err(H12_E_HIP, "hipMemset: %s", hipGetErrorString(e)); }
+  }
+  h->W.F = (float*)state_dev;
+  h->W.I = (int32_t*)((float*)state_dev + (size_t)H12_NF_FLOAT * n_envs);
+  h->W.n = n_envs;
+  h->device = device;
+  h->env_offset = env_offset;
+  h->reset_calls = 0;
+  // counted algorithmic FLOPs per env step (DESIGN.md "Roofline"): per inner step and leg lane
+  // ~2.9k (pass 1 0.6k, contacts 0.35k, pass 2 1.5k, pass 3 0.25k, integration 0.1k), base combine +
+  // 6x6 solve ~0.3k per lane; MDP (rewards, resets, commands, obs, RNG) ~3k per env
+  h->flops_per_env = (double)cfg->decimation * cfg->inner_steps * 2.0 * (2900.0 + 300.0) + 3000.0;
+  *out = (h12env*)h;
+  return 0;
+}
+
+void h12env_destroy(h12env* hh) {
+  Handle* h = (Handle*)hh;
+  if (!h) return;
+  if (h->own && h->W.F) (void)hipFree(h->W.F);
+  delete h;
+}
+
+int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!obs) return set_err(H12_E_ARG, "obs is required");
+  StepArgs A = {};
+  A.obs = obs;
+  A.reset_mask = mask;
+  A.env_offset = h->env_offset;
+  A.lo = (uint32_t)h->reset_calls;
+  A.hi = 0xFFFFFFFFu;
+  h->reset_calls++;
+  hipLaunchKernelGGL(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h12env_step_out* out,
+                int64_t step_index, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!actions || !obs_prev || !out || !out->obs || !out->rew || !out->terminated || !out->truncated)
+    return set_err(H12_E_ARG, "actions, obs_prev, obs, rew, terminated, truncated are required");
+  if (step_index < 1) return set_err(H12_E_ARG, "step_index must be >= 1 (got %lld)", (long long)step_index);
+  StepArgs A = {};
+  A.actions = actions;
+  A.obs_prev = obs_prev;
+  A.obs = out->obs;
+  A.rew = out->rew;
+  A.term = out->terminated;
+  A.trunc = out->truncated;
+  A.log_acc = out->log_acc;
+  A.applied_torque = out->applied_torque;
+  A.foot_force = out->foot_force;
+  A.env_offset = h->env_offset;
+  A.lo = (uint32_t)step_index;
+  A.hi = (uint32_t)((uint64_t)step_index >> 32);
+  hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_step_physics(h12env* hh, const float* q_ref, int n_substeps, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!q_ref || n_substeps < 0) return set_err(H12_E_ARG, "q_ref required, n_substeps >= 0");
+  StepArgs A = {};
+  A.q_ref = q_ref;
+  A.n_substeps = n_substeps;
+  hipLaunchKernelGGL(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+void* h12env_field_ptr(h12env* hh, int is_int, int field) {
+  Handle* h = (Handle*)hh;
+  if (!h) { set_err(H12_E_ARG, "null handle"); return nullptr; }
+  if (is_int) {
+    if (field < 0 || field >= H12_NF_INT) { set_err(H12_E_ARG, "int field %d out of range", field); return nullptr; }
+    return h->W.I + (size_t)field * h->W.n;
+  }
+  if (field < 0 || field >= H12_NF_FLOAT) { set_err(H12_E_ARG, "float field %d out of range", field); return nullptr; }
+  return h->W.F + (size_t)field * h->W.n;
+}
+
+int h12env_num_envs(const h12env* hh) { return hh ? ((const Handle*)hh)->W.n : -1; }
+
+int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_env) {
+  const Handle* h = (const Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  // compulsory HBM bytes per env step: state read + write, actions, obs (9 old frames read, 10
+  // written), reward / terminated / truncated
+  double state = (double)(H12_NF_FLOAT + H12_NF_INT) * 4.0 * 2.0;
+  double obs = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_NOBS * 4.0;
+  double io = (double)H12_NJ * 4.0 + 4.0 + 2.0;
+  if (bytes_per_env) *bytes_per_env = state + obs + io;
+  if (flops_per_env) *flops_per_env = h->flops_per_env;
+  return 0;
+}
+
+}  // extern "C"

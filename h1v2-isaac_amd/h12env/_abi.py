@@ -1,0 +1,206 @@
+"""ctypes mirror of include/h12env.h (the C-ABI of libh12env.so).
+
+Kept field-for-field identical to the header; tests/test_abi.py checks struct sizes against
+the library's own sizeof via h12env_state_bytes / h12env_config_default round-trips.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+NJ = 12
+NHIST = 10
+OBS_FRAME = 45
+NOBS = OBS_FRAME * NHIST
+NFOOT_PTS = 4
+NREW = 12
+NLOG = 16
+ABI_VERSION = 1
+
+MODE_ISAACLAB = 0
+MODE_MUJOCO = 1
+
+# state field offsets (H12_F_* / H12_I_*)
+F = dict(POS=(0, 3), QUAT=(3, 4), VLIN=(7, 3), WANG=(10, 3), Q=(13, 12), QD=(25, 12), ACT=(37, 12),
+         ACT_PREV=(49, 12), CMD=(61, 3), HEADING=(64, 1), CMD_TIME=(65, 1), AIR=(66, 2), CONTACT=(68, 2),
+         LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16))
+NF_FLOAT = 102
+I = dict(EPLEN=(0, 1), PACK=(1, 1))
+NF_INT = 2
+
+REWARD_TERMS = [
+    "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "ang_vel_xy_l2", "dof_torques_l2", "dof_acc_l2",
+    "action_rate_l2", "feet_air_time", "flat_orientation_l2", "dof_pos_limits", "termination_penalty",
+    "feet_slide", "joint_deviation_hip",
+]
+
+f32 = C.c_float
+i32 = C.c_int32
+
+
+class H12Model(C.Structure):
+    _fields_ = [
+        ("version", i32),
+        ("parent", i32 * NJ),
+        ("axis", i32 * NJ),
+        ("joint_pos", (f32 * 3) * NJ),
+        ("link_mass", f32 * NJ),
+        ("link_com", (f32 * 3) * NJ),
+        ("link_inertia", (f32 * 6) * NJ),
+        ("base_mass", f32),
+        ("base_com", f32 * 3),
+        ("base_inertia", f32 * 6),
+        ("q_lower", f32 * NJ),
+        ("q_upper", f32 * NJ),
+        ("armature", f32 * NJ),
+        ("damping", f32 * NJ),
+        ("frictionloss", f32 * NJ),
+        ("mj_frc_limit", f32 * NJ),
+        ("q_default", f32 * NJ),
+        ("root_height", f32),
+        ("foot_pts", (f32 * 3) * NFOOT_PTS),
+        ("foot_radius", f32),
+        ("knee_p0", f32 * 3),
+        ("knee_p1", f32 * 3),
+        ("knee_radius", f32),
+        ("torso_center", f32 * 3),
+        ("torso_half", f32 * 3),
+        ("gravity", f32),
+    ]
+
+
+class H12Config(C.Structure):
+    _fields_ = [
+        ("abi_version", i32),
+        ("mode", i32),
+        ("physics_dt", f32),
+        ("decimation", i32),
+        ("inner_steps", i32),
+        ("max_episode_length", i32),
+        ("action_scale", f32),
+        ("kp", f32 * NJ),
+        ("kd", f32 * NJ),
+        ("effort_limit", f32 * NJ),
+        ("delay_group", i32 * NJ),
+        ("min_delay", i32),
+        ("max_delay", i32),
+        ("fix_base", i32),
+        ("use_frictionloss", i32),
+        ("contact_k", f32),
+        ("contact_c", f32),
+        ("mu_static", f32),
+        ("mu_dynamic", f32),
+        ("friction_k", f32),
+        ("friction_c", f32),
+        ("limit_k", f32),
+        ("limit_c", f32),
+        ("contact_threshold", f32),
+        ("cmd_resample_time", f32),
+        ("cmd_lin_x", f32 * 2),
+        ("cmd_lin_y", f32 * 2),
+        ("cmd_ang_z", f32 * 2),
+        ("cmd_heading", f32 * 2),
+        ("rel_standing_envs", f32),
+        ("rel_heading_envs", f32),
+        ("heading_stiffness", f32),
+        ("reset_x", f32 * 2),
+        ("reset_y", f32 * 2),
+        ("reset_yaw", f32 * 2),
+        ("enable_corruption", i32),
+        ("noise_ang_vel", f32),
+        ("noise_gravity", f32),
+        ("noise_joint_pos", f32),
+        ("noise_joint_vel", f32),
+        ("rew_w", f32 * NREW),
+        ("track_std", f32),
+        ("air_time_threshold", f32),
+        ("soft_limit_factor", f32),
+        ("illegal_contact_knees", i32),
+        ("illegal_contact_torso", i32),
+        ("seed", C.c_uint64),
+    ]
+
+
+class H12StepOut(C.Structure):
+    _fields_ = [
+        ("obs", C.c_void_p),
+        ("rew", C.c_void_p),
+        ("terminated", C.c_void_p),
+        ("truncated", C.c_void_p),
+        ("log_acc", C.c_void_p),
+        ("applied_torque", C.c_void_p),
+        ("foot_force", C.c_void_p),
+    ]
+
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libh12env.so"
+
+_lib = None
+
+
+class H12EnvError(RuntimeError):
+    pass
+
+
+def load_library(path: str | os.PathLike | None = None):
+    """Load libh12env.so (built in-tree by __graft_entry__.build()).  Fails loudly: there is no
+    CPU fallback for the product path."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise H12EnvError(f"HIP extension {p} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    # torch's bundled libamdhip64.so.7 must be the one the library binds to (same soname):
+    # importing torch first guarantees it is already resident in the process.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is always present in this image
+        pass
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    vp = C.c_void_p
+    lib.h12env_config_default.argtypes = [C.POINTER(H12Config)]
+    lib.h12env_config_default.restype = C.c_int
+    lib.h12env_state_bytes.argtypes = [C.c_int]
+    lib.h12env_state_bytes.restype = C.c_size_t
+    lib.h12env_create.argtypes = [C.POINTER(H12Model), C.POINTER(H12Config), C.c_int, C.c_int64, C.c_int, vp,
+                                  C.POINTER(vp)]
+    lib.h12env_create.restype = C.c_int
+    lib.h12env_destroy.argtypes = [vp]
+    lib.h12env_destroy.restype = None
+    lib.h12env_reset.argtypes = [vp, vp, vp, vp]
+    lib.h12env_reset.restype = C.c_int
+    lib.h12env_step.argtypes = [vp, vp, vp, C.POINTER(H12StepOut), C.c_int64, vp]
+    lib.h12env_step.restype = C.c_int
+    lib.h12env_step_physics.argtypes = [vp, vp, C.c_int, vp]
+    lib.h12env_step_physics.restype = C.c_int
+    lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
+    lib.h12env_field_ptr.restype = vp
+    lib.h12env_num_envs.argtypes = [vp]
+    lib.h12env_num_envs.restype = C.c_int
+    lib.h12env_step_cost.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.h12env_step_cost.restype = C.c_int
+    lib.h12env_last_error.argtypes = []
+    lib.h12env_last_error.restype = C.c_char_p
+    lib.h12env_abi_version.argtypes = []
+    lib.h12env_abi_version.restype = C.c_int
+    if lib.h12env_abi_version() != ABI_VERSION:
+        raise H12EnvError(f"libh12env ABI {lib.h12env_abi_version()} != python mirror {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(lib, rc: int, what: str):
+    if rc != 0:
+        msg = lib.h12env_last_error()
+        raise H12EnvError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+EXPORTED_SYMBOLS = [
+    "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
+    "h12env_step", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
+    "h12env_last_error", "h12env_abi_version",
+]

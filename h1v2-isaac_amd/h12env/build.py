@@ -1,0 +1,56 @@
+"""Build libh12env.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m h12env.build            # from h1v2-isaac_amd/
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+SRC_ROOT = PKG.parent
+REPO = SRC_ROOT.parent
+CSRC = SRC_ROOT / "csrc"
+OUT = PKG / "libh12env.so"
+ARCH = os.environ.get("H12_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found (ROCm is required to build libh12env.so)")
+
+
+def sources():
+    return [CSRC / "h12env.hip", CSRC / "h12_math.h", CSRC / "h12_model_gen.h", REPO / "include" / "h12env.h"]
+
+
+def needs_build() -> bool:
+    if not OUT.exists():
+        return True
+    t = OUT.stat().st_mtime
+    return any(s.stat().st_mtime > t for s in sources())
+
+
+def build(force: bool = False, verbose: bool = True, extra_flags: list[str] | None = None) -> Path:
+    # regenerate the constexpr model header from the committed JSON (pure data)
+    subprocess.run([sys.executable, str(REPO / "tools" / "gen_model_header.py")], check=True,
+                   stdout=subprocess.DEVNULL)
+    if not force and not needs_build():
+        return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-unused-function", "-o", str(OUT), str(CSRC / "h12env.hip")]
+    if extra_flags:
+        cmd += extra_flags
+    if verbose:
+        print("[h12env.build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,314 @@
+"""Configuration tree of `Isaac-Velocity-Flat-H12_12dof-v0`, restated as plain dataclasses.
+
+Attribute paths mirror the IsaacLab cfg objects the reference composes, so scripts that poke at
+`env_cfg.scene.num_envs`, `env_cfg.seed`, `env_cfg.sim.device`, `env_cfg.rewards.<term>.weight`,
+`env_cfg.commands.base_velocity.ranges.lin_vel_x` ... keep working.  Values are the merged Flat
+config:
+
+  - sim / decimation / episode: velocity_env_cfg.py:299-315 (dt 0.005, decimation 4, 20 s)
+  - actions: velocity_env_cfg.py:111 (JointPositionAction, scale 0.5, default offset)
+  - actuators: packages/biped_assets/biped_assets/robots/h12.py:58-112 (DelayedPD, Kp/Kd/E, 0-5 delay)
+  - commands: velocity_env_cfg.py:90-104 + flat_env_cfg.py:46-48
+  - observations: velocity_env_cfg.py:124-132, flat_env_cfg.py:25-27 (no lin vel, history 10, noise on)
+  - events: rough_env_cfg.py:140-155 (x,y +-0.5, yaw +-3.14, joints x1.0, no push, no mass)
+  - rewards: rough_env_cfg.py:82-125, 174-183 + flat_env_cfg.py:35-44
+  - terminations: velocity_env_cfg.py:264-268 + rough_env_cfg.py:158-172
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+
+from ._abi import ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NJ, NREW, REWARD_TERMS, H12Config
+from .model import DEFAULT_JOINT_POS
+
+
+@dataclass
+class SimCfg:
+    dt: float = 0.005
+    device: str = "cuda:0"
+    render_interval: int = 4
+    # contact / integration parameters of the build's penalty model (DESIGN.md "Physics model")
+    inner_steps: int = 2
+    contact_k: float = 3.0e4
+    contact_c: float = 100.0
+    friction_k: float = 3.0e4
+    friction_c: float = 100.0
+    limit_k: float = 1.0e3
+    limit_c: float = 2.0
+    static_friction: float = 0.8   # randomize_rigid_body_material startup (velocity_env_cfg.py:153-163)
+    dynamic_friction: float = 0.6
+
+
+@dataclass
+class SceneCfg:
+    num_envs: int = 4096
+    env_spacing: float = 2.5
+    lazy_sensor_update: bool = True
+
+
+@dataclass
+class ActuatorGroupCfg:
+    joint_names_expr: list
+    effort_limit: float
+    stiffness: float
+    damping: float
+    armature: float = 0.01
+    friction: float = 0.0
+    min_delay: int = 0
+    max_delay: int = 5
+
+
+@dataclass
+class RobotCfg:
+    init_pos: tuple = (0.0, 0.0, 1.05)
+    joint_pos: tuple = tuple(DEFAULT_JOINT_POS)
+    soft_joint_pos_limit_factor: float = 0.9
+    actuators: dict = field(default_factory=lambda: {
+        "legs": ActuatorGroupCfg([".*_hip_yaw_joint", ".*_hip_roll_joint", ".*_hip_pitch_joint"], 220.0, 200.0, 2.5),
+        "knees": ActuatorGroupCfg([".*_knee_joint"], 360.0, 300.0, 4.0),
+        "feet": ActuatorGroupCfg([".*_ankle_pitch_joint", ".*_ankle_roll_joint"], 45.0, 40.0, 2.0),
+    })
+
+
+@dataclass
+class JointPositionActionCfg:
+    asset_name: str = "robot"
+    joint_names: tuple = (".*",)
+    scale: float = 0.5
+    use_default_offset: bool = True
+
+
+@dataclass
+class ActionsCfg:
+    joint_pos: JointPositionActionCfg = field(default_factory=JointPositionActionCfg)
+
+
+@dataclass
+class Ranges:
+    lin_vel_x: tuple = (0.0, 1.0)
+    lin_vel_y: tuple = (-0.5, 0.5)
+    ang_vel_z: tuple = (-1.0, 1.0)
+    heading: tuple = (-math.pi, math.pi)
+
+
+@dataclass
+class UniformVelocityCommandCfg:
+    asset_name: str = "robot"
+    resampling_time_range: tuple = (10.0, 10.0)
+    rel_standing_envs: float = 0.02
+    rel_heading_envs: float = 1.0
+    heading_command: bool = True
+    heading_control_stiffness: float = 0.5
+    debug_vis: bool = False
+    ranges: Ranges = field(default_factory=Ranges)
+
+
+@dataclass
+class CommandsCfg:
+    base_velocity: UniformVelocityCommandCfg = field(default_factory=UniformVelocityCommandCfg)
+
+
+@dataclass
+class Unoise:
+    n_min: float
+    n_max: float
+
+
+@dataclass
+class PolicyObsCfg:
+    enable_corruption: bool = True
+    concatenate_terms: bool = True
+    history_length: int = 10
+    # term order preserved (velocity_env_cfg.py:124-132; base_lin_vel and height_scan removed for Flat)
+    base_ang_vel: Unoise = field(default_factory=lambda: Unoise(-0.2, 0.2))
+    projected_gravity: Unoise = field(default_factory=lambda: Unoise(-0.05, 0.05))
+    velocity_commands: None = None
+    joint_pos: Unoise = field(default_factory=lambda: Unoise(-0.01, 0.01))
+    joint_vel: Unoise = field(default_factory=lambda: Unoise(-1.5, 1.5))
+    actions: None = None
+
+
+@dataclass
+class ObservationsCfg:
+    policy: PolicyObsCfg = field(default_factory=PolicyObsCfg)
+
+
+@dataclass
+class RewTerm:
+    weight: float
+    params: dict = field(default_factory=dict)
+
+
+def _rewards():
+    return {
+        "track_lin_vel_xy_exp": RewTerm(1.0, {"command_name": "base_velocity", "std": 0.5}),
+        "track_ang_vel_z_exp": RewTerm(1.0, {"command_name": "base_velocity", "std": 0.5}),
+        "ang_vel_xy_l2": RewTerm(-0.05),
+        "dof_torques_l2": RewTerm(-2.0e-6),
+        "dof_acc_l2": RewTerm(-1.0e-7),
+        "action_rate_l2": RewTerm(-0.005),
+        "feet_air_time": RewTerm(0.75, {"command_name": "base_velocity", "threshold": 0.4}),
+        "flat_orientation_l2": RewTerm(-1.0),
+        "dof_pos_limits": RewTerm(-1.0),
+        "termination_penalty": RewTerm(-200.0),
+        "feet_slide": RewTerm(-0.25),
+        "joint_deviation_hip": RewTerm(-0.2),
+    }
+
+
+class RewardsCfg:
+    """Attribute-access container keeping RewardManager term order (REWARD_TERMS)."""
+
+    def __init__(self, terms=None):
+        object.__setattr__(self, "_terms", terms or _rewards())
+
+    def __getattr__(self, name):
+        try:
+            return self._terms[name]
+        except KeyError as e:
+            raise AttributeError(name) from e
+
+    def __setattr__(self, name, value):
+        if name not in self._terms:
+            raise AttributeError(f"unknown reward term {name!r} (the HIP kernel implements {REWARD_TERMS})")
+        self._terms[name] = value
+
+    def items(self):
+        return [(k, self._terms[k]) for k in REWARD_TERMS]
+
+    def to_dict(self):
+        return {k: {"weight": v.weight, "params": dict(v.params)} for k, v in self.items()}
+
+
+@dataclass
+class TerminationsCfg:
+    time_out: bool = True
+    base_contact_threshold: float = 1.0
+    # bodies of the illegal-contact list that carry colliders in the USD's source URDF
+    base_contact_knees: bool = True
+    base_contact_torso: bool = True
+
+
+@dataclass
+class EventsCfg:
+    reset_base_pose_range: dict = field(default_factory=lambda: {"x": (-0.5, 0.5), "y": (-0.5, 0.5), "yaw": (-3.14, 3.14)})
+    reset_joints_position_range: tuple = (1.0, 1.0)
+    push_robot: None = None
+    add_base_mass: None = None
+
+
+@dataclass
+class H12FlatEnvCfg:
+    """Merged cfg of `Isaac-Velocity-Flat-H12_12dof-v0` (H12_12dof_FlatEnvCfg, flat_env_cfg.py:13-48)."""
+
+    seed: int | None = 42
+    decimation: int = 4
+    episode_length_s: float = 20.0
+    mode: int = MODE_ISAACLAB
+    sim: SimCfg = field(default_factory=SimCfg)
+    scene: SceneCfg = field(default_factory=SceneCfg)
+    robot: RobotCfg = field(default_factory=RobotCfg)
+    actions: ActionsCfg = field(default_factory=ActionsCfg)
+    commands: CommandsCfg = field(default_factory=CommandsCfg)
+    observations: ObservationsCfg = field(default_factory=ObservationsCfg)
+    rewards: RewardsCfg = field(default_factory=RewardsCfg)
+    terminations: TerminationsCfg = field(default_factory=TerminationsCfg)
+    events: EventsCfg = field(default_factory=EventsCfg)
+    fix_base: bool = False
+
+    @property
+    def step_dt(self) -> float:
+        return self.sim.dt * self.decimation
+
+    @property
+    def max_episode_length(self) -> int:
+        return math.ceil(self.episode_length_s / self.step_dt)
+
+    def to_c(self) -> H12Config:
+        from .model import joint_names
+
+        names = joint_names()
+        c = H12Config()
+        c.abi_version = ABI_VERSION
+        c.mode = self.mode
+        c.physics_dt = self.sim.dt
+        c.decimation = self.decimation
+        c.inner_steps = self.sim.inner_steps
+        c.max_episode_length = self.max_episode_length
+        c.action_scale = self.actions.joint_pos.scale
+        import re
+
+        groups = list(self.robot.actuators.items())
+        for j, name in enumerate(names):
+            hit = None
+            for gi, (gname, g) in enumerate(groups):
+                if any(re.fullmatch(p, name) for p in g.joint_names_expr):
+                    hit = (gi, g)
+                    break
+            if hit is None:
+                raise ValueError(f"joint {name} has no actuator group")
+            gi, g = hit
+            c.kp[j] = g.stiffness
+            c.kd[j] = g.damping
+            c.effort_limit[j] = g.effort_limit
+            c.delay_group[j] = gi
+        g0 = groups[0][1]
+        c.min_delay, c.max_delay = g0.min_delay, g0.max_delay
+        if any((g.min_delay, g.max_delay) != (g0.min_delay, g0.max_delay) for _, g in groups):
+            raise ValueError("all actuator groups must share the delay range")
+        if c.max_delay > 2 * self.decimation:
+            raise ValueError("max_delay must be <= 2 * decimation (delay ring holds two env steps)")
+        c.fix_base = int(self.fix_base)
+        c.use_frictionloss = 0
+        s = self.sim
+        c.contact_k, c.contact_c = s.contact_k, s.contact_c
+        c.friction_k, c.friction_c = s.friction_k, s.friction_c
+        c.mu_static, c.mu_dynamic = s.static_friction, s.dynamic_friction
+        c.limit_k, c.limit_c = s.limit_k, s.limit_c
+        c.contact_threshold = self.terminations.base_contact_threshold
+        bv = self.commands.base_velocity
+        c.cmd_resample_time = bv.resampling_time_range[0]
+        if bv.resampling_time_range[0] != bv.resampling_time_range[1]:
+            raise ValueError("only a constant resampling time is supported")
+        r = bv.ranges
+        c.cmd_lin_x[:] = r.lin_vel_x
+        c.cmd_lin_y[:] = r.lin_vel_y
+        c.cmd_ang_z[:] = r.ang_vel_z
+        c.cmd_heading[:] = r.heading
+        c.rel_standing_envs = bv.rel_standing_envs
+        c.rel_heading_envs = bv.rel_heading_envs if bv.heading_command else -1.0
+        c.heading_stiffness = bv.heading_control_stiffness
+        pr = self.events.reset_base_pose_range
+        c.reset_x[:] = pr["x"]
+        c.reset_y[:] = pr["y"]
+        c.reset_yaw[:] = pr["yaw"]
+        po = self.observations.policy
+        if po.history_length != 10:
+            raise ValueError("the kernel's observation history is fixed at 10 frames")
+        c.enable_corruption = int(po.enable_corruption)
+        c.noise_ang_vel = po.base_ang_vel.n_max
+        c.noise_gravity = po.projected_gravity.n_max
+        c.noise_joint_pos = po.joint_pos.n_max
+        c.noise_joint_vel = po.joint_vel.n_max
+        for t, (name, term) in enumerate(self.rewards.items()):
+            c.rew_w[t] = 0.0 if term is None else term.weight
+        c.track_std = self.rewards.track_lin_vel_xy_exp.params.get("std", 0.5)
+        c.air_time_threshold = self.rewards.feet_air_time.params.get("threshold", 0.4)
+        c.soft_limit_factor = self.robot.soft_joint_pos_limit_factor
+        c.illegal_contact_knees = int(self.terminations.base_contact_knees)
+        c.illegal_contact_torso = int(self.terminations.base_contact_torso)
+        c.seed = (self.seed if self.seed is not None else 0) & 0xFFFFFFFFFFFFFFFF
+        assert len(REWARD_TERMS) == NREW and NJ == 12
+        return c
+
+
+def mujoco_cfg(**kw) -> H12FlatEnvCfg:
+    """sim2sim semantics (scripts/deploy/config.yaml:7, policies/demo_rsl/env.yaml): dt 1 ms x 20,
+    PD every physics step, no delay, MJCF clamps, q_ref = q0 + 0.25 a."""
+    c = H12FlatEnvCfg(mode=MODE_MUJOCO, decimation=20)
+    c.sim = replace(c.sim, dt=0.001, inner_steps=1)
+    c.actions.joint_pos.scale = 0.25
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c

@@ -1,0 +1,357 @@
+"""`Isaac-Velocity-Flat-H12_12dof-v0` as a ManagerBasedRLEnv-compatible vectorised env on MI355X.
+
+Mirrors the public surface of IsaacLab 2.1's ``ManagerBasedRLEnv`` that the reference's training
+script reaches through ``RslRlVecEnvWrapper`` (scripts/rsl_rl/train.py:102,120; mirror of step()
+in packages/biped_tasks/biped_tasks/utils/cat/cat_env.py:95-193):
+
+  reset(seed=None, options=None) -> (obs_dict, extras)
+  step(actions (N,12)) -> (obs_dict{"policy": (N,450)}, rew (N,), terminated (N,), truncated (N,), extras)
+  num_envs, device, step_dt, physics_dt, max_episode_length(_s), episode_length_buf (writable),
+  cfg, observation_manager.group_obs_dim, action_manager.total_action_dim, unwrapped, close()
+
+Every step is ONE launch of the fused HIP kernel in libh12env.so (no CPU fallback: a missing
+extension raises).  State lives in one device workspace owned by a torch uint8 tensor; fields are
+exposed as zero-copy torch views.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from types import SimpleNamespace
+
+import torch
+
+from . import _abi
+from ._abi import F as FIELDS
+from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, REWARD_TERMS, H12StepOut, check, load_library
+from .cfg import H12FlatEnvCfg
+from .model import body_names, build_model, joint_names
+
+_LOG_RING = 128   # log accumulator slots (zeroed in chunks, see _log_slot)
+_LOG_CHUNK = 32
+
+
+def env_origins_grid(num_envs: int, spacing: float, device) -> torch.Tensor:
+    """TerrainImporter._compute_env_origins_grid (plane terrain): row/col grid centred at 0."""
+    num_rows = math.ceil(num_envs / int(math.sqrt(num_envs)))
+    num_cols = math.ceil(num_envs / num_rows)
+    ii, jj = torch.meshgrid(torch.arange(num_rows, device=device), torch.arange(num_cols, device=device), indexing="ij")
+    origins = torch.zeros(num_envs, 3, device=device)
+    origins[:, 0] = -(ii.flatten()[:num_envs] - (num_rows - 1) / 2) * spacing
+    origins[:, 1] = (jj.flatten()[:num_envs] - (num_cols - 1) / 2) * spacing
+    return origins
+
+
+class _LazyLog(dict):
+    """extras["log"]: IsaacLab's Episode_Reward/* and Episode_Termination/* values, materialised on
+    first access from the step's device-side accumulator (no host sync inside step())."""
+
+    def __init__(self, acc: torch.Tensor, max_episode_length_s: float):
+        super().__init__()
+        self._acc = acc
+        self._T = max_episode_length_s
+        self._keys = [f"Episode_Reward/{t}" for t in REWARD_TERMS] + [
+            "Episode_Termination/time_out", "Episode_Termination/base_contact"]
+        self._done = False
+
+    def _fill(self):
+        if self._done:
+            return
+        a = self._acc
+        n = a[12].clamp(min=1.0)
+        vals = torch.cat([a[:12] / n / self._T, a[13:15]])
+        for i, k in enumerate(self._keys):
+            dict.__setitem__(self, k, vals[i])
+        self._done = True
+
+    def __getitem__(self, k):
+        self._fill()
+        return dict.__getitem__(self, k)
+
+    def keys(self):
+        self._fill()
+        return dict.keys(self)
+
+    def items(self):
+        self._fill()
+        return dict.items(self)
+
+    def values(self):
+        self._fill()
+        return dict.values(self)
+
+    def __iter__(self):
+        self._fill()
+        return dict.__iter__(self)
+
+    def __len__(self):
+        return len(self._keys)
+
+    def __contains__(self, k):
+        return k in self._keys
+
+
+class _ObservationManager:
+    def __init__(self, env):
+        self._env = env
+        self.group_obs_dim = {"policy": (NOBS,)}
+        self.group_obs_concatenate = {"policy": True}
+        self.active_terms = {"policy": ["base_ang_vel", "projected_gravity", "velocity_commands", "joint_pos",
+                                        "joint_vel", "actions"]}
+
+    def compute(self):
+        return {"policy": self._env._obs[self._env._k]}
+
+
+class _ActionManager:
+    def __init__(self, env):
+        self._env = env
+        self.total_action_dim = NJ
+        self.action_term_dim = [NJ]
+
+    @property
+    def action(self):
+        return self._env._field("ACT").T
+
+    @property
+    def prev_action(self):
+        return self._env._field("ACT_PREV").T
+
+
+class _ArticulationData:
+    """Zero-copy (N, k) views of the SoA workspace in IsaacLab's ArticulationData vocabulary."""
+
+    def __init__(self, env):
+        self._env = env
+        self.joint_names = joint_names()
+        self.body_names = body_names()
+        dev = env.device
+        m = build_model()
+        self.default_joint_pos = torch.tensor(list(m.q_default), device=dev).repeat(env.num_envs, 1)
+        self.default_joint_vel = torch.zeros(env.num_envs, NJ, device=dev)
+        lo = torch.tensor(list(m.q_lower), device=dev)
+        hi = torch.tensor(list(m.q_upper), device=dev)
+        self.joint_pos_limits = torch.stack([lo, hi], -1).repeat(env.num_envs, 1, 1)
+        f = env.cfg.robot.soft_joint_pos_limit_factor
+        mid, half = (lo + hi) / 2, (hi - lo) / 2 * f
+        self.soft_joint_pos_limits = torch.stack([mid - half, mid + half], -1).repeat(env.num_envs, 1, 1)
+
+    @property
+    def joint_pos(self):
+        return self._env._field("Q").T
+
+    @property
+    def joint_vel(self):
+        return self._env._field("QD").T
+
+    @property
+    def root_pos_w(self):
+        return self._env._field("POS").T + self._env.scene.env_origins
+
+    @property
+    def root_quat_w(self):
+        return self._env._field("QUAT").T
+
+    @property
+    def root_ang_vel_b(self):
+        return self._env._field("WANG").T
+
+    @property
+    def root_link_lin_vel_w(self):
+        return self._env._field("VLIN").T
+
+
+class H12VelocityEnv:
+    """Drop-in for ``ManagerBasedRLEnv`` on ``Isaac-Velocity-Flat-H12_12dof-v0``."""
+
+    is_vector_env = True
+    metadata = {"render_modes": [None], "isaac_sim_version": "none (MI355X-native)"}
+
+    def __init__(self, cfg: H12FlatEnvCfg | None = None, render_mode: str | None = None, env_offset: int = 0,
+                 obs_copy: bool = False, **kwargs):
+        self.cfg = cfg if cfg is not None else H12FlatEnvCfg()
+        self.render_mode = render_mode
+        self.device = torch.device(self.cfg.sim.device)
+        if self.device.type != "cuda":
+            raise RuntimeError(f"H12VelocityEnv runs on the MI355X HIP path only (device={self.device})")
+        self.num_envs = int(self.cfg.scene.num_envs)
+        self.env_offset = int(env_offset)
+        self.obs_copy = obs_copy
+        self._lib = load_library()
+        self._model = build_model()
+        self._ccfg = self.cfg.to_c()
+        torch.cuda.set_device(self.device)
+        nbytes = self._lib.h12env_state_bytes(self.num_envs)
+        self._state = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        h = C.c_void_p()
+        check(self._lib, self._lib.h12env_create(C.byref(self._model), C.byref(self._ccfg), self.num_envs,
+                                                 self.env_offset, self.device.index or 0,
+                                                 C.c_void_p(self._state.data_ptr()), C.byref(h)), "h12env_create")
+        self._h = h
+        self._fstate = self._state.view(torch.float32)[: NF_FLOAT * self.num_envs].view(NF_FLOAT, self.num_envs)
+        self._istate = self._state.view(torch.int32)[NF_FLOAT * self.num_envs:].view(NF_INT, self.num_envs)
+        n = self.num_envs
+        self._obs = [torch.zeros(n, NOBS, device=self.device), torch.zeros(n, NOBS, device=self.device)]
+        self._k = 0
+        self.reward_buf = torch.zeros(n, device=self.device)
+        self.reset_terminated = torch.zeros(n, dtype=torch.bool, device=self.device)
+        self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=self.device)
+        self.reset_buf = self.reset_terminated
+        self._log_ring = torch.zeros(_LOG_RING, NLOG, device=self.device)
+        self._applied_torque = torch.zeros(n, NJ, device=self.device)
+        self._out = H12StepOut()
+        self.common_step_counter = 0
+        self.extras: dict = {}
+        self.scene = SimpleNamespace(env_origins=env_origins_grid(n, self.cfg.scene.env_spacing, self.device),
+                                     num_envs=n)
+        self.observation_manager = _ObservationManager(self)
+        self.action_manager = _ActionManager(self)
+        self._data = _ArticulationData(self)
+        self.scene.articulations = {"robot": SimpleNamespace(data=self._data, joint_names=self._data.joint_names,
+                                                             body_names=self._data.body_names,
+                                                             num_joints=NJ)}
+        self.scene.__dict__["robot"] = self.scene.articulations["robot"]
+        self._configure_spaces()
+        self._closed = False
+
+    # ------------------------------------------------------------------ properties (ManagerBasedEnv)
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def physics_dt(self) -> float:
+        return self.cfg.sim.dt
+
+    @property
+    def step_dt(self) -> float:
+        return self.cfg.sim.dt * self.cfg.decimation
+
+    @property
+    def max_episode_length_s(self) -> float:
+        return self.cfg.episode_length_s
+
+    @property
+    def max_episode_length(self) -> int:
+        return math.ceil(self.max_episode_length_s / self.step_dt)
+
+    @property
+    def episode_length_buf(self) -> torch.Tensor:
+        return self._istate[_abi.I["EPLEN"][0]]
+
+    @episode_length_buf.setter
+    def episode_length_buf(self, value: torch.Tensor):
+        self._istate[_abi.I["EPLEN"][0]].copy_(value.to(self.device))
+
+    @property
+    def obs_buf(self):
+        return {"policy": self._obs[self._k]}
+
+    def _field(self, name: str) -> torch.Tensor:
+        off, cnt = FIELDS[name]
+        return self._fstate[off:off + cnt]
+
+    def _configure_spaces(self):
+        try:
+            import gymnasium as gym
+            import numpy as np
+
+            self.single_observation_space = gym.spaces.Dict(
+                {"policy": gym.spaces.Box(low=-np.inf, high=np.inf, shape=(NOBS,))})
+            self.single_action_space = gym.spaces.Box(low=-np.inf, high=np.inf, shape=(NJ,))
+            self.observation_space = gym.vector.utils.batch_space(self.single_observation_space, self.num_envs)
+            self.action_space = gym.vector.utils.batch_space(self.single_action_space, self.num_envs)
+        except Exception:  # gymnasium is optional for the hot path
+            self.single_observation_space = {"policy": (NOBS,)}
+            self.single_action_space = (NJ,)
+            self.observation_space = {"policy": (self.num_envs, NOBS)}
+            self.action_space = (self.num_envs, NJ)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ gym API
+    def seed(self, seed: int = -1) -> int:
+        self.cfg.seed = int(seed)
+        self._ccfg = self.cfg.to_c()
+        # rebuild the kernel parameters with the new seed, keeping the workspace
+        h = C.c_void_p()
+        check(self._lib, self._lib.h12env_create(C.byref(self._model), C.byref(self._ccfg), self.num_envs,
+                                                 self.env_offset, self.device.index or 0,
+                                                 C.c_void_p(self._state.data_ptr()), C.byref(h)), "h12env_create")
+        self._lib.h12env_destroy(self._h)
+        self._h = h
+        return int(seed)
+
+    def reset(self, seed: int | None = None, env_ids=None, options=None):
+        if seed is not None:
+            self.seed(seed)
+        mask = None
+        if env_ids is not None:
+            mask = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+            mask[torch.as_tensor(env_ids, device=self.device, dtype=torch.long)] = 1
+        obs = self._obs[self._k]
+        check(self._lib, self._lib.h12env_reset(self._h, None if mask is None else C.c_void_p(mask.data_ptr()),
+                                                C.c_void_p(obs.data_ptr()), self._stream()), "h12env_reset")
+        self.extras = {}
+        return {"policy": obs.clone() if self.obs_copy else obs}, self.extras
+
+    def step(self, action: torch.Tensor):
+        a = action.to(device=self.device, dtype=torch.float32)
+        if not a.is_contiguous():
+            a = a.contiguous()
+        if a.shape != (self.num_envs, NJ):
+            raise ValueError(f"actions must be ({self.num_envs}, {NJ}), got {tuple(a.shape)}")
+        self.common_step_counter += 1
+        prev = self._obs[self._k]
+        self._k ^= 1
+        obs = self._obs[self._k]
+        slot = self.common_step_counter % _LOG_RING
+        if slot % _LOG_CHUNK == 0:
+            self._log_ring[slot:slot + _LOG_CHUNK].zero_()
+        acc = self._log_ring[slot]
+        o = self._out
+        o.obs = obs.data_ptr()
+        o.rew = self.reward_buf.data_ptr()
+        o.terminated = self.reset_terminated.data_ptr()
+        o.truncated = self.reset_time_outs.data_ptr()
+        o.log_acc = acc.data_ptr()
+        o.applied_torque = self._applied_torque.data_ptr()
+        o.foot_force = None
+        rc = self._lib.h12env_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(prev.data_ptr()), C.byref(o),
+                                   self.common_step_counter, self._stream())
+        if rc:
+            check(self._lib, rc, "h12env_step")
+        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s), "time_outs": self.reset_time_outs}
+        obs_out = obs.clone() if self.obs_copy else obs
+        return {"policy": obs_out}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
+
+    def step_physics(self, q_ref: torch.Tensor, n_substeps: int):
+        """Parity hook: physics only, PD towards a held joint target (h12env_step_physics)."""
+        q = q_ref.to(device=self.device, dtype=torch.float32).contiguous()
+        check(self._lib, self._lib.h12env_step_physics(self._h, C.c_void_p(q.data_ptr()), int(n_substeps),
+                                                       self._stream()), "h12env_step_physics")
+
+    def get_observations(self):
+        return {"policy": self._obs[self._k]}
+
+    def render(self, recompute: bool = False):
+        return None
+
+    def close(self):
+        if not self._closed:
+            torch.cuda.synchronize(self.device)
+            self._lib.h12env_destroy(self._h)
+            self._closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ accounting
+    def step_cost(self):
+        b, f = C.c_double(), C.c_double()
+        self._lib.h12env_step_cost(self._h, C.byref(b), C.byref(f))
+        return b.value, f.value

@@ -1,0 +1,211 @@
+/*
+ * h12env.h — C-ABI of the MI355X-native H1-2 12-DoF velocity-tracking environment
+ * (the hot path of `Isaac-Velocity-Flat-H12_12dof-v0`, reference repo
+ * olivier-stasse/h1v2-Isaac; paths below are relative to that repository).
+ *
+ * What each entry point replaces on the reference side (the reference reaches all of
+ * this through IsaacLab 2.1 / PhysX; the in-repo mirrors are cited):
+ *
+ *   h12env_create      ManagerBasedRLEnv.__init__ -> load_managers + scene cloning
+ *                      (packages/biped_tasks/biped_tasks/utils/cat/cat_env.py:31-93; task cfg
+ *                      .../velocity/config/h12_12dof/flat_env_cfg.py:13-48, rough_env_cfg.py:128-188;
+ *                      robot cfg packages/biped_assets/biped_assets/robots/h12.py:18-114)
+ *   h12env_reset       ManagerBasedRLEnv._reset_idx + reset events + ObservationManager.compute
+ *                      (cat_env.py:195-248; rough_env_cfg.py:140-155; observation_manager.py:271-355)
+ *   h12env_step        ManagerBasedRLEnv.step (cat_env.py:95-193): action processing, 4 x (delayed PD
+ *                      actuator -> PhysX step -> sensor update), terminations, rewards, resets,
+ *                      commands, observations with 10-frame history (circular_buffer.py:79-170)
+ *   h12env_step_physics  parity hook: the MuJoCo sim2sim substep loop
+ *                      (packages/biped_deploy/biped_deploy/robots/h12_mujoco.py:55-67,
+ *                      packages/biped_deploy/biped_deploy/simulator/sim_mujoco.py:102-121)
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative H12_E* code; the message of the last
+ *     failure on the calling thread is h12env_last_error().
+ *   - All array arguments are DEVICE pointers on the handle's device unless named *_host.
+ *   - Calls are stream-ordered on the hipStream_t passed in (NULL = default stream) and never
+ *     synchronise the host.  One handle per device; calls on one handle are not re-entrant.
+ *   - Persistent per-env state lives in ONE device workspace of h12env_state_bytes(n) bytes,
+ *     field-major structure-of-arrays (field f of env i at offset f*n + i).  The caller may
+ *     supply the workspace (e.g. a torch uint8 tensor) so that it can view fields in place
+ *     (episode_length_buf is writable from Python, as rsl_rl's OnPolicyRunner requires).
+ */
+#ifndef H12ENV_H
+#define H12ENV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H12ENV_ABI_VERSION 1
+#define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
+#define H12_NHIST 10       /* observation history length (flat_env_cfg.py:26) */
+#define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
+#define H12_NOBS (H12_OBS_FRAME * H12_NHIST) /* 450 */
+#define H12_NFOOT_PTS 4    /* sole contact spheres per foot (URDF rods, h12_12dof.urdf:168-191) */
+#define H12_NREW 12        /* active reward terms of the Flat task */
+#define H12_NLOG 16        /* log accumulator: 12 episode sums, count, 2 termination counts, spare */
+
+/* error codes */
+#define H12_OK 0
+#define H12_E_ARG (-1)
+#define H12_E_HIP (-2)
+#define H12_E_STATE (-3)
+#define H12_E_ALLOC (-4)
+
+/* simulation modes */
+#define H12_MODE_ISAACLAB 0 /* explicit PD once per physics step with per-group delay + effort clip */
+#define H12_MODE_MUJOCO 1   /* PD every substep, no delay, MJCF actuatorfrcrange clamp (sim2sim) */
+
+/* reward term order (RewardManager order of the merged Flat cfg; weights in h12env_config.rew_w) */
+enum {
+  H12_R_TRACK_LIN_VEL_XY = 0, /* track_lin_vel_xy_yaw_frame_exp, std 0.5   rough_env_cfg.py:87-91 */
+  H12_R_TRACK_ANG_VEL_Z,      /* track_ang_vel_z_world_exp, std 0.5       rough_env_cfg.py:92-96 */
+  H12_R_ANG_VEL_XY_L2,        /* ang_vel_xy_l2                            velocity_env_cfg.py:237 */
+  H12_R_DOF_TORQUES_L2,       /* joint_torques_l2                         flat_env_cfg.py:40-44 */
+  H12_R_DOF_ACC_L2,           /* joint_acc_l2                             flat_env_cfg.py:37 */
+  H12_R_ACTION_RATE_L2,       /* action_rate_l2                           flat_env_cfg.py:36 */
+  H12_R_FEET_AIR_TIME,        /* feet_air_time_positive_biped, thr 0.4    rough_env_cfg.py:97-105 */
+  H12_R_FLAT_ORIENTATION_L2,  /* flat_orientation_l2                      rough_env_cfg.py:176 */
+  H12_R_DOF_POS_LIMITS,       /* joint_pos_limits (ankles)                rough_env_cfg.py:115-119 */
+  H12_R_TERMINATION,          /* is_terminated                            rough_env_cfg.py:85 */
+  H12_R_FEET_SLIDE,           /* feet_slide                               rough_env_cfg.py:106-113 */
+  H12_R_JOINT_DEV_HIP         /* joint_deviation_l1 (hip yaw/roll)        rough_env_cfg.py:121-125 */
+};
+
+/* Model constants (filled from h12env/assets/h12_12dof_model.json, generated from the MJCF). */
+typedef struct h12env_model {
+  int32_t version;
+  int32_t parent[H12_NJ];        /* -1 = floating base */
+  int32_t axis[H12_NJ];          /* 0=x 1=y 2=z (all H1-2 leg axes are coordinate axes) */
+  float joint_pos[H12_NJ][3];    /* joint frame origin in parent frame at q=0 (no rotation) */
+  float link_mass[H12_NJ];
+  float link_com[H12_NJ][3];
+  float link_inertia[H12_NJ][6]; /* about COM, link frame: xx yy zz xy xz yz */
+  float base_mass;
+  float base_com[3];
+  float base_inertia[6];         /* pelvis + 39 welded upper-body bodies, about composite COM */
+  float q_lower[H12_NJ], q_upper[H12_NJ];
+  float armature[H12_NJ], damping[H12_NJ], frictionloss[H12_NJ];
+  float mj_frc_limit[H12_NJ];    /* MJCF actuatorfrcrange (MuJoCo mode clamp) */
+  float q_default[H12_NJ];       /* keyframe / init_state joint_pos (h12.py:39-53) */
+  float root_height;             /* init_state pos z = 1.05 */
+  float foot_pts[H12_NFOOT_PTS][3]; /* sole sphere centres in ankle-roll frame */
+  float foot_radius;
+  float knee_p0[3], knee_p1[3];  /* knee capsule segment in knee frame */
+  float knee_radius;
+  float torso_center[3], torso_half[3]; /* torso collision box in base frame */
+  float gravity;                 /* 9.81 */
+} h12env_model;
+
+/* Task / simulation configuration. h12env_config_default() fills the Flat-H12_12dof values. */
+typedef struct h12env_config {
+  int32_t abi_version;
+  int32_t mode;                /* H12_MODE_* */
+  float physics_dt;            /* 0.005 (velocity_env_cfg.py:305); MuJoCo mode: 0.001 */
+  int32_t decimation;          /* 4 (velocity_env_cfg.py:302); MuJoCo mode: 20 */
+  int32_t inner_steps;         /* contact/dynamics integration substeps per physics step (>=1) */
+  int32_t max_episode_length;  /* ceil(20 s / step_dt) = 1000 */
+  float action_scale;          /* 0.5 (velocity_env_cfg.py:111) */
+  float kp[H12_NJ], kd[H12_NJ], effort_limit[H12_NJ]; /* h12.py:58-112 */
+  int32_t delay_group[H12_NJ]; /* 0 legs, 1 knees, 2 feet */
+  int32_t min_delay, max_delay;/* 0, 5 physics steps */
+  int32_t fix_base;            /* parity hook: base welded in place (scene_12dof.xml:23-25) */
+  int32_t use_frictionloss;    /* smooth MJCF frictionloss (off by default) */
+  /* penalty contact + joint limits */
+  float contact_k, contact_c;  /* normal spring [N/m] / damper [N s/m] */
+  float mu_static, mu_dynamic; /* 0.8 / 0.6 (velocity_env_cfg.py:153-163, multiply with ground 1.0) */
+  float friction_k, friction_c;/* sole stiction spring [N/m] / damper [N s/m] (anchored, Coulomb-capped) */
+  float limit_k, limit_c;      /* joint-limit penalty [Nm/rad], [Nm s/rad] */
+  float contact_threshold;     /* ContactSensorCfg.force_threshold = 1.0 N */
+  /* commands: UniformVelocityCommandCfg (velocity_env_cfg.py:90-104, flat_env_cfg.py:46-48) */
+  float cmd_resample_time;
+  float cmd_lin_x[2], cmd_lin_y[2], cmd_ang_z[2], cmd_heading[2];
+  float rel_standing_envs, rel_heading_envs, heading_stiffness;
+  /* reset events (rough_env_cfg.py:143-155) */
+  float reset_x[2], reset_y[2], reset_yaw[2];
+  /* observation corruption: AdditiveUniformNoise half-widths (velocity_env_cfg.py:124-131) */
+  int32_t enable_corruption;
+  float noise_ang_vel, noise_gravity, noise_joint_pos, noise_joint_vel;
+  /* rewards */
+  float rew_w[H12_NREW];
+  float track_std;             /* 0.5 */
+  float air_time_threshold;    /* 0.4 */
+  float soft_limit_factor;     /* 0.9 (h12.py:56) */
+  int32_t illegal_contact_knees, illegal_contact_torso; /* bodies with colliders among the list */
+  uint64_t seed;
+} h12env_config;
+
+/* Persistent per-env state fields (field-major SoA in the workspace). */
+enum {
+  H12_F_POS = 0,        /* 3  base position, env-local frame [m] */
+  H12_F_QUAT = 3,       /* 4  base orientation w x y z */
+  H12_F_VLIN = 7,       /* 3  base-origin linear velocity, world frame (MuJoCo qvel[0:3]) */
+  H12_F_WANG = 10,      /* 3  base angular velocity, base frame (MuJoCo qvel[3:6]) */
+  H12_F_Q = 13,         /* 12 joint positions */
+  H12_F_QD = 25,        /* 12 joint velocities */
+  H12_F_ACT = 37,       /* 12 action_manager.action  (a_t, raw) */
+  H12_F_ACT_PREV = 49,  /* 12 action_manager.prev_action (a_{t-1}) */
+  H12_F_CMD = 61,       /* 3  vel_command_b */
+  H12_F_HEADING = 64,   /* 1  heading_target */
+  H12_F_CMD_TIME = 65,  /* 1  command time_left */
+  H12_F_AIR = 66,       /* 2  current_air_time (feet) */
+  H12_F_CONTACT = 68,   /* 2  current_contact_time (feet) */
+  H12_F_LAST_AIR = 70,  /* 2  last_air_time */
+  H12_F_LAST_CONTACT = 72, /* 2 last_contact_time */
+  H12_F_EPSUM = 74,     /* 12 episode reward sums */
+  H12_F_ANCHOR = 86,    /* 16 sole-sphere stiction anchors: [foot][pt][x,y] world (env-local) */
+  H12_NF_FLOAT = 102
+};
+enum {
+  H12_I_EPLEN = 0,      /* episode_length_buf (int32) */
+  H12_I_PACK = 1,       /* bits 0-8 lags (3 x 3 bits), 9-10 steps since reset (sat. 2), 11 heading env,
+                           12 standing env, 13-20 sole-sphere contact flags (bit 13 + 4*foot + pt) */
+  H12_NF_INT = 2
+};
+
+/* Optional per-step outputs; any pointer may be NULL. */
+typedef struct h12env_step_out {
+  float* obs;              /* N x 450 (required) */
+  float* rew;              /* N       (required) */
+  uint8_t* terminated;     /* N       (required) */
+  uint8_t* truncated;      /* N       (required) */
+  float* log_acc;          /* H12_NLOG floats, accumulated with atomics (caller zeroes) */
+  float* applied_torque;   /* N x 12, last physics step (ArticulationData.applied_torque) */
+  float* foot_force;       /* N x 2,  |net contact force| of the feet, last physics step */
+} h12env_step_out;
+
+typedef struct h12env h12env;
+
+int h12env_config_default(h12env_config* cfg);
+size_t h12env_state_bytes(int n_envs);
+/* device: HIP ordinal; env_offset: global id of this shard's first env (RNG keying, sharding
+ * invariance); state_dev: caller workspace of h12env_state_bytes(n_envs) bytes or NULL. */
+int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_envs, int64_t env_offset,
+                  int device, void* state_dev, h12env** out);
+void h12env_destroy(h12env* h);
+/* Reset the envs flagged in mask (N bytes, NULL = all) and write their first observation
+ * (history filled with the first frame) into obs (N x 450); other rows are left untouched. */
+int h12env_reset(h12env* h, const uint8_t* mask, float* obs, void* stream);
+/* One env step (decimation x physics).  obs_prev: previous obs (history source), may equal
+ * out->obs.  step_index: common_step_counter after increment (>= 1). */
+int h12env_step(h12env* h, const float* actions, const float* obs_prev, const h12env_step_out* out,
+                int64_t step_index, void* stream);
+/* Parity hook: n_substeps physics steps with a held joint target q_ref (N x 12) using the
+ * configured mode (PD, limits, contact), no MDP.  Mirrors H12Mujoco.step. */
+int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* stream);
+/* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
+void* h12env_field_ptr(h12env* h, int is_int, int field);
+int h12env_num_envs(const h12env* h);
+/* Algorithmic accounting of one env step for the roofline report. */
+int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_env);
+const char* h12env_last_error(void);
+int h12env_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* H12ENV_H */

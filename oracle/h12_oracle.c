@@ -1,0 +1,981 @@
+/*
+ * h12_oracle.c — CPU restatement of the H1-2 Flat velocity env (TEST INFRASTRUCTURE ONLY).
+ * See h12_oracle.h for scope and parity status.  Double precision, generic 6x6 spatial
+ * algebra (Featherstone, "Rigid Body Dynamics Algorithms", 2008): written for clarity, not speed,
+ * and independent of the fp32 structured kernel in h1v2-isaac_amd/csrc/h12env.hip.
+ */
+#include "h12_oracle.h"
+
+#include <math.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NJ H12_NJ
+#define NB (NJ + 1)
+#define PI_D 3.14159265358979323846
+
+/* ------------------------------------------------------------------ RNG (Philox4x32-10) */
+void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = c3;
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * x0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * x2;
+    uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0;
+    uint32_t y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1;
+    x1 = (uint32_t)p1;
+    x3 = (uint32_t)p0;
+    x0 = y0;
+    x2 = y2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+}
+/* streams (counter word c2 = stream << 16 | block) */
+enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3 };
+static double u01(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
+static double uab(uint32_t x, double a, double b) { return a + (b - a) * (double)(float)u01(x); }
+
+static void rng_block(uint64_t seed, int64_t env, uint32_t ctr_lo, uint32_t ctr_hi, int stream, int block,
+                      uint32_t out[4]) {
+  orc_philox(seed, (uint32_t)env, ctr_lo, ((uint32_t)stream << 16) | (uint32_t)block, ctr_hi, out);
+}
+
+/* ------------------------------------------------------------------ small linear algebra */
+typedef double m3[3][3];
+static void cross3(const double a[3], const double b[3], double o[3]) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+static void m3v(const m3 A, const double v[3], double o[3]) {
+  double t[3];
+  for (int i = 0; i < 3; ++i) t[i] = A[i][0] * v[0] + A[i][1] * v[1] + A[i][2] * v[2];
+  memcpy(o, t, sizeof t);
+}
+static void m3tv(const m3 A, const double v[3], double o[3]) {
+  double t[3];
+  for (int i = 0; i < 3; ++i) t[i] = A[0][i] * v[0] + A[1][i] * v[1] + A[2][i] * v[2];
+  memcpy(o, t, sizeof t);
+}
+static void m3mul(const m3 A, const m3 B, m3 C) {
+  m3 T;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+  memcpy(C, T, sizeof T);
+}
+static void rot_axis(int axis, double q, m3 R) { /* child frame rotated by q about parent axis */
+  double c = cos(q), s = sin(q);
+  memset(R, 0, sizeof(m3));
+  if (axis == 0) { R[0][0] = 1; R[1][1] = c; R[1][2] = -s; R[2][1] = s; R[2][2] = c; }
+  else if (axis == 1) { R[1][1] = 1; R[0][0] = c; R[0][2] = s; R[2][0] = -s; R[2][2] = c; }
+  else { R[2][2] = 1; R[0][0] = c; R[0][1] = -s; R[1][0] = s; R[1][1] = c; }
+}
+static void quat_to_R(const double q[4], m3 R) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  double n = sqrt(w * w + x * x + y * y + z * z);
+  w /= n; x /= n; y /= n; z /= n;
+  R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - w * z); R[0][2] = 2 * (x * z + w * y);
+  R[1][0] = 2 * (x * y + w * z); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - w * x);
+  R[2][0] = 2 * (x * z - w * y); R[2][1] = 2 * (y * z + w * x); R[2][2] = 1 - 2 * (x * x + y * y);
+}
+
+/* 6x6 spatial matrices (row major, blocks [ang; lin]) */
+typedef double m6[6][6];
+static void m6v(const m6 A, const double v[6], double o[6]) {
+  double t[6];
+  for (int i = 0; i < 6; ++i) { t[i] = 0; for (int j = 0; j < 6; ++j) t[i] += A[i][j] * v[j]; }
+  memcpy(o, t, sizeof t);
+}
+static void m6tv(const m6 A, const double v[6], double o[6]) {
+  double t[6];
+  for (int i = 0; i < 6; ++i) { t[i] = 0; for (int j = 0; j < 6; ++j) t[i] += A[j][i] * v[j]; }
+  memcpy(o, t, sizeof t);
+}
+/* C = X^T I X */
+static void congruence(const m6 X, const m6 I, m6 C) {
+  m6 T;
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) { double s = 0; for (int k = 0; k < 6; ++k) s += I[i][k] * X[k][j]; T[i][j] = s; }
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) { double s = 0; for (int k = 0; k < 6; ++k) s += X[k][i] * T[k][j]; C[i][j] = s; }
+}
+/* motion transform parent->child from (E, r): [E 0; -E rx E] */
+static void xform(const m3 E, const double r[3], m6 X) {
+  memset(X, 0, sizeof(m6));
+  m3 rx = {{0, -r[2], r[1]}, {r[2], 0, -r[0]}, {-r[1], r[0], 0}};
+  m3 Erx;
+  m3mul(E, rx, Erx);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) { X[i][j] = E[i][j]; X[3 + i][3 + j] = E[i][j]; X[3 + i][j] = -Erx[i][j]; }
+}
+static void crm(const double v[6], const double m[6], double o[6]) { /* v x m */
+  double a[3], b[3];
+  cross3(v, m, a);
+  cross3(v, m + 3, o + 3);
+  cross3(v + 3, m, b);
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2];
+  o[3] += b[0]; o[4] += b[1]; o[5] += b[2];
+}
+static void crf(const double v[6], const double f[6], double o[6]) { /* v x* f */
+  double a[3], b[3];
+  cross3(v, f, a);
+  cross3(v + 3, f + 3, b);
+  cross3(v, f + 3, o + 3);
+  o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
+}
+/* rigid-body spatial inertia at body origin from mass, COM, COM inertia (xx yy zz xy xz yz) */
+static void rb_inertia(double mass, const float com[3], const float Ic[6], m6 I) {
+  double c[3] = {com[0], com[1], com[2]};
+  double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+  double Icm[3][3] = {{Ic[0], Ic[3], Ic[4]}, {Ic[3], Ic[1], Ic[5]}, {Ic[4], Ic[5], Ic[2]}};
+  m3 cx = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
+  memset(I, 0, sizeof(m6));
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      I[i][j] = Icm[i][j] + mass * ((i == j ? cc : 0.0) - c[i] * c[j]);
+      I[i][3 + j] = mass * cx[i][j];
+      I[3 + i][j] = -mass * cx[i][j]; /* (m cx)^T = -m cx */
+      I[3 + i][3 + j] = (i == j) ? mass : 0.0;
+    }
+}
+/* in-place Cholesky solve of SPD A (n x n) x = b */
+static int chol_solve(double* A, int n, double* b) {
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
+    if (!(s > 0)) return -1;
+    double d = sqrt(s);
+    A[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / d;
+    }
+  }
+  for (int i = 0; i < n; ++i) { double t = b[i]; for (int k = 0; k < i; ++k) t -= A[i * n + k] * b[k]; b[i] = t / A[i * n + i]; }
+  for (int i = n - 1; i >= 0; --i) { double t = b[i]; for (int k = i + 1; k < n; ++k) t -= A[k * n + i] * b[k]; b[i] = t / A[i * n + i]; }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ kinematics */
+typedef struct kin_t {
+  m6 X[NB];        /* parent -> body motion transforms (X[0] unused) */
+  m6 I[NB];        /* rigid spatial inertias at body origins */
+  double v[NB][6]; /* body spatial velocities (body coords) */
+  m3 R[NB];        /* world rotation of body frames */
+  double p[NB][3]; /* world position of body origins */
+  double ag[6];    /* gravity spatial acceleration in base coords */
+} kin_t;
+
+static void kinematics(const h12env_model* m, const orc_phys* s, kin_t* k) {
+  quat_to_R(s->quat, k->R[0]);
+  memcpy(k->p[0], s->pos, sizeof(double) * 3);
+  rb_inertia(m->base_mass, m->base_com, m->base_inertia, k->I[0]);
+  double vb[3];
+  m3tv(k->R[0], s->vlin, vb);
+  k->v[0][0] = s->wang[0]; k->v[0][1] = s->wang[1]; k->v[0][2] = s->wang[2];
+  k->v[0][3] = vb[0]; k->v[0][4] = vb[1]; k->v[0][5] = vb[2];
+  double gw[3] = {0, 0, -m->gravity}, gb[3];
+  m3tv(k->R[0], gw, gb);
+  k->ag[0] = k->ag[1] = k->ag[2] = 0;
+  k->ag[3] = gb[0]; k->ag[4] = gb[1]; k->ag[5] = gb[2];
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1, par = m->parent[j] + 1;
+    m3 Rj, E;
+    rot_axis(m->axis[j], s->q[j], Rj);
+    for (int a = 0; a < 3; ++a)
+      for (int c = 0; c < 3; ++c) E[a][c] = Rj[c][a];
+    double r[3] = {m->joint_pos[j][0], m->joint_pos[j][1], m->joint_pos[j][2]};
+    xform(E, r, k->X[b]);
+    rb_inertia(m->link_mass[j], m->link_com[j], m->link_inertia[j], k->I[b]);
+    m6v(k->X[b], k->v[par], k->v[b]);
+    k->v[b][m->axis[j]] += s->qd[j];
+    m3mul(k->R[par], Rj, k->R[b]);
+    double t[3];
+    m3v(k->R[par], r, t);
+    for (int a = 0; a < 3; ++a) k->p[b][a] = k->p[par][a] + t[a];
+  }
+}
+
+/* ------------------------------------------------------------------ penalty contact */
+/* Penalty force on a sphere (centre pl in body b coords, radius rad).  Normal: spring-damper,
+ * clipped at 0.  Tangential: for sole spheres (anc != NULL) an anchored stiction spring-damper
+ * capped by the Coulomb cone (mu_static to stick, mu_dynamic while slipping, anchor dragged
+ * along when slipping); for knee / torso a viscous term capped at mu_dynamic.  Accumulates the
+ * spatial force (body coords) into fext[b] and the world force into fw.  Returns 1 in contact. */
+static int contact_point(const h12env_config* c, const kin_t* k, int b, const double pl[3], double rad,
+                         double fext[NB][6], double fw[3], const double* anc_in, int was_in, double* anc_out) {
+  double xw[3];
+  m3v(k->R[b], pl, xw);
+  for (int a = 0; a < 3; ++a) xw[a] += k->p[b][a];
+  double depth = rad - xw[2];
+  if (depth <= 0) return 0;
+  double vl[3];
+  cross3(k->v[b], pl, vl);
+  for (int a = 0; a < 3; ++a) vl[a] += k->v[b][3 + a];
+  double vw[3];
+  m3v(k->R[b], vl, vw);
+  double fn = c->contact_k * depth - c->contact_c * vw[2];
+  if (fn <= 0) return 0;
+  double ft0, ft1;
+  if (anc_out) {
+    double ax = was_in ? anc_in[0] : xw[0], ay = was_in ? anc_in[1] : xw[1];
+    ft0 = -c->friction_k * (xw[0] - ax) - c->friction_c * vw[0];
+    ft1 = -c->friction_k * (xw[1] - ay) - c->friction_c * vw[1];
+    double ftn = sqrt(ft0 * ft0 + ft1 * ft1);
+    if (ftn > c->mu_static * fn) {
+      double sc = c->mu_dynamic * fn / ftn;
+      ft0 *= sc;
+      ft1 *= sc;
+      ax = xw[0] + ft0 / c->friction_k;
+      ay = xw[1] + ft1 / c->friction_k;
+    }
+    anc_out[0] = ax;
+    anc_out[1] = ay;
+  } else {
+    ft0 = -c->friction_c * vw[0];
+    ft1 = -c->friction_c * vw[1];
+    double ftn = sqrt(ft0 * ft0 + ft1 * ft1), cap = c->mu_dynamic * fn;
+    if (ftn > cap) { ft0 *= cap / ftn; ft1 *= cap / ftn; }
+  }
+  double F[3] = {ft0, ft1, fn}, fl[3], nl[3];
+  m3tv(k->R[b], F, fl);
+  cross3(pl, fl, nl);
+  for (int a = 0; a < 3; ++a) { fext[b][a] += nl[a]; fext[b][3 + a] += fl[a]; fw[a] += F[a]; }
+  return 1;
+}
+
+/* evaluates every contact primitive; s->anchor/cmask are read, next_anchor/next_mask written */
+static void contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
+                     double fext[NB][6], orc_contact_report* rep, double next_anchor[2][H12_NFOOT_PTS][2],
+                     int32_t* next_mask) {
+  orc_contact_report r;
+  memset(&r, 0, sizeof r);
+  int32_t mask = 0;
+  for (int f = 0; f < 2; ++f) {
+    int b = 6 * f + 6; /* ankle roll link of leg f */
+    for (int p = 0; p < H12_NFOOT_PTS; ++p) {
+      double pl[3] = {m->foot_pts[p][0], m->foot_pts[p][1], m->foot_pts[p][2]};
+      int bit = 4 * f + p;
+      double tmp[2];
+      double* out = next_anchor ? next_anchor[f][p] : tmp;
+      if (contact_point(c, k, b, pl, m->foot_radius, fext, r.foot_force[f], s->anchor[f][p], (s->cmask >> bit) & 1, out))
+        mask |= 1 << bit;
+    }
+    /* knee capsule: lower end point of the segment in world z */
+    int bk = 6 * f + 4;
+    double a0[3] = {m->knee_p0[0], m->knee_p0[1], m->knee_p0[2]}, a1[3] = {m->knee_p1[0], m->knee_p1[1], m->knee_p1[2]};
+    double w0[3], w1[3];
+    m3v(k->R[bk], a0, w0);
+    m3v(k->R[bk], a1, w1);
+    contact_point(c, k, bk, (w0[2] <= w1[2]) ? a0 : a1, m->knee_radius, fext, r.knee_force[f], 0, 0, 0);
+  }
+  /* torso box (welded to the base): lowest corner */
+  double corner[3];
+  for (int a = 0; a < 3; ++a) {
+    double sg = k->R[0][2][a] > 0 ? -1.0 : 1.0;
+    corner[a] = m->torso_center[a] + sg * m->torso_half[a];
+  }
+  contact_point(c, k, 0, corner, 0.0, fext, r.torso_force, 0, 0, 0);
+  if (rep) *rep = r;
+  if (next_mask) *next_mask = mask;
+}
+
+/* ------------------------------------------------------------------ dynamics */
+/* RNEA: generalised force for accelerations nudot (base spatial accel + qdd), with external forces */
+static void rnea(const h12env_model* m, const kin_t* k, const orc_phys* s, const double nudot[18],
+                 double fext[NB][6], double out[18]) {
+  double a[NB][6], f[NB][6];
+  for (int i = 0; i < 6; ++i) a[0][i] = nudot[i] - k->ag[i];
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1, par = m->parent[j] + 1;
+    double sq[6] = {0, 0, 0, 0, 0, 0}, t[6];
+    sq[m->axis[j]] = s->qd[j];
+    m6v(k->X[b], a[par], a[b]);
+    a[b][m->axis[j]] += nudot[6 + j];
+    crm(k->v[b], sq, t);
+    for (int i = 0; i < 6; ++i) a[b][i] += t[i];
+  }
+  for (int b = 0; b < NB; ++b) {
+    double Iv[6], Ia[6], t[6];
+    m6v(k->I[b], k->v[b], Iv);
+    m6v(k->I[b], a[b], Ia);
+    crf(k->v[b], Iv, t);
+    for (int i = 0; i < 6; ++i) f[b][i] = Ia[i] + t[i] - fext[b][i];
+  }
+  for (int j = NJ - 1; j >= 0; --j) {
+    int b = j + 1, par = m->parent[j] + 1;
+    out[6 + j] = f[b][m->axis[j]];
+    double t[6];
+    m6tv(k->X[b], f[b], t);
+    for (int i = 0; i < 6; ++i) f[par][i] += t[i];
+  }
+  for (int i = 0; i < 6; ++i) out[i] = f[0][i];
+}
+
+static void crba(const h12env_model* m, const kin_t* k, double H[18 * 18]) {
+  m6 Ic[NB];
+  memcpy(Ic, k->I, sizeof Ic);
+  for (int j = NJ - 1; j >= 0; --j) {
+    int b = j + 1, par = m->parent[j] + 1;
+    m6 T;
+    congruence(k->X[b], Ic[b], T);
+    for (int a = 0; a < 6; ++a)
+      for (int c = 0; c < 6; ++c) Ic[par][a][c] += T[a][c];
+  }
+  memset(H, 0, sizeof(double) * 18 * 18);
+  for (int a = 0; a < 6; ++a)
+    for (int c = 0; c < 6; ++c) H[a * 18 + c] = Ic[0][a][c];
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1;
+    double F[6];
+    for (int i = 0; i < 6; ++i) F[i] = Ic[b][i][m->axis[j]];
+    H[(6 + j) * 18 + 6 + j] = F[m->axis[j]];
+    int jj = j;
+    while (m->parent[jj] >= 0) {
+      double t[6];
+      m6tv(k->X[jj + 1], F, t);
+      memcpy(F, t, sizeof t);
+      jj = m->parent[jj];
+      H[(6 + j) * 18 + 6 + jj] = H[(6 + jj) * 18 + 6 + j] = F[m->axis[jj]];
+    }
+    double t[6];
+    m6tv(k->X[jj + 1], F, t);
+    for (int i = 0; i < 6; ++i) H[(6 + j) * 18 + i] = H[i * 18 + 6 + j] = t[i];
+  }
+}
+
+static int aba(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
+               const double tau[NJ], const double dimpl[NJ], double fext[NB][6], double nudot[18]) {
+  m6 IA[NB];
+  double pA[NB][6], cb[NB][6], U[NB][6], D[NB], u[NB];
+  for (int b = 0; b < NB; ++b) {
+    double Iv[6];
+    memcpy(IA[b], k->I[b], sizeof(m6));
+    m6v(k->I[b], k->v[b], Iv);
+    crf(k->v[b], Iv, pA[b]);
+    for (int i = 0; i < 6; ++i) pA[b][i] -= fext[b][i];
+  }
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1;
+    double sq[6] = {0, 0, 0, 0, 0, 0};
+    sq[m->axis[j]] = s->qd[j];
+    crm(k->v[b], sq, cb[b]);
+  }
+  for (int j = NJ - 1; j >= 0; --j) {
+    int b = j + 1, par = m->parent[j] + 1, ax = m->axis[j];
+    for (int i = 0; i < 6; ++i) U[b][i] = IA[b][i][ax];
+    D[b] = U[b][ax] + m->armature[j] + dimpl[j];
+    u[b] = tau[j] - pA[b][ax];
+    m6 Ia;
+    for (int a = 0; a < 6; ++a)
+      for (int cc = 0; cc < 6; ++cc) Ia[a][cc] = IA[b][a][cc] - U[b][a] * U[b][cc] / D[b];
+    double pa[6], t[6];
+    m6v(Ia, cb[b], t);
+    for (int i = 0; i < 6; ++i) pa[i] = pA[b][i] + t[i] + U[b][i] * u[b] / D[b];
+    m6 T;
+    congruence(k->X[b], Ia, T);
+    for (int a = 0; a < 6; ++a)
+      for (int cc = 0; cc < 6; ++cc) IA[par][a][cc] += T[a][cc];
+    m6tv(k->X[b], pa, t);
+    for (int i = 0; i < 6; ++i) pA[par][i] += t[i];
+  }
+  double a[NB][6];
+  if (c->fix_base) {
+    for (int i = 0; i < 6; ++i) a[0][i] = -k->ag[i];
+  } else {
+    double A[36], rhs[6];
+    for (int i = 0; i < 6; ++i) { rhs[i] = -pA[0][i]; for (int j = 0; j < 6; ++j) A[i * 6 + j] = IA[0][i][j]; }
+    if (chol_solve(A, 6, rhs)) return -1;
+    memcpy(a[0], rhs, sizeof rhs);
+  }
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1, par = m->parent[j] + 1, ax = m->axis[j];
+    double ap[6];
+    m6v(k->X[b], a[par], ap);
+    for (int i = 0; i < 6; ++i) ap[i] += cb[b][i];
+    double ua = 0;
+    for (int i = 0; i < 6; ++i) ua += U[b][i] * ap[i];
+    double qdd = (u[b] - ua) / D[b];
+    ap[ax] += qdd;
+    memcpy(a[b], ap, sizeof ap);
+    nudot[6 + j] = qdd;
+  }
+  if (c->fix_base) for (int i = 0; i < 6; ++i) nudot[i] = 0;
+  else for (int i = 0; i < 6; ++i) nudot[i] = a[0][i] + k->ag[i];
+  return 0;
+}
+
+int orc_mass_matrix(const h12env_model* m, const orc_phys* s, double M[18 * 18]) {
+  kin_t k;
+  kinematics(m, s, &k);
+  crba(m, &k, M);
+  for (int j = 0; j < NJ; ++j) M[(6 + j) * 18 + 6 + j] += m->armature[j];
+  return 0;
+}
+
+static void joint_limit_torque(const h12env_model* m, const h12env_config* c, const orc_phys* s, double tau[NJ]) {
+  for (int j = 0; j < NJ; ++j) {
+    double q = s->q[j], qd = s->qd[j], t = 0;
+    if (q > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - c->limit_c * qd; if (t > 0) t = 0; }
+    else if (q < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - c->limit_c * qd; if (t < 0) t = 0; }
+    tau[j] += t;
+  }
+}
+
+static int forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s, const double tau[NJ],
+                            int algo, double dt_impl, int with_contact, double nudot[18], orc_contact_report* rep,
+                            double next_anchor[2][H12_NFOOT_PTS][2], int32_t* next_mask) {
+  kin_t k;
+  kinematics(m, s, &k);
+  double fext[NB][6];
+  memset(fext, 0, sizeof fext);
+  if (with_contact) contacts(m, c, &k, s, fext, rep, next_anchor, next_mask);
+  else {
+    if (rep) memset(rep, 0, sizeof *rep);
+    if (next_mask) *next_mask = 0;
+  }
+  double dimpl[NJ], tq[NJ];
+  int mj = (c->mode == H12_MODE_MUJOCO);
+  for (int j = 0; j < NJ; ++j) {
+    double d = mj ? m->damping[j] : 0.0;
+    dimpl[j] = dt_impl * d;
+    tq[j] = tau[j] - d * s->qd[j];
+    if (c->use_frictionloss) tq[j] -= m->frictionloss[j] * tanh(s->qd[j] / 0.01);
+  }
+  if (algo == 1) return aba(m, c, &k, s, tq, dimpl, fext, nudot);
+  double H[18 * 18], C[18], zero[18] = {0};
+  crba(m, &k, H);
+  rnea(m, &k, s, zero, fext, C);
+  for (int j = 0; j < NJ; ++j) H[(6 + j) * 18 + 6 + j] += m->armature[j] + dimpl[j];
+  double b[18];
+  for (int i = 0; i < 6; ++i) b[i] = -C[i];
+  for (int j = 0; j < NJ; ++j) b[6 + j] = tq[j] - C[6 + j];
+  if (c->fix_base) {
+    /* base rows removed: solve the 12 x 12 joint block with the base held (nudot_base = 0) */
+    double Hj[NJ * NJ];
+    for (int a = 0; a < NJ; ++a)
+      for (int cc = 0; cc < NJ; ++cc) Hj[a * NJ + cc] = H[(6 + a) * 18 + 6 + cc];
+    double bj[NJ];
+    memcpy(bj, b + 6, sizeof bj);
+    if (chol_solve(Hj, NJ, bj)) return -1;
+    for (int i = 0; i < 6; ++i) nudot[i] = 0;
+    memcpy(nudot + 6, bj, sizeof bj);
+    return 0;
+  }
+  if (chol_solve(H, 18, b)) return -1;
+  memcpy(nudot, b, sizeof b);
+  return 0;
+}
+
+int orc_forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s, const double tau[NJ],
+                         int algo, double dt_impl, int with_contact, double nudot[18], orc_contact_report* rep) {
+  return forward_dynamics(m, c, s, tau, algo, dt_impl, with_contact, nudot, rep, 0, 0);
+}
+
+int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy, double lin[3], double ang[3]) {
+  kin_t k;
+  kinematics(m, s, &k);
+  double ke = 0, pe = 0;
+  for (int a = 0; a < 3; ++a) lin[a] = ang[a] = 0;
+  for (int b = 0; b < NB; ++b) {
+    double h[6];
+    m6v(k.I[b], k.v[b], h);
+    for (int i = 0; i < 6; ++i) ke += 0.5 * k.v[b][i] * h[i];
+    double hl[3], ha[3], t[3];
+    m3v(k.R[b], h + 3, hl);
+    m3v(k.R[b], h, ha);
+    cross3(k.p[b], hl, t);
+    for (int a = 0; a < 3; ++a) { lin[a] += hl[a]; ang[a] += ha[a] + t[a]; }
+    double mass = b == 0 ? m->base_mass : m->link_mass[b - 1];
+    const float* com = b == 0 ? m->base_com : m->link_com[b - 1];
+    double cl[3] = {com[0], com[1], com[2]}, cw[3];
+    m3v(k.R[b], cl, cw);
+    pe += mass * m->gravity * (k.p[b][2] + cw[2]);
+  }
+  for (int j = 0; j < NJ; ++j) ke += 0.5 * m->armature[j] * s->qd[j] * s->qd[j];
+  *energy = ke + pe;
+  return 0;
+}
+
+/* semi-implicit Euler in MuJoCo coordinates (mj_Euler + mju_quatIntegrate) */
+static void integrate(orc_phys* s, const double nd[18], double dt, int fix_base) {
+  if (!fix_base) {
+    m3 R;
+    quat_to_R(s->quat, R);
+    double vb[3], wxv[3], al[3], aw[3];
+    m3tv(R, s->vlin, vb);
+    cross3(s->wang, vb, wxv);
+    for (int a = 0; a < 3; ++a) al[a] = nd[3 + a] + wxv[a];
+    m3v(R, al, aw);
+    for (int a = 0; a < 3; ++a) { s->vlin[a] += dt * aw[a]; s->wang[a] += dt * nd[a]; }
+    for (int a = 0; a < 3; ++a) s->pos[a] += dt * s->vlin[a];
+    double w2 = s->wang[0] * s->wang[0] + s->wang[1] * s->wang[1] + s->wang[2] * s->wang[2];
+    double wn = sqrt(w2);
+    if (wn > 0) {
+      double ang = wn * dt, sh = sin(0.5 * ang) / wn, ch = cos(0.5 * ang);
+      double r[4] = {ch, s->wang[0] * sh, s->wang[1] * sh, s->wang[2] * sh};
+      double* q = s->quat;
+      double o[4] = {q[0] * r[0] - q[1] * r[1] - q[2] * r[2] - q[3] * r[3],
+                     q[0] * r[1] + q[1] * r[0] + q[2] * r[3] - q[3] * r[2],
+                     q[0] * r[2] - q[1] * r[3] + q[2] * r[0] + q[3] * r[1],
+                     q[0] * r[3] + q[1] * r[2] - q[2] * r[1] + q[3] * r[0]};
+      double n = sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
+      for (int a = 0; a < 4; ++a) q[a] = o[a] / n;
+    }
+  }
+  for (int j = 0; j < NJ; ++j) { s->qd[j] += dt * nd[6 + j]; s->q[j] += dt * s->qd[j]; }
+}
+
+int orc_physics_step(const h12env_model* m, const h12env_config* c, orc_phys* s, const double tau_pd[NJ],
+                     int with_contact, int algo, orc_contact_report* rep) {
+  int n = c->inner_steps < 1 ? 1 : c->inner_steps;
+  double h = c->physics_dt / n;
+  orc_contact_report acc;
+  memset(&acc, 0, sizeof acc);
+  for (int it = 0; it < n; ++it) {
+    double tau[NJ], nd[18];
+    memcpy(tau, tau_pd, sizeof tau);
+    joint_limit_torque(m, c, s, tau);
+    orc_contact_report r;
+    double nanc[2][H12_NFOOT_PTS][2];
+    int32_t nmask = 0;
+    memcpy(nanc, s->anchor, sizeof nanc);
+    if (forward_dynamics(m, c, s, tau, algo, h, with_contact, nd, &r, nanc, &nmask)) return -1;
+    double* pa = (double*)&acc;
+    const double* pr = (const double*)&r;
+    for (size_t i = 0; i < sizeof acc / sizeof(double); ++i) pa[i] += pr[i] / n;
+    integrate(s, nd, h, c->fix_base);
+    memcpy(s->anchor, nanc, sizeof nanc);
+    s->cmask = nmask;
+  }
+  if (rep) *rep = acc;
+  return 0;
+}
+
+int orc_mujoco_rollout(const h12env_model* m, const h12env_config* c, orc_phys* s, const double* q_ref, int n_steps,
+                       int with_contact, int algo, double* traj_q) {
+  for (int t = 0; t < n_steps; ++t) {
+    double tau[NJ];
+    for (int j = 0; j < NJ; ++j) {
+      double v = c->kp[j] * (q_ref[j] - s->q[j]) - c->kd[j] * s->qd[j];
+      double lim = m->mj_frc_limit[j];
+      tau[j] = v > lim ? lim : (v < -lim ? -lim : v);
+    }
+    if (orc_physics_step(m, c, s, tau, with_contact, algo, 0)) return -1;
+    if (traj_q) memcpy(traj_q + (size_t)t * NJ, s->q, sizeof(double) * NJ);
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ MDP (IsaacLab semantics) */
+typedef struct orc_env {
+  orc_phys p;
+  double act[NJ], act_prev[NJ], cmd[3], heading, cmd_time, air[2], con[2], last_air[2], last_con[2], epsum[H12_NREW];
+  int eplen, lag[3], since_reset, is_heading, is_standing;
+} orc_env;
+
+static void env_load(const float* F, const int32_t* I, int n, int i, orc_env* e) {
+#define LD(dst, fld, cnt) for (int a = 0; a < (cnt); ++a) (dst)[a] = F[(size_t)((fld) + a) * n + i]
+  LD(e->p.pos, H12_F_POS, 3); LD(e->p.quat, H12_F_QUAT, 4); LD(e->p.vlin, H12_F_VLIN, 3);
+  LD(e->p.wang, H12_F_WANG, 3); LD(e->p.q, H12_F_Q, NJ); LD(e->p.qd, H12_F_QD, NJ);
+  LD(e->act, H12_F_ACT, NJ); LD(e->act_prev, H12_F_ACT_PREV, NJ); LD(e->cmd, H12_F_CMD, 3);
+  LD(&e->heading, H12_F_HEADING, 1); LD(&e->cmd_time, H12_F_CMD_TIME, 1); LD(e->air, H12_F_AIR, 2);
+  LD(e->con, H12_F_CONTACT, 2); LD(e->last_air, H12_F_LAST_AIR, 2); LD(e->last_con, H12_F_LAST_CONTACT, 2);
+  LD(e->epsum, H12_F_EPSUM, H12_NREW);
+  LD(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
+#undef LD
+  e->eplen = I[(size_t)H12_I_EPLEN * n + i];
+  int32_t pk = I[(size_t)H12_I_PACK * n + i];
+  for (int g = 0; g < 3; ++g) e->lag[g] = (pk >> (3 * g)) & 7;
+  e->since_reset = (pk >> 9) & 3;
+  e->is_heading = (pk >> 11) & 1;
+  e->is_standing = (pk >> 12) & 1;
+  e->p.cmask = (pk >> 13) & 0xFF;
+}
+static void env_store(float* F, int32_t* I, int n, int i, const orc_env* e) {
+#define ST(src, fld, cnt) for (int a = 0; a < (cnt); ++a) F[(size_t)((fld) + a) * n + i] = (float)(src)[a]
+  ST(e->p.pos, H12_F_POS, 3); ST(e->p.quat, H12_F_QUAT, 4); ST(e->p.vlin, H12_F_VLIN, 3);
+  ST(e->p.wang, H12_F_WANG, 3); ST(e->p.q, H12_F_Q, NJ); ST(e->p.qd, H12_F_QD, NJ);
+  ST(e->act, H12_F_ACT, NJ); ST(e->act_prev, H12_F_ACT_PREV, NJ); ST(e->cmd, H12_F_CMD, 3);
+  ST(&e->heading, H12_F_HEADING, 1); ST(&e->cmd_time, H12_F_CMD_TIME, 1); ST(e->air, H12_F_AIR, 2);
+  ST(e->con, H12_F_CONTACT, 2); ST(e->last_air, H12_F_LAST_AIR, 2); ST(e->last_con, H12_F_LAST_CONTACT, 2);
+  ST(e->epsum, H12_F_EPSUM, H12_NREW);
+  ST(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
+#undef ST
+  I[(size_t)H12_I_EPLEN * n + i] = e->eplen;
+  int32_t pk = 0;
+  for (int g = 0; g < 3; ++g) pk |= (e->lag[g] & 7) << (3 * g);
+  pk |= (e->since_reset & 3) << 9;
+  pk |= (e->is_heading & 1) << 11;
+  pk |= (e->is_standing & 1) << 12;
+  pk |= (e->p.cmask & 0xFF) << 13;
+  I[(size_t)H12_I_PACK * n + i] = pk;
+}
+
+static double wrap_to_pi(double x) {
+  double r = fmod(x, 2 * PI_D);
+  if (r < 0) r += 2 * PI_D;
+  return r > PI_D ? r - 2 * PI_D : r;
+}
+static double heading_w(const orc_phys* p) { /* atan2 of the body x axis in world */
+  m3 R;
+  quat_to_R(p->quat, R);
+  return atan2(R[1][0], R[0][0]);
+}
+
+/* UniformVelocityCommand._resample_command (upstream; in-repo twin utils/mdp/commands.py:19-59) */
+static void cmd_resample(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi) {
+  uint32_t r0[4], r1[4];
+  rng_block(c->seed, g, lo, hi, ST_CMD, 0, r0);
+  rng_block(c->seed, g, lo, hi, ST_CMD, 1, r1);
+  e->cmd[0] = uab(r0[0], c->cmd_lin_x[0], c->cmd_lin_x[1]);
+  e->cmd[1] = uab(r0[1], c->cmd_lin_y[0], c->cmd_lin_y[1]);
+  e->cmd[2] = uab(r0[2], c->cmd_ang_z[0], c->cmd_ang_z[1]);
+  e->heading = uab(r0[3], c->cmd_heading[0], c->cmd_heading[1]);
+  e->is_heading = (float)u01(r1[0]) <= c->rel_heading_envs;
+  e->is_standing = (float)u01(r1[1]) <= c->rel_standing_envs;
+  e->cmd_time = c->cmd_resample_time;
+}
+/* UniformVelocityCommand._update_command */
+static void cmd_update(const h12env_config* c, orc_env* e) {
+  if (e->is_heading) {
+    double err = wrap_to_pi(e->heading - heading_w(&e->p));
+    double w = c->heading_stiffness * err;
+    e->cmd[2] = w < c->cmd_ang_z[0] ? c->cmd_ang_z[0] : (w > c->cmd_ang_z[1] ? c->cmd_ang_z[1] : w);
+  }
+  if (e->is_standing) e->cmd[0] = e->cmd[1] = e->cmd[2] = 0;
+}
+
+/* _reset_idx: scene reset (delay lags, sensor), reset events, manager resets (cat_env.py:195-248) */
+static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env* e, int64_t g, uint32_t lo,
+                          uint32_t hi) {
+  uint32_t r0[4], r1[4];
+  rng_block(c->seed, g, lo, hi, ST_RESET, 0, r0);
+  rng_block(c->seed, g, lo, hi, ST_RESET, 1, r1);
+  memset(&e->p, 0, sizeof e->p);
+  e->p.pos[0] = uab(r0[0], c->reset_x[0], c->reset_x[1]);
+  e->p.pos[1] = uab(r0[1], c->reset_y[0], c->reset_y[1]);
+  e->p.pos[2] = m->root_height;
+  double yaw = uab(r0[2], c->reset_yaw[0], c->reset_yaw[1]);
+  e->p.quat[0] = cos(0.5 * (float)yaw);
+  e->p.quat[3] = sin(0.5 * (float)yaw);
+  for (int j = 0; j < NJ; ++j) {
+    double q = m->q_default[j];
+    double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+    if (q < mid - half) q = mid - half;
+    if (q > mid + half) q = mid + half;
+    e->p.q[j] = q;
+  }
+  int span = c->max_delay - c->min_delay + 1;
+  e->lag[0] = c->min_delay + (int)(r0[3] % (uint32_t)span);
+  e->lag[1] = c->min_delay + (int)(r1[0] % (uint32_t)span);
+  e->lag[2] = c->min_delay + (int)(r1[1] % (uint32_t)span);
+  e->since_reset = 0;
+  memset(e->act, 0, sizeof e->act);
+  memset(e->act_prev, 0, sizeof e->act_prev);
+  memset(e->air, 0, sizeof e->air);
+  memset(e->con, 0, sizeof e->con);
+  memset(e->last_air, 0, sizeof e->last_air);
+  memset(e->last_con, 0, sizeof e->last_con);
+  memset(e->epsum, 0, sizeof e->epsum);
+  e->eplen = 0;
+  cmd_resample(c, e, g, lo, hi);
+}
+
+/* observation frame (ObservationManager.compute_group, observation_manager.py:318-351) */
+static void obs_frame(const h12env_model* m, const h12env_config* c, const orc_env* e, int64_t g, uint32_t lo,
+                      uint32_t hi, double fr[H12_OBS_FRAME]) {
+  m3 R;
+  quat_to_R(e->p.quat, R);
+  double gw[3] = {0, 0, -1}, gb[3];
+  m3tv(R, gw, gb);
+  double noise[32];
+  for (int b = 0; b < 8; ++b) {
+    uint32_t r[4];
+    rng_block(c->seed, g, lo, hi, ST_OBS, b, r);
+    for (int a = 0; a < 4; ++a) noise[4 * b + a] = u01(r[a]);
+  }
+  int k = 0;
+  for (int a = 0; a < 3; ++a) fr[k++] = e->p.wang[a];
+  for (int a = 0; a < 3; ++a) fr[k++] = gb[a];
+  for (int a = 0; a < 3; ++a) fr[k++] = e->cmd[a];
+  for (int j = 0; j < NJ; ++j) fr[k++] = e->p.q[j] - m->q_default[j];
+  for (int j = 0; j < NJ; ++j) fr[k++] = e->p.qd[j];
+  for (int j = 0; j < NJ; ++j) fr[k++] = e->act[j];
+  if (c->enable_corruption) {
+    const int idx[30] = {0, 1, 2, 3, 4, 5, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20,
+                         21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32};
+    for (int t = 0; t < 30; ++t) {
+      double nmax = t < 3 ? c->noise_ang_vel : t < 6 ? c->noise_gravity : t < 18 ? c->noise_joint_pos : c->noise_joint_vel;
+      fr[idx[t]] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)noise[t]);
+    }
+  }
+}
+static const int TERM_DIM[6] = {3, 3, 3, NJ, NJ, NJ};
+static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* out, int fill) {
+  int off = 0, fo = 0;
+  for (int t = 0; t < 6; ++t) {
+    int d = TERM_DIM[t];
+    for (int h = 0; h < H12_NHIST; ++h)
+      for (int a = 0; a < d; ++a) {
+        double v;
+        if (fill || h == H12_NHIST - 1) v = fr[fo + a];
+        else v = prev[off + (h + 1) * d + a];
+        out[off + h * d + a] = (float)v;
+      }
+    off += d * H12_NHIST;
+    fo += d;
+  }
+}
+
+int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
+                  const uint8_t* mask, float* obs, uint64_t reset_counter) {
+  uint32_t lo = (uint32_t)reset_counter, hi = 0xFFFFFFFFu;
+  for (int i = 0; i < n; ++i) {
+    if (mask && !mask[i]) continue;
+    orc_env e;
+    memset(&e, 0, sizeof e);
+    int64_t g = env_offset + i;
+    env_reset_one(m, c, &e, g, lo, hi);
+    double fr[H12_OBS_FRAME];
+    obs_frame(m, c, &e, g, lo, hi, fr);
+    obs_write(fr, 0, obs + (size_t)i * H12_NOBS, 1);
+    env_store(F, I, n, i, &e);
+  }
+  return 0;
+}
+
+static double sq(double x) { return x * x; }
+
+int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
+                 const float* actions, const float* obs_prev, float* obs, float* rew, uint8_t* terminated,
+                 uint8_t* truncated, float* log_acc, float* applied_torque, float* foot_force, int64_t step_index,
+                 int n_threads) {
+  const uint32_t lo = (uint32_t)step_index, hi = (uint32_t)((uint64_t)step_index >> 32);
+  const int dec = c->decimation;
+  const double dt = c->physics_dt, step_dt = c->physics_dt * dec;
+  int err = 0;
+#ifdef _OPENMP
+  if (n_threads < 1) n_threads = 1;
+#pragma omp parallel for num_threads(n_threads) schedule(static)
+#endif
+  for (int i = 0; i < n; ++i) {
+    orc_env e;
+    env_load(F, I, n, i, &e);
+    const int64_t g = env_offset + i;
+    double a_t[NJ], a_t1[NJ], a_t2[NJ];
+    for (int j = 0; j < NJ; ++j) {
+      a_t[j] = actions[(size_t)i * NJ + j];
+      a_t1[j] = e.act[j];
+      a_t2[j] = e.act_prev[j];
+    }
+    /* ActionManager.process_action: prev_action <- action; action <- a */
+    memcpy(e.act_prev, e.act, sizeof e.act);
+    memcpy(e.act, a_t, sizeof a_t);
+    double tau_applied[NJ] = {0}, jacc[NJ] = {0};
+    double fmax_knee[2] = {0, 0}, fmax_torso = 0, fmax_foot[2] = {0, 0}, flast_foot[2] = {0, 0};
+    for (int s = 0; s < dec; ++s) {
+      double tau[NJ];
+      if (c->mode == H12_MODE_ISAACLAB) {
+        /* DelayedPDActuator.compute: delay buffer read at lag (clamped to pushes-1) */
+        int npush = e.since_reset * dec + s + 1;
+        for (int j = 0; j < NJ; ++j) {
+          int L = e.lag[c->delay_group[j]];
+          if (L > npush - 1) L = npush - 1;
+          double a = L <= s ? a_t[j] : (L <= s + dec ? a_t1[j] : a_t2[j]);
+          double tgt = m->q_default[j] + c->action_scale * (double)(float)a;
+          double v = c->kp[j] * (tgt - e.p.q[j]) + c->kd[j] * (0.0 - e.p.qd[j]);
+          double E = c->effort_limit[j];
+          tau[j] = v > E ? E : (v < -E ? -E : v);
+        }
+      } else {
+        for (int j = 0; j < NJ; ++j) {
+          double tgt = m->q_default[j] + c->action_scale * a_t[j];
+          double v = c->kp[j] * (tgt - e.p.q[j]) - c->kd[j] * e.p.qd[j];
+          double E = m->mj_frc_limit[j];
+          tau[j] = v > E ? E : (v < -E ? -E : v);
+        }
+      }
+      double qd0[NJ];
+      memcpy(qd0, e.p.qd, sizeof qd0);
+      orc_contact_report rep;
+      if (orc_physics_step(m, c, &e.p, tau, 1, 1, &rep)) err = -1;
+      memcpy(tau_applied, tau, sizeof tau);
+      for (int j = 0; j < NJ; ++j) jacc[j] = (e.p.qd[j] - qd0[j]) / dt;
+      /* ContactSensor._update_buffers_impl: air / contact time (history 3, threshold 1 N) */
+      for (int f = 0; f < 2; ++f) {
+        double fn = sqrt(sq(rep.foot_force[f][0]) + sq(rep.foot_force[f][1]) + sq(rep.foot_force[f][2]));
+        int is_c = fn > c->contact_threshold;
+        int first_c = (e.air[f] > 0) && is_c;
+        int first_d = (e.con[f] > 0) && !is_c;
+        if (first_c) e.last_air[f] = e.air[f] + dt;
+        e.air[f] = is_c ? 0.0 : e.air[f] + dt;
+        if (first_d) e.last_con[f] = e.con[f] + dt;
+        e.con[f] = is_c ? e.con[f] + dt : 0.0;
+        flast_foot[f] = fn;
+        if (s >= dec - 3 && fn > fmax_foot[f]) fmax_foot[f] = fn;
+      }
+      if (s >= dec - 3) {
+        for (int f = 0; f < 2; ++f) {
+          double fk = sqrt(sq(rep.knee_force[f][0]) + sq(rep.knee_force[f][1]) + sq(rep.knee_force[f][2]));
+          if (fk > fmax_knee[f]) fmax_knee[f] = fk;
+        }
+        double ft = sqrt(sq(rep.torso_force[0]) + sq(rep.torso_force[1]) + sq(rep.torso_force[2]));
+        if (ft > fmax_torso) fmax_torso = ft;
+      }
+    }
+    e.eplen += 1;
+    /* terminations: time_out, illegal_contact (velocity_env_cfg.py:264-268) */
+    int tout = e.eplen >= c->max_episode_length;
+    int term = 0;
+    if (c->illegal_contact_knees && (fmax_knee[0] > c->contact_threshold || fmax_knee[1] > c->contact_threshold)) term = 1;
+    if (c->illegal_contact_torso && fmax_torso > c->contact_threshold) term = 1;
+    /* rewards (pre-reset state) */
+    m3 R;
+    quat_to_R(e.p.quat, R);
+    double wb[3] = {e.p.wang[0], e.p.wang[1], e.p.wang[2]}, ww[3];
+    m3v(R, wb, ww);
+    double gw[3] = {0, 0, -1}, gb[3];
+    m3tv(R, gw, gb);
+    /* root (COM) linear velocity in world: v_origin + w x (R c) */
+    double cw[3], bc[3] = {m->base_com[0], m->base_com[1], m->base_com[2]}, wxc[3], vcom[3];
+    m3v(R, bc, cw);
+    cross3(ww, cw, wxc);
+    for (int a = 0; a < 3; ++a) vcom[a] = e.p.vlin[a] + wxc[a];
+    double yaw = atan2(R[1][0], R[0][0]);
+    double cy = cos(yaw), sy = sin(yaw);
+    double vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
+    double terms[H12_NREW];
+    double std2 = c->track_std * c->track_std;
+    terms[H12_R_TRACK_LIN_VEL_XY] = exp(-(sq(e.cmd[0] - vy0) + sq(e.cmd[1] - vy1)) / std2);
+    terms[H12_R_TRACK_ANG_VEL_Z] = exp(-sq(e.cmd[2] - ww[2]) / std2);
+    terms[H12_R_ANG_VEL_XY_L2] = sq(wb[0]) + sq(wb[1]);
+    double s_t = 0, s_a = 0, s_r = 0, s_lim = 0, s_dev = 0;
+    for (int j = 0; j < NJ; ++j) {
+      s_t += sq(tau_applied[j]);
+      s_a += sq(jacc[j]);
+      s_r += sq(e.act[j] - e.act_prev[j]);
+    }
+    terms[H12_R_DOF_TORQUES_L2] = s_t;
+    terms[H12_R_DOF_ACC_L2] = s_a;
+    terms[H12_R_ACTION_RATE_L2] = s_r;
+    /* feet_air_time_positive_biped (mdp/rewards.py:38-62) */
+    {
+      int inc[2] = {e.con[0] > 0, e.con[1] > 0};
+      double mode_t[2] = {inc[0] ? e.con[0] : e.air[0], inc[1] ? e.con[1] : e.air[1]};
+      int single = (inc[0] + inc[1]) == 1;
+      double r = single ? (mode_t[0] < mode_t[1] ? mode_t[0] : mode_t[1]) : 0.0;
+      if (r > c->air_time_threshold) r = c->air_time_threshold;
+      double cn = sqrt(sq(e.cmd[0]) + sq(e.cmd[1]));
+      terms[H12_R_FEET_AIR_TIME] = cn > 0.1 ? r : 0.0;
+    }
+    terms[H12_R_FLAT_ORIENTATION_L2] = sq(gb[0]) + sq(gb[1]);
+    for (int f = 0; f < 2; ++f)
+      for (int k = 4; k < 6; ++k) { /* ankle pitch, ankle roll */
+        int j = 6 * f + k;
+        double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+        double lo_s = mid - half, hi_s = mid + half, q = e.p.q[j];
+        s_lim += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
+      }
+    terms[H12_R_DOF_POS_LIMITS] = s_lim;
+    terms[H12_R_TERMINATION] = term ? 1.0 : 0.0;
+    {
+      /* feet_slide: |v_xy| of the ankle-roll link COM where max_h |F| > 1 */
+      kin_t k;
+      kinematics(m, &e.p, &k);
+      double fs = 0;
+      for (int f = 0; f < 2; ++f) {
+        int b = 6 * f + 6;
+        if (!(fmax_foot[f] > 1.0)) continue;
+        double cl[3] = {m->link_com[b - 1][0], m->link_com[b - 1][1], m->link_com[b - 1][2]}, vl[3], vw[3];
+        cross3(k.v[b], cl, vl);
+        for (int a = 0; a < 3; ++a) vl[a] += k.v[b][3 + a];
+        m3v(k.R[b], vl, vw);
+        fs += sqrt(sq(vw[0]) + sq(vw[1]));
+      }
+      terms[H12_R_FEET_SLIDE] = fs;
+    }
+    for (int f = 0; f < 2; ++f) {
+      int j0 = 6 * f + 0, j2 = 6 * f + 2; /* hip yaw, hip roll */
+      s_dev += fabs(e.p.q[j0] - m->q_default[j0]) + fabs(e.p.q[j2] - m->q_default[j2]);
+    }
+    terms[H12_R_JOINT_DEV_HIP] = s_dev;
+    double r = 0;
+    for (int t = 0; t < H12_NREW; ++t) {
+      double v = terms[t] * c->rew_w[t] * step_dt;
+      r += v;
+      e.epsum[t] += v;
+    }
+    rew[i] = (float)r;
+    terminated[i] = (uint8_t)term;
+    truncated[i] = (uint8_t)tout;
+    if (applied_torque) for (int j = 0; j < NJ; ++j) applied_torque[(size_t)i * NJ + j] = (float)tau_applied[j];
+    if (foot_force) { foot_force[2 * i] = (float)flast_foot[0]; foot_force[2 * i + 1] = (float)flast_foot[1]; }
+    int reset = term || tout;
+    if (reset) {
+      if (log_acc) {
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+          for (int t = 0; t < H12_NREW; ++t) log_acc[t] += (float)e.epsum[t];
+          log_acc[12] += 1.0f;
+          log_acc[13] += (float)tout;
+          log_acc[14] += (float)term;
+        }
+      }
+      env_reset_one(m, c, &e, g, lo, hi);
+    } else {
+      e.since_reset = e.since_reset < 2 ? e.since_reset + 1 : 2;
+    }
+    /* CommandTerm.compute(dt) */
+    e.cmd_time -= step_dt;
+    if (e.cmd_time <= 0) cmd_resample(c, &e, g, lo, hi);
+    cmd_update(c, &e);
+    double fr[H12_OBS_FRAME];
+    obs_frame(m, c, &e, g, lo, hi, fr);
+    obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, reset);
+    env_store(F, I, n, i, &e);
+  }
+  return err;
+}
+
+int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, float* F, int32_t* I,
+                         const float* q_ref, int n_substeps) {
+  for (int i = 0; i < n; ++i) {
+    orc_env e;
+    memset(&e, 0, sizeof e);
+    int32_t pk = I ? I[(size_t)H12_I_PACK * n + i] : 0;
+    int32_t cm = (pk >> 13) & 0xFF;
+    int32_t* cmask = &cm;
+    /* only physics fields are used */
+    for (int a = 0; a < 3; ++a) e.p.pos[a] = F[(size_t)(H12_F_POS + a) * n + i];
+    for (int a = 0; a < 4; ++a) e.p.quat[a] = F[(size_t)(H12_F_QUAT + a) * n + i];
+    for (int a = 0; a < 3; ++a) e.p.vlin[a] = F[(size_t)(H12_F_VLIN + a) * n + i];
+    for (int a = 0; a < 3; ++a) e.p.wang[a] = F[(size_t)(H12_F_WANG + a) * n + i];
+    for (int j = 0; j < NJ; ++j) { e.p.q[j] = F[(size_t)(H12_F_Q + j) * n + i]; e.p.qd[j] = F[(size_t)(H12_F_QD + j) * n + i]; }
+    for (int a = 0; a < 16; ++a) (&e.p.anchor[0][0][0])[a] = F[(size_t)(H12_F_ANCHOR + a) * n + i];
+    e.p.cmask = *cmask;
+    for (int t = 0; t < n_substeps; ++t) {
+      double tau[NJ];
+      for (int j = 0; j < NJ; ++j) {
+        double v = c->kp[j] * (q_ref[(size_t)i * NJ + j] - e.p.q[j]) - c->kd[j] * e.p.qd[j];
+        double E = c->mode == H12_MODE_MUJOCO ? m->mj_frc_limit[j] : c->effort_limit[j];
+        tau[j] = v > E ? E : (v < -E ? -E : v);
+      }
+      if (orc_physics_step(m, c, &e.p, tau, 1, 1, 0)) return -1;
+    }
+    for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_POS + a) * n + i] = (float)e.p.pos[a];
+    for (int a = 0; a < 4; ++a) F[(size_t)(H12_F_QUAT + a) * n + i] = (float)e.p.quat[a];
+    for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_VLIN + a) * n + i] = (float)e.p.vlin[a];
+    for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_WANG + a) * n + i] = (float)e.p.wang[a];
+    for (int j = 0; j < NJ; ++j) { F[(size_t)(H12_F_Q + j) * n + i] = (float)e.p.q[j]; F[(size_t)(H12_F_QD + j) * n + i] = (float)e.p.qd[j]; }
+    for (int a = 0; a < 16; ++a) F[(size_t)(H12_F_ANCHOR + a) * n + i] = (float)(&e.p.anchor[0][0][0])[a];
+    if (I) I[(size_t)H12_I_PACK * n + i] = (pk & ~(0xFF << 13)) | ((e.p.cmask & 0xFF) << 13);
+  }
+  return 0;
+}

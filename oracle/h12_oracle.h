@@ -1,0 +1,87 @@
+/*
+ * h12_oracle.h — CPU restatement (TEST INFRASTRUCTURE ONLY) of the H1-2 Flat velocity env step.
+ *
+ * This is the parity oracle for the HIP library: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path (h12env python package -> libh12env.so)
+ * never links or calls it.
+ *
+ * It restates, in double precision and with deliberately different algorithms from the
+ * GPU kernel where that strengthens the check:
+ *   - rigid-body dynamics: CRBA + RNEA + dense Cholesky (MuJoCo's own formulation, the
+ *     sim2sim oracle path packages/biped_deploy/biped_deploy/simulator/sim_mujoco.py:39-44,109)
+ *     and, separately, Featherstone ABA (cross-checked against CRBA in tests);
+ *   - the explicit delayed PD actuator (packages/biped_assets/biped_assets/robots/h12.py:58-112;
+ *     delay indexing = CircularBuffer.__getitem__, .../utils/history/circular_buffer.py:139-170);
+ *   - the MDP terms of Isaac-Velocity-Flat-H12_12dof-v0 (rewards, terminations, resets,
+ *     commands, observations + 10-frame history) as restated in SURVEY.md §8(a).
+ *
+ * Parity status: the algorithm of record (PhysX / MuJoCo / IsaacLab managers) is not present
+ * in this container, so physics parity against it is UNPINNED; the oracle itself is pinned
+ * by the reference's importable pieces (CircularBuffer, deploy ObservationHandler) through
+ * tests/golden fixtures, and by physical invariants (energy, momentum, ABA == CRBA).
+ */
+#ifndef H12_ORACLE_H
+#define H12_ORACLE_H
+#include <stdint.h>
+#include "../include/h12env.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* physics state in double (MuJoCo layout: pos, quat(wxyz), v_world, w_body, q, qd) */
+typedef struct orc_phys {
+  double pos[3], quat[4], vlin[3], wang[3], q[H12_NJ], qd[H12_NJ];
+  double anchor[2][H12_NFOOT_PTS][2]; /* sole-sphere stiction anchors (world x, y) */
+  int32_t cmask;                      /* bit 4f+p: sole sphere p of foot f was in contact */
+} orc_phys;
+
+/* per physics-step contact report */
+typedef struct orc_contact_report {
+  double foot_force[2][3];   /* net world force on each foot */
+  double knee_force[2][3];
+  double torso_force[3];
+} orc_contact_report;
+
+/* ---- single-env physics (double) ---- */
+/* Forward dynamics: generalised acceleration nudot = (wdot_b, vdot_b (spatial), qdd).
+ * tau: joint torques; algo 0 = CRBA+Cholesky, 1 = ABA.  dt_impl: implicit damping dt (0 = none).
+ * with_contact: evaluate penalty contact forces (report may be NULL). */
+int orc_forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s,
+                         const double tau[H12_NJ], int algo, double dt_impl, int with_contact,
+                         double nudot[18], orc_contact_report* rep);
+/* Joint-space mass matrix (18 x 18, row major, base coords (w_b, v_b)), armature included. */
+int orc_mass_matrix(const h12env_model* m, const orc_phys* s, double M[18 * 18]);
+/* Total mechanical energy (kinetic + potential), linear + angular momentum about the world origin. */
+int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy, double lin_mom[3],
+                        double ang_mom[3]);
+/* One physics step of length c->physics_dt split into c->inner_steps, holding tau_pd;
+ * joint limits (+ contact unless disabled) re-evaluated per inner step.  Averaged contact
+ * forces are written to rep (may be NULL). */
+int orc_physics_step(const h12env_model* m, const h12env_config* c, orc_phys* s, const double tau_pd[H12_NJ],
+                     int with_contact, int algo, orc_contact_report* rep);
+/* MuJoCo sim2sim loop (h12_mujoco.py:55-67): n_steps physics steps, PD to q_ref recomputed
+ * every step, clamp at MJCF actuatorfrcrange.  traj (may be NULL) gets q after every step. */
+int orc_mujoco_rollout(const h12env_model* m, const h12env_config* c, orc_phys* s, const double* q_ref,
+                       int n_steps, int with_contact, int algo, double* traj_q);
+
+/* ---- batched env API on the GPU workspace layout (field-major SoA floats / ints) ----
+ * These mirror h12env_reset / h12env_step on host arrays so tests can feed both sides the
+ * same state.  Compute is double; state storage is float (same as the workspace). */
+int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset,
+                  float* fstate, int32_t* istate, const uint8_t* mask, float* obs, uint64_t reset_counter);
+int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* fstate,
+                 int32_t* istate, const float* actions, const float* obs_prev, float* obs, float* rew,
+                 uint8_t* terminated, uint8_t* truncated, float* log_acc, float* applied_torque,
+                 float* foot_force, int64_t step_index, int n_threads);
+/* Physics-only batched step (h12env_step_physics): n_substeps with held q_ref per env. */
+int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, float* fstate, int32_t* istate,
+                         const float* q_ref, int n_substeps);
+
+/* RNG shared by both sides (Philox4x32-10). */
+void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

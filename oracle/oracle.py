@@ -1,0 +1,185 @@
+"""ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+The product path (h12env -> libh12env.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent
+sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
+
+from h12env._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, H12Config, H12Model  # noqa: E402
+
+LIB = HERE / "liboracle.so"
+
+
+class Phys(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("quat", C.c_double * 4), ("vlin", C.c_double * 3),
+                ("wang", C.c_double * 3), ("q", C.c_double * NJ), ("qd", C.c_double * NJ),
+                ("anchor", C.c_double * 16), ("cmask", C.c_int32)]
+
+    def to_numpy(self) -> np.ndarray:
+        """37 physics coordinates + 16 anchors + contact mask (as float)."""
+        return np.concatenate([np.array(self.pos), np.array(self.quat), np.array(self.vlin), np.array(self.wang),
+                               np.array(self.q), np.array(self.qd), np.array(self.anchor), [float(self.cmask)]])
+
+    @classmethod
+    def from_numpy(cls, x) -> "Phys":
+        x = np.asarray(x, dtype=np.float64)
+        p = cls()
+        p.pos[:] = x[0:3]
+        p.quat[:] = x[3:7]
+        p.vlin[:] = x[7:10]
+        p.wang[:] = x[10:13]
+        p.q[:] = x[13:25]
+        p.qd[:] = x[25:37]
+        if x.size >= 54:
+            p.anchor[:] = x[37:53]
+            p.cmask = int(x[53])
+        return p
+
+
+class Report(C.Structure):
+    _fields_ = [("foot_force", (C.c_double * 3) * 2), ("knee_force", (C.c_double * 3) * 2),
+                ("torso_force", C.c_double * 3)]
+
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = C.CDLL(str(LIB))
+        vp, dp = C.c_void_p, C.POINTER(C.c_double)
+        M, Cf = C.POINTER(H12Model), C.POINTER(H12Config)
+        L.orc_forward_dynamics.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_double, C.c_int, dp, C.POINTER(Report)]
+        L.orc_mass_matrix.argtypes = [M, C.POINTER(Phys), dp]
+        L.orc_energy_momentum.argtypes = [M, C.POINTER(Phys), dp, dp, dp]
+        L.orc_physics_step.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.POINTER(Report)]
+        L.orc_mujoco_rollout.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.c_int, dp]
+        L.orc_env_reset.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, C.c_uint64]
+        L.orc_env_step.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int64,
+                                   C.c_int]
+        L.orc_env_step_physics.argtypes = [M, Cf, C.c_int, vp, vp, vp, C.c_int]
+        L.orc_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.orc_philox.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _d(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def philox(seed, c0, c1, c2, c3):
+    out = (C.c_uint32 * 4)()
+    lib().orc_philox(seed, c0, c1, c2, c3, out)
+    return list(out)
+
+
+def forward_dynamics(model, cfg, state, tau, algo=0, dt_impl=0.0, contact=True):
+    s = Phys.from_numpy(state)
+    tau = np.ascontiguousarray(tau, dtype=np.float64)
+    nd = np.zeros(18)
+    rep = Report()
+    rc = lib().orc_forward_dynamics(C.byref(model), C.byref(cfg), C.byref(s), _d(tau), algo, dt_impl, int(contact),
+                                    _d(nd), C.byref(rep))
+    if rc:
+        raise RuntimeError("oracle forward dynamics failed")
+    return nd, rep
+
+
+def mass_matrix(model, state):
+    s = Phys.from_numpy(state)
+    M = np.zeros((18, 18))
+    lib().orc_mass_matrix(C.byref(model), C.byref(s), _d(M))
+    return M
+
+
+def energy_momentum(model, state):
+    s = Phys.from_numpy(state)
+    e = np.zeros(1)
+    lin = np.zeros(3)
+    ang = np.zeros(3)
+    lib().orc_energy_momentum(C.byref(model), C.byref(s), _d(e), _d(lin), _d(ang))
+    return float(e[0]), lin, ang
+
+
+def physics_step(model, cfg, state, tau_pd, contact=True, algo=1):
+    s = Phys.from_numpy(state)
+    tau = np.ascontiguousarray(tau_pd, dtype=np.float64)
+    rep = Report()
+    if lib().orc_physics_step(C.byref(model), C.byref(cfg), C.byref(s), _d(tau), int(contact), algo, C.byref(rep)):
+        raise RuntimeError("oracle physics step failed")
+    return s.to_numpy(), rep
+
+
+def mujoco_rollout(model, cfg, state, q_ref, n_steps, contact=False, algo=0):
+    s = Phys.from_numpy(state)
+    q_ref = np.ascontiguousarray(q_ref, dtype=np.float64)
+    traj = np.zeros((n_steps, NJ))
+    if lib().orc_mujoco_rollout(C.byref(model), C.byref(cfg), C.byref(s), _d(q_ref), n_steps, int(contact), algo,
+                                _d(traj)):
+        raise RuntimeError("oracle rollout failed")
+    return s.to_numpy(), traj
+
+
+class OracleEnv:
+    """Batched oracle env on the same SoA workspace layout as libh12env."""
+
+    def __init__(self, model, cfg, n, env_offset=0):
+        self.model, self.cfg, self.n, self.env_offset = model, cfg, n, env_offset
+        self.F = np.zeros((NF_FLOAT, n), dtype=np.float32)
+        self.I = np.zeros((NF_INT, n), dtype=np.int32)
+        self.obs = np.zeros((n, NOBS), dtype=np.float32)
+        self.reset_counter = 0
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        lib().orc_env_reset(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, _p(self.F), _p(self.I),
+                            _p(m), _p(self.obs), self.reset_counter)
+        self.reset_counter += 1
+        return self.obs.copy()
+
+    def step(self, actions, step_index, n_threads=1):
+        a = np.ascontiguousarray(actions, dtype=np.float32)
+        obs = np.empty_like(self.obs)
+        rew = np.empty(self.n, dtype=np.float32)
+        term = np.empty(self.n, dtype=np.uint8)
+        trunc = np.empty(self.n, dtype=np.uint8)
+        log = np.zeros(NLOG, dtype=np.float32)
+        tq = np.empty((self.n, NJ), dtype=np.float32)
+        ff = np.empty((self.n, 2), dtype=np.float32)
+        rc = lib().orc_env_step(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, _p(self.F), _p(self.I),
+                                _p(a), _p(self.obs), _p(obs), _p(rew), _p(term), _p(trunc), _p(log), _p(tq), _p(ff),
+                                step_index, n_threads)
+        if rc:
+            raise RuntimeError("oracle env step failed")
+        self.obs = obs
+        return obs.copy(), rew, term.astype(bool), trunc.astype(bool), dict(log=log, applied_torque=tq, foot_force=ff)
+
+    def step_physics(self, q_ref, n_substeps):
+        q = np.ascontiguousarray(q_ref, dtype=np.float32)
+        if lib().orc_env_step_physics(C.byref(self.model), C.byref(self.cfg), self.n, _p(self.F), _p(self.I), _p(q),
+                                      n_substeps):
+            raise RuntimeError("oracle physics failed")
