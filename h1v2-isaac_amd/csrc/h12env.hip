@@ -959,6 +959,30 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, St
   if (n_rows > 0) write_obs_block(A.obs, A.obs, e0, n_rows, s_frame, s_fill, s_write);
 }
 
+// ObservationManager.compute() outside step(): new frame from the current state, history shifted
+// (or filled where fill_mask[e]); RNG counter domain (observe call, 0xFFFFFFFE)
+__global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, StepArgs A) {
+  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
+  __shared__ int s_fill[ENVS_PER_BLOCK];
+  __shared__ int s_write[ENVS_PER_BLOCK];
+  const int lane_pair = threadIdx.x >> 1;
+  const int leg = threadIdx.x & 1;
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e = e0 + lane_pair;
+  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
+  if (e < W.n) {
+    EnvSt s;
+    load_env(W, e, leg, s);
+    obs_frame(P, s, leg, (uint32_t)(A.env_offset + e), A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
+    if (leg == 0) {
+      s_write[lane_pair] = 1;
+      s_fill[lane_pair] = A.reset_mask ? (int)A.reset_mask[e] : 0;
+    }
+  }
+  __syncthreads();
+  if (n_rows > 0) write_obs_block(A.obs_prev, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+}
+
 // parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
 __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
@@ -990,7 +1014,7 @@ struct Handle {
   bool own;
   int device;
   int64_t env_offset;
-  uint64_t reset_calls;
+  uint64_t reset_calls, observe_calls;
   double flops_per_env;
 };
 
@@ -1090,6 +1114,15 @@ int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_
 extern "C" {
 
 int h12env_abi_version(void) { return H12ENV_ABI_VERSION; }
+
+size_t h12env_sizeof_struct(int which) {
+  switch (which) {
+    case 0: return sizeof(h12env_model);
+    case 1: return sizeof(h12env_config);
+    case 2: return sizeof(h12env_step_out);
+    default: return 0;
+  }
+}
 const char* h12env_last_error(void) { return g_err; }
 
 int h12env_config_default(h12env_config* c) {
@@ -1161,6 +1194,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->device = device;
   h->env_offset = env_offset;
   h->reset_calls = 0;
+  h->observe_calls = 0;
   // counted algorithmic FLOPs per env step (DESIGN.md "Roofline"): per inner step and leg lane
   // ~2.9k (pass 1 0.6k, contacts 0.35k, pass 2 1.5k, pass 3 0.25k, integration 0.1k), base combine +
   // 6x6 solve ~0.3k per lane; MDP (rewards, resets, commands, obs, RNG) ~3k per env
@@ -1213,6 +1247,23 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.lo = (uint32_t)step_index;
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!obs_prev || !obs) return set_err(H12_E_ARG, "obs_prev and obs are required");
+  StepArgs A = {};
+  A.obs_prev = obs_prev;
+  A.obs = obs;
+  A.reset_mask = fill_mask;
+  A.env_offset = h->env_offset;
+  A.lo = (uint32_t)h->observe_calls;
+  A.hi = 0xFFFFFFFEu;
+  h->observe_calls++;
+  hipLaunchKernelGGL(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -174,6 +174,8 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_reset.restype = C.c_int
     lib.h12env_step.argtypes = [vp, vp, vp, C.POINTER(H12StepOut), C.c_int64, vp]
     lib.h12env_step.restype = C.c_int
+    lib.h12env_observe.argtypes = [vp, vp, vp, vp, vp]
+    lib.h12env_observe.restype = C.c_int
     lib.h12env_step_physics.argtypes = [vp, vp, C.c_int, vp]
     lib.h12env_step_physics.restype = C.c_int
     lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
@@ -186,6 +188,11 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_last_error.restype = C.c_char_p
     lib.h12env_abi_version.argtypes = []
     lib.h12env_abi_version.restype = C.c_int
+    lib.h12env_sizeof_struct.argtypes = [C.c_int]
+    lib.h12env_sizeof_struct.restype = C.c_size_t
+    for i, st in enumerate((H12Model, H12Config, H12StepOut)):
+        if lib.h12env_sizeof_struct(i) != C.sizeof(st):
+            raise H12EnvError(f"{st.__name__}: ctypes size {C.sizeof(st)} != C size {lib.h12env_sizeof_struct(i)}")
     if lib.h12env_abi_version() != ABI_VERSION:
         raise H12EnvError(f"libh12env ABI {lib.h12env_abi_version()} != python mirror {ABI_VERSION}")
     if path is None:
@@ -201,6 +208,6 @@ def check(lib, rc: int, what: str):
 
 EXPORTED_SYMBOLS = [
     "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
-    "h12env_step", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
-    "h12env_last_error", "h12env_abi_version",
+    "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
+    "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct",
 ]

@@ -332,6 +332,17 @@ class H12VelocityEnv:
         check(self._lib, self._lib.h12env_step_physics(self._h, C.c_void_p(q.data_ptr()), int(n_substeps),
                                                        self._stream()), "h12env_step_physics")
 
+    def observe(self, fill_mask: torch.Tensor | None = None):
+        """ObservationManager.compute(): append a frame of the current state to the history."""
+        prev = self._obs[self._k]
+        self._k ^= 1
+        out = self._obs[self._k]
+        fm = None if fill_mask is None else fill_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        check(self._lib, self._lib.h12env_observe(self._h, C.c_void_p(prev.data_ptr()), C.c_void_p(out.data_ptr()),
+                                                  None if fm is None else C.c_void_p(fm.data_ptr()),
+                                                  self._stream()), "h12env_observe")
+        return {"policy": out}
+
     def get_observations(self):
         return {"policy": self._obs[self._k]}
 

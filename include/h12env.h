@@ -194,6 +194,10 @@ int h12env_reset(h12env* h, const uint8_t* mask, float* obs, void* stream);
  * out->obs.  step_index: common_step_counter after increment (>= 1). */
 int h12env_step(h12env* h, const float* actions, const float* obs_prev, const h12env_step_out* out,
                 int64_t step_index, void* stream);
+/* ObservationManager.compute() outside step(): appends one frame of the current state to every
+ * env's history (obs_prev -> obs, may alias); fill_mask[i] != 0 fills env i's history with the frame
+ * (the first push after a reset).  fill_mask may be NULL. */
+int h12env_observe(h12env* h, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream);
 /* Parity hook: n_substeps physics steps with a held joint target q_ref (N x 12) using the
  * configured mode (PD, limits, contact), no MDP.  Mirrors H12Mujoco.step. */
 int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* stream);
@@ -204,6 +208,9 @@ int h12env_num_envs(const h12env* h);
 int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_env);
 const char* h12env_last_error(void);
 int h12env_abi_version(void);
+/* sizeof of the ABI structs as compiled (0 = h12env_model, 1 = h12env_config, 2 = h12env_step_out),
+ * so bindings can verify their mirrors; 0 for an unknown id. */
+size_t h12env_sizeof_struct(int which);
 
 #ifdef __cplusplus
 }

@@ -732,6 +732,35 @@ static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* 
   }
 }
 
+/* DelayBuffer = CircularBuffer(max_delay + 1)[lag] (circular_buffer.py:139-170) with one push per
+ * physics step and a constant target within an env step: the delayed target of substep s is the
+ * target of env step t - src.  The first push after a reset fills the ring (:131-135), which the
+ * clamp lag <= pushes - 1 reproduces. */
+int orc_delay_source(int lag, int since_reset, int substep, int decimation) {
+  int npush = since_reset * decimation + substep + 1;
+  int L = lag > npush - 1 ? npush - 1 : lag;
+  return L <= substep ? 0 : (L <= substep + decimation ? 1 : 2);
+}
+
+void orc_history_write(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill) {
+  obs_write(frame, prev_row, out_row, fill);
+}
+
+/* ObservationManager.compute() outside step(): one new frame per env, history shifted (or filled
+ * where fill_mask[i]); noise stream keyed by (env, counter, 0xFFFFFFFE). */
+int orc_env_observe(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
+                    const float* obs_prev, float* obs, const uint8_t* fill_mask, uint64_t counter) {
+  uint32_t lo = (uint32_t)counter, hi = 0xFFFFFFFEu;
+  for (int i = 0; i < n; ++i) {
+    orc_env e;
+    env_load(F, I, n, i, &e);
+    double fr[H12_OBS_FRAME];
+    obs_frame(m, c, &e, env_offset + i, lo, hi, fr);
+    obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, fill_mask ? fill_mask[i] : 0);
+  }
+  return 0;
+}
+
 int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
                   const uint8_t* mask, float* obs, uint64_t reset_counter) {
   uint32_t lo = (uint32_t)reset_counter, hi = 0xFFFFFFFFu;
@@ -782,11 +811,9 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       double tau[NJ];
       if (c->mode == H12_MODE_ISAACLAB) {
         /* DelayedPDActuator.compute: delay buffer read at lag (clamped to pushes-1) */
-        int npush = e.since_reset * dec + s + 1;
         for (int j = 0; j < NJ; ++j) {
-          int L = e.lag[c->delay_group[j]];
-          if (L > npush - 1) L = npush - 1;
-          double a = L <= s ? a_t[j] : (L <= s + dec ? a_t1[j] : a_t2[j]);
+          int src = orc_delay_source(e.lag[c->delay_group[j]], e.since_reset, s, dec);
+          double a = src == 0 ? a_t[j] : (src == 1 ? a_t1[j] : a_t2[j]);
           double tgt = m->q_default[j] + c->action_scale * (double)(float)a;
           double v = c->kp[j] * (tgt - e.p.q[j]) + c->kd[j] * (0.0 - e.p.qd[j]);
           double E = c->effort_limit[j];

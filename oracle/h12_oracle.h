@@ -78,6 +78,14 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
 int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, float* fstate, int32_t* istate,
                          const float* q_ref, int n_substeps);
 
+/* Observation of the current state (ObservationManager.compute outside step), fill_mask may be NULL. */
+int orc_env_observe(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* fstate,
+                    int32_t* istate, const float* obs_prev, float* obs, const uint8_t* fill_mask, uint64_t counter);
+/* Delayed-target source of substep `substep`: 0 = a_t, 1 = a_{t-1}, 2 = a_{t-2}. */
+int orc_delay_source(int lag, int since_reset, int substep, int decimation);
+/* One history update of a 450-float observation row (term-major, oldest -> newest). */
+void orc_history_write(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill);
+
 /* RNG shared by both sides (Philox4x32-10). */
 void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]);
 

@@ -77,6 +77,11 @@ def lib():
         L.orc_env_step.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int64,
                                    C.c_int]
         L.orc_env_step_physics.argtypes = [M, Cf, C.c_int, vp, vp, vp, C.c_int]
+        L.orc_env_observe.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, C.c_uint64]
+        L.orc_delay_source.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_delay_source.restype = C.c_int
+        L.orc_history_write.argtypes = [dp, vp, vp, C.c_int]
+        L.orc_history_write.restype = None
         L.orc_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
         L.orc_philox.restype = None
         _lib = L
@@ -89,6 +94,18 @@ def _p(a):
 
 def _d(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def delay_source(lag, since_reset, substep, decimation):
+    return lib().orc_delay_source(lag, since_reset, substep, decimation)
+
+
+def history_write(frame, prev_row, fill):
+    frame = np.ascontiguousarray(frame, dtype=np.float64)
+    prev = np.ascontiguousarray(prev_row, dtype=np.float32)
+    out = np.empty(NOBS, dtype=np.float32)
+    lib().orc_history_write(_d(frame), _p(prev), _p(out), int(fill))
+    return out
 
 
 def philox(seed, c0, c1, c2, c3):
@@ -153,6 +170,7 @@ class OracleEnv:
         self.I = np.zeros((NF_INT, n), dtype=np.int32)
         self.obs = np.zeros((n, NOBS), dtype=np.float32)
         self.reset_counter = 0
+        self.observe_counter = 0
 
     def reset(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
@@ -177,6 +195,15 @@ class OracleEnv:
             raise RuntimeError("oracle env step failed")
         self.obs = obs
         return obs.copy(), rew, term.astype(bool), trunc.astype(bool), dict(log=log, applied_torque=tq, foot_force=ff)
+
+    def observe(self, fill_mask=None):
+        m = None if fill_mask is None else np.ascontiguousarray(fill_mask, dtype=np.uint8)
+        out = np.empty_like(self.obs)
+        lib().orc_env_observe(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, _p(self.F), _p(self.I),
+                              _p(self.obs), _p(out), _p(m), self.observe_counter)
+        self.observe_counter += 1
+        self.obs = out
+        return out.copy()
 
     def step_physics(self, q_ref, n_substeps):
         q = np.ascontiguousarray(q_ref, dtype=np.float32)

@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library loads, exports every symbol include/h12env.h declares, its struct layouts
+match the ctypes mirror, and its defaults equal the Python restatement of the Flat cfg.
+No compute entry point is called (no GPU here)."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from h12env import H12FlatEnvCfg
+from h12env._abi import EXPORTED_SYMBOLS, LIB_PATH, H12Config, H12Model, H12StepOut, load_library
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def header_functions():
+    src = (ROOT / "include" / "h12env.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(h12env_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    assert LIB_PATH.exists(), "build the extension first (__graft_entry__.build())"
+    lib = load_library()
+    names = header_functions()
+    assert set(names) == set(EXPORTED_SYMBOLS), (names, EXPORTED_SYMBOLS)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_struct_sizes_match():
+    lib = load_library()
+    for i, st in enumerate((H12Model, H12Config, H12StepOut)):
+        assert lib.h12env_sizeof_struct(i) == C.sizeof(st)
+    assert lib.h12env_sizeof_struct(7) == 0
+
+
+def test_state_bytes_and_abi():
+    lib = load_library()
+    assert lib.h12env_abi_version() == 1
+    assert lib.h12env_state_bytes(0) == 0
+    assert lib.h12env_state_bytes(4096) == (102 + 2) * 4 * 4096
+
+
+def test_config_default_equals_python_cfg():
+    lib = load_library()
+    c = H12Config()
+    assert lib.h12env_config_default(C.byref(c)) == 0
+    p = H12FlatEnvCfg().to_c()
+    for name, _ in H12Config._fields_:
+        a, b = getattr(c, name), getattr(p, name)
+        if hasattr(a, "__len__"):
+            np.testing.assert_allclose(list(a), list(b), rtol=1e-6, err_msg=name)
+        else:
+            assert a == pytest.approx(b, rel=1e-6), name
+
+
+def test_create_rejects_bad_arguments_without_gpu(model):
+    """Argument validation happens before any HIP call."""
+    lib = load_library()
+    cfg = H12FlatEnvCfg().to_c()
+    h = C.c_void_p()
+    assert lib.h12env_create(C.byref(model), C.byref(cfg), 0, 0, 0, None, C.byref(h)) == -1
+    assert b"n_envs" in lib.h12env_last_error()
+    bad = H12FlatEnvCfg().to_c()
+    bad.max_delay = 9
+    assert lib.h12env_create(C.byref(model), C.byref(bad), 16, 0, 0, None, C.byref(h)) == -1
+    from h12env.model import build_model
+
+    m2 = build_model()
+    m2.link_mass[3] *= 1.5  # not the compiled H1-2 model
+    assert lib.h12env_create(C.byref(m2), C.byref(cfg), 16, 0, 0, None, C.byref(h)) == -1
+    assert b"compiled H1-2 model" in lib.h12env_last_error()
