@@ -166,6 +166,12 @@ H12_DEV void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t
   }
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
+// single-instruction transcendental / reciprocal / sqrt (v_sin, v_cos, v_rcp, v_sqrt: ~1 ulp, no
+// range-reduction or Newton sequences; arguments here are joint angles and positive magnitudes)
+H12_DEV void fsincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+H12_DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+H12_DEV float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 H12_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 H12_DEV float uab(uint32_t x, float a, float b) { return a + (b - a) * u01(x); }
 

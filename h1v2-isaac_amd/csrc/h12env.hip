@@ -14,6 +14,10 @@
 // copies bit-identical).  State is structure-of-arrays so each field access of a wave is one
 // contiguous segment; the 450-float observation rows are written cooperatively through LDS so each
 // wave stores its 32 consecutive rows as one contiguous, coalesced block.
+//
+// Register budget (one wave per SIMD, latency-bound): ABA keeps only the link spatial velocities
+// between passes (bias forces and velocity-product accelerations are recomputed from them), MDP state
+// is loaded after the physics loop, and the contact-sensor timers are replayed from per-substep flags.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -36,6 +40,7 @@ constexpr int ENVS_PER_BLOCK = 32;  // 64 lanes = 32 lane pairs
 constexpr int BLOCK = 64;
 // joint axes per leg link: hip yaw z, hip pitch y, hip roll x, knee y, ankle pitch y, ankle roll x
 constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
+constexpr int MAX_DEC = 32;         // contact flags of one env step are kept in a 32-bit mask
 
 thread_local char g_err[512] = "";
 int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -88,6 +93,8 @@ H12_DEV float soft_lo(const KParams& P, int k) {
 H12_DEV float soft_hi(const KParams& P, int k) {
   return 0.5f * (h12m::QLO[k] + h12m::QHI[k]) + 0.5f * (h12m::QHI[k] - h12m::QLO[k]) * P.soft_f;
 }
+// spatial sign of the y-mirror for component i of a motion / force 6-vector (ang x,y,z, lin x,y,z)
+H12_DEV float s6(int i, float sg) { return (i % 2 == 0) ? sg : 1.f; }
 
 // ------------------------------------------------------------------ per-lane simulation state
 struct Base {               // shared floating base, REAL coordinates (identical in both lanes)
@@ -98,7 +105,7 @@ struct Leg {                // this lane's leg in the lane frame (mirrored for t
   float anc[H12_NFOOT_PTS][2];
   int cmask;                // 4 bits: sole sphere (lane-frame index) in contact
 };
-struct Forces {             // net contact force of this lane's bodies (lane world frame)
+struct Forces {             // net contact force of this lane's bodies (lane world frame), summed
   float foot[3], knee[3], torso[3];
 };
 
@@ -124,21 +131,22 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
     float ax = was_in ? anc[0] : xw[0], ay = was_in ? anc[1] : xw[1];
     ft0 = -P.fk * (xw[0] - ax) - P.fc * vw[0];
     ft1 = -P.fk * (xw[1] - ay) - P.fc * vw[1];
-    float ftn = sqrtf(ft0 * ft0 + ft1 * ft1);
-    if (ftn > P.mus * fn) {
-      float sc = P.mud * fn / ftn;
+    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = P.mus * fn;
+    if (ftn2 > cap * cap) {
+      float sc = P.mud * fn * __builtin_amdgcn_rsqf(ftn2);
       ft0 *= sc;
       ft1 *= sc;
-      ax = xw[0] + ft0 / P.fk;
-      ay = xw[1] + ft1 / P.fk;
+      float ik = frcp(P.fk);
+      ax = xw[0] + ft0 * ik;
+      ay = xw[1] + ft1 * ik;
     }
     anc[0] = ax;
     anc[1] = ay;
   } else {
     ft0 = -P.fc * vw[0];
     ft1 = -P.fc * vw[1];
-    float ftn = sqrtf(ft0 * ft0 + ft1 * ft1), cap = P.mud * fn;
-    if (ftn > cap) { float sc = cap / ftn; ft0 *= sc; ft1 *= sc; }
+    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = P.mud * fn;
+    if (ftn2 > cap * cap) { float sc = cap * __builtin_amdgcn_rsqf(ftn2); ft0 *= sc; ft1 *= sc; }
   }
   float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
   mtv(Rb, Fw, fl);
@@ -150,17 +158,18 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
 }
 
 H12_DEV void quat_integrate(float* q, const float* w, float h) {
-  float wn = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  if (wn > 0.f) {
-    float half = 0.5f * wn * h, sh, ch;
-    sincosf(half, &sh, &ch);
-    sh /= wn;
+  float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (w2 > 0.f) {
+    float wn = fsqrt(w2);
+    float sh, ch;
+    fsincos(0.5f * wn * h, &sh, &ch);
+    sh *= frcp(wn);
     float r[4] = {ch, w[0] * sh, w[1] * sh, w[2] * sh};
     float o[4] = {q[0] * r[0] - q[1] * r[1] - q[2] * r[2] - q[3] * r[3],
                   q[0] * r[1] + q[1] * r[0] + q[2] * r[3] - q[3] * r[2],
                   q[0] * r[2] - q[1] * r[3] + q[2] * r[0] + q[3] * r[1],
                   q[0] * r[3] + q[1] * r[2] - q[2] * r[1] + q[3] * r[0]};
-    float inv = rsqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
+    float inv = __builtin_amdgcn_rsqf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3]);
     q[0] = o[0] * inv; q[1] = o[1] * inv; q[2] = o[2] * inv; q[3] = o[3] * inv;
   }
 }
@@ -182,7 +191,7 @@ H12_DEV void solve6(const AInertia& I, const float* b, float* x) {
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
     D[j] = d;
-    Dinv[j] = 1.f / d;
+    Dinv[j] = frcp(d);
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       float t = M[i][j];
@@ -208,62 +217,70 @@ H12_DEV void solve6(const AInertia& I, const float* b, float* x) {
   }
 }
 
-// ---- ABA pass 1 for leg link LINK: velocity, velocity-product accel, bias force, world pose
-template <int LINK>
-H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], float* v, float (&cb)[NL][6], float (&pA)[NL][6],
-                        float (&R)[3][3], float* p) {
-  constexpr int A = AX[LINK];
-  const float* r = h12m::R[LINK];
-  float s, c;
-  sincosf(lg.q[LINK], &s, &c);
-  cs[LINK][0] = c;
-  cs[LINK][1] = s;
-  float t[3], wl[3], vl[3];
-  cross(r, v, t);
-  float lin[3] = {v[3] - t[0], v[4] - t[1], v[5] - t[2]};
-  rotT<A>(c, s, v, wl);
-  rotT<A>(c, s, lin, vl);
-  float qd = lg.qd[LINK];
-  wl[A] += qd;
-  v[0] = wl[0]; v[1] = wl[1]; v[2] = wl[2]; v[3] = vl[0]; v[4] = vl[1]; v[5] = vl[2];
-  // c = v x (e_A qd)
+// velocity-product acceleration c = v x (e_A qd)
+template <int A>
+H12_DEV void vprod(const float* v, float qd, float* c) {
   float e[3] = {0.f, 0.f, 0.f};
   e[A] = qd;
-  cross(wl, e, cb[LINK]);
-  cross(vl, e, cb[LINK] + 3);
-  // bias force v x* (I v) with I = (Ibar, m c, m)
+  cross(v, e, c);
+  cross(v + 3, e, c + 3);
+}
+// rigid-body bias force v x* (I v) of leg link LINK (I = (Ibar, m c, m) in link coords)
+template <int LINK>
+H12_DEV void bias(const float* v, float* p) {
   const float* Ibar = h12m::IBAR[LINK];
   const float* mc = h12m::MC[LINK];
   const float m = h12m::M[LINK];
+  const float* w = v;
+  const float* vl = v + 3;
   float n[3], f[3], a1[3], a2[3];
-  for (int i = 0; i < 3; ++i) n[i] = sget(Ibar, i, 0) * wl[0] + sget(Ibar, i, 1) * wl[1] + sget(Ibar, i, 2) * wl[2];
+  for (int i = 0; i < 3; ++i) n[i] = sget(Ibar, i, 0) * w[0] + sget(Ibar, i, 1) * w[1] + sget(Ibar, i, 2) * w[2];
   cross(mc, vl, a1);
   n[0] += a1[0]; n[1] += a1[1]; n[2] += a1[2];
-  cross(mc, wl, a2);
+  cross(mc, w, a2);
   f[0] = m * vl[0] - a2[0]; f[1] = m * vl[1] - a2[1]; f[2] = m * vl[2] - a2[2];
   float x1[3], x2[3], x3[3];
-  cross(wl, n, x1);
+  cross(w, n, x1);
   cross(vl, f, x2);
-  cross(wl, f, x3);
-  pA[LINK][0] = x1[0] + x2[0]; pA[LINK][1] = x1[1] + x2[1]; pA[LINK][2] = x1[2] + x2[2];
-  pA[LINK][3] = x3[0]; pA[LINK][4] = x3[1]; pA[LINK][5] = x3[2];
-  // world pose of the link frame
+  cross(w, f, x3);
+  p[0] = x1[0] + x2[0]; p[1] = x1[1] + x2[1]; p[2] = x1[2] + x2[2];
+  p[3] = x3[0]; p[4] = x3[1]; p[5] = x3[2];
+}
+
+// ---- ABA pass 1 for leg link LINK: spatial velocity v[LINK] from the parent's vp, world pose
+template <int LINK>
+H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, float (&v)[NL][6], float (&R)[3][3],
+                        float* p) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  float s, c;
+  fsincos(lg.q[LINK], &s, &c);
+  cs[LINK][0] = c;
+  cs[LINK][1] = s;
+  float t[3];
+  cross(r, vp, t);
+  float lin[3] = {vp[3] - t[0], vp[4] - t[1], vp[5] - t[2]};
+  rotT<A>(c, s, vp, v[LINK]);
+  rotT<A>(c, s, lin, v[LINK] + 3);
+  v[LINK][A] += lg.qd[LINK];
   float Rr[3];
   mv(R, r, Rr);
   p[0] += Rr[0]; p[1] += Rr[1]; p[2] += Rr[2];
   rmul_axis<A>(R, c, s);
 }
 
-// ---- ABA pass 2 for leg link LINK (leaf -> root), leaves the result expressed at the parent origin
+// ---- ABA pass 2 for leg link LINK (leaf -> root).  On entry IA / pAcc are the articulated inertia /
+// bias force of LINK in its own frame; on exit those of the parent (rigid part and bias included;
+// for LINK == 0 the leg's contribution to the base, at the base origin).
 template <int LINK>
-H12_DEV void link_pass2(const KParams& P, const float (&cs)[NL][2], const float (&cb)[NL][6], const float (&pA)[NL][6],
-                        const float* tau, AInertia& IA, float* pAcc, float (&U)[NL][6], float (&Dinv)[NL],
-                        float (&u)[NL], float h) {
+H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
+                        const float* fext_knee, const float* tau, AInertia& IA, float* pAcc, float (&U)[NL][6],
+                        float (&Dinv)[NL], float (&u)[NL], float h) {
   constexpr int A = AX[LINK];
   float Ua[3] = {sget(IA.A, 0, A), sget(IA.A, 1, A), sget(IA.A, 2, A)};
   float Ul[3] = {IA.B[A][0], IA.B[A][1], IA.B[A][2]};
   float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK];
-  float di = 1.f / D;
+  float di = frcp(D);
   float uu = tau[LINK] - pAcc[A];
   U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
   U[LINK][3] = Ul[0]; U[LINK][4] = Ul[1]; U[LINK][5] = Ul[2];
@@ -279,8 +296,9 @@ H12_DEV void link_pass2(const KParams& P, const float (&cs)[NL][2], const float 
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * Uld[j];
   // pa = pA + Ia c + U u / D
-  float Ic[6];
-  ai_mul(IA, cb[LINK], Ic);
+  float cb[6], Ic[6];
+  vprod<A>(v[LINK], lg.qd[LINK], cb);
+  ai_mul(IA, cb, Ic);
   float ud = uu * di;
   float pa[6];
   for (int i = 0; i < 3; ++i) {
@@ -302,13 +320,17 @@ H12_DEV void link_pass2(const KParams& P, const float (&cs)[NL][2], const float 
     AInertia Rg;
     ai_rigid(Rg, h12m::IBAR[LINK - 1], h12m::MC[LINK - 1], h12m::M[LINK - 1]);
     ai_add(IA, Rg);
-    for (int i = 0; i < 6; ++i) pAcc[i] += pA[LINK - 1][i];
+    float pb[6];
+    bias<LINK - 1>(v[LINK - 1], pb);
+    for (int i = 0; i < 6; ++i) pAcc[i] += pb[i];
+    if constexpr (LINK - 1 == 3)
+      for (int i = 0; i < 6; ++i) pAcc[i] -= fext_knee[i];
   }
 }
 
 // ---- ABA pass 3 for leg link LINK (root -> leaf)
 template <int LINK>
-H12_DEV void link_pass3(const float (&cs)[NL][2], const float (&cb)[NL][6], const float (&U)[NL][6],
+H12_DEV void link_pass3(const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6], const float (&U)[NL][6],
                         const float (&Dinv)[NL], const float (&u)[NL], float* a, float* qdd) {
   constexpr int A = AX[LINK];
   const float* r = h12m::R[LINK];
@@ -316,11 +338,12 @@ H12_DEV void link_pass3(const float (&cs)[NL][2], const float (&cb)[NL][6], cons
   float t[3];
   cross(r, a, t);
   float lin[3] = {a[3] - t[0], a[4] - t[1], a[5] - t[2]};
-  float w[3], l[3];
+  float w[3], l[3], cb[6];
   rotT<A>(c, s, a, w);
   rotT<A>(c, s, lin, l);
-  a[0] = w[0] + cb[LINK][0]; a[1] = w[1] + cb[LINK][1]; a[2] = w[2] + cb[LINK][2];
-  a[3] = l[0] + cb[LINK][3]; a[4] = l[1] + cb[LINK][4]; a[5] = l[2] + cb[LINK][5];
+  vprod<A>(v[LINK], lg.qd[LINK], cb);
+  a[0] = w[0] + cb[0]; a[1] = w[1] + cb[1]; a[2] = w[2] + cb[2];
+  a[3] = l[0] + cb[3]; a[4] = l[1] + cb[4]; a[5] = l[2] + cb[5];
   float ua = 0.f;
   for (int i = 0; i < 6; ++i) ua += U[LINK][i] * a[i];
   float x = (u[LINK] - ua) * Dinv[LINK];
@@ -328,13 +351,9 @@ H12_DEV void link_pass3(const float (&cs)[NL][2], const float (&cb)[NL][6], cons
   a[A] += x;
 }
 
-// spatial sign of the y-mirror for component i of a motion / force 6-vector (ang x,y,z, lin x,y,z)
-H12_DEV float s6(int i, float sg) { return (i % 2 == 0) ? sg : 1.f; }
-
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
-// lane's 6 joints (lane frame).  Adds this lane's contact forces * wgt into fr.
-H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
-                        float wgt) {
+// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
+H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr) {
   const float sg = leg ? -1.f : 1.f;
   float R0[3][3];
   quat_R(b.quat, R0);
@@ -346,43 +365,42 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) R[i][j] = mm[i] * mm[j] * R0[i][j];
   float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
-  float v[6];
-  for (int i = 0; i < 6; ++i) v[i] = s6(i, sg) * v0[i];
+  float vl0[6];
+  for (int i = 0; i < 6; ++i) vl0[i] = s6(i, sg) * v0[i];
   float p[3] = {b.pos[0], sg * b.pos[1], b.pos[2]};
-  float cs[NL][2], cb[NL][6], pA[NL][6];
-  float Rk[3][3], pk[3], vk[6];
-  link_pass1<0>(lg, cs, v, cb, pA, R, p);
-  link_pass1<1>(lg, cs, v, cb, pA, R, p);
-  link_pass1<2>(lg, cs, v, cb, pA, R, p);
-  link_pass1<3>(lg, cs, v, cb, pA, R, p);
-  for (int i = 0; i < 3; ++i) { pk[i] = p[i]; for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j]; }
-  for (int i = 0; i < 6; ++i) vk[i] = v[i];
-  link_pass1<4>(lg, cs, v, cb, pA, R, p);
-  link_pass1<5>(lg, cs, v, cb, pA, R, p);
-
-  // ---- contacts: external forces are subtracted from the bias forces
+  float cs[NL][2], v[NL][6];
+  float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  link_pass1<0>(lg, cs, vl0, v, R, p);
+  link_pass1<1>(lg, cs, v[0], v, R, p);
+  link_pass1<2>(lg, cs, v[1], v, R, p);
+  link_pass1<3>(lg, cs, v[2], v, R, p);
+  {
+    // knee capsule: lower end point, contact evaluated at the knee link pose
+    float w0[3], w1[3];
+    mv(R, h12m::KNEE0, w0);
+    mv(R, h12m::KNEE1, w1);
+    const float* pl = (w0[2] <= w1[2]) ? h12m::KNEE0 : h12m::KNEE1;
+    float dummy[2];
+    contact_sphere<false>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false);
+  }
+  link_pass1<4>(lg, cs, v[3], v, R, p);
+  link_pass1<5>(lg, cs, v[4], v, R, p);
+  // ---- foot: 4 anchored sole spheres on the ankle-roll link; starts pass 2 of link 5
+  AInertia IA;
+  ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
+  float pAcc[6];
+  bias<5>(v[5], pAcc);
   {
     float fext[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int nmask = 0;
 #pragma unroll
     for (int q = 0; q < H12_NFOOT_PTS; ++q) {
       bool was = (lg.cmask >> q) & 1;
-      if (contact_sphere<true>(P, R, p, v, h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was)) nmask |= 1 << q;
+      if (contact_sphere<true>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was))
+        nmask |= 1 << q;
     }
     lg.cmask = nmask;
-    for (int i = 0; i < 6; ++i) pA[5][i] -= fext[i];
-  }
-  {
-    float w0[3], w1[3];
-    mv(Rk, h12m::KNEE0, w0);
-    mv(Rk, h12m::KNEE1, w1);
-    const float* pl = (w0[2] <= w1[2]) ? h12m::KNEE0 : h12m::KNEE1;
-    float fk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float tmp[3] = {0.f, 0.f, 0.f};
-    float dummy[2];
-    contact_sphere<false>(P, Rk, pk, vk, pl, h12m::KNEE_R, fk, tmp, dummy, false);
-    for (int i = 0; i < 6; ++i) pA[3][i] -= fk[i];
-    fr.knee[0] += wgt * tmp[0]; fr.knee[1] += wgt * tmp[1]; fr.knee[2] += wgt * tmp[2];
+    for (int i = 0; i < 6; ++i) pAcc[i] -= fext[i];
   }
   // ---- joint torques for this inner step: actuator + limit penalty (+ MuJoCo passive)
   float tau[NL];
@@ -397,21 +415,16 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     tau[k] = t;
   }
   // ---- pass 2 (leaf -> root)
-  AInertia IA;
-  ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
-  float pAcc[6];
-  for (int i = 0; i < 6; ++i) pAcc[i] = pA[5][i];
   float U[NL][6], Dinv[NL], u[NL];
-  link_pass2<5>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<4>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<3>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<2>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<1>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<0>(P, cs, cb, pA, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<5>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<4>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<3>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<2>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<1>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<0>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
   // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
-  }
   IA.A[3] *= sg; IA.A[5] *= sg;  // xy, yz of the angular block (s = (sg,1,sg))
   IA.C[3] *= sg; IA.C[5] *= sg;  // xy, yz of the linear block (s = (1,sg,1))
   for (int i = 0; i < 6; ++i) pAcc[i] *= s6(i, sg);
@@ -432,11 +445,9 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     float corner[3];
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float tmp[3] = {0.f, 0.f, 0.f};
     float dummy[2];
-    contact_sphere<false>(P, R0, b.pos, v0, corner, 0.f, ft, tmp, dummy, false);
+    contact_sphere<false>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
-    fr.torso[0] += wgt * tmp[0]; fr.torso[1] += wgt * tmp[1]; fr.torso[2] += wgt * tmp[2];
   }
   // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
   AInertia IB;
@@ -461,12 +472,12 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float a[6];
   for (int i = 0; i < 6; ++i) a[i] = s6(i, sg) * a0[i];
   float qdd[NL];
-  link_pass3<0>(cs, cb, U, Dinv, u, a, qdd);
-  link_pass3<1>(cs, cb, U, Dinv, u, a, qdd);
-  link_pass3<2>(cs, cb, U, Dinv, u, a, qdd);
-  link_pass3<3>(cs, cb, U, Dinv, u, a, qdd);
-  link_pass3<4>(cs, cb, U, Dinv, u, a, qdd);
-  link_pass3<5>(cs, cb, U, Dinv, u, a, qdd);
+  link_pass3<0>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<1>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<2>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<3>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<4>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<5>(lg, cs, v, U, Dinv, u, a, qdd);
   // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates
   if (!P.fix_base) {
     float nd[6];
@@ -500,7 +511,8 @@ struct EnvSt {
   int eplen, lag[3], since_reset, is_heading, is_standing;
 };
 
-H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
+// physics part of the state (loaded before the physics loop)
+H12_DEV void load_phys(const Workspace& W, int e, int leg, EnvSt& s) {
   const float sg = leg ? -1.f : 1.f;
   for (int i = 0; i < 3; ++i) s.b.pos[i] = ldf(W, H12_F_POS + i, e);
   for (int i = 0; i < 4; ++i) s.b.quat[i] = ldf(W, H12_F_QUAT + i, e);
@@ -524,6 +536,14 @@ H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
     s.lg.anc[q][1] = sg * ldf(W, H12_F_ANCHOR + 8 * leg + 2 * qr + 1, e);
     s.lg.cmask |= ((cm >> qr) & 1) << q;
   }
+  for (int g = 0; g < 3; ++g) s.lag[g] = (pk >> (3 * g)) & 7;
+  s.since_reset = (pk >> 9) & 3;
+  s.is_heading = (pk >> 11) & 1;
+  s.is_standing = (pk >> 12) & 1;
+}
+
+// MDP part of the state (loaded after the physics loop)
+H12_DEV void load_mdp(const Workspace& W, int e, int leg, EnvSt& s) {
   for (int i = 0; i < 3; ++i) s.cmd[i] = ldf(W, H12_F_CMD + i, e);
   s.heading = ldf(W, H12_F_HEADING, e);
   s.cmd_time = ldf(W, H12_F_CMD_TIME, e);
@@ -533,10 +553,11 @@ H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
   s.last_con = ldf(W, H12_F_LAST_CONTACT + leg, e);
   for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
   s.eplen = W.I[(size_t)H12_I_EPLEN * W.n + e];
-  for (int g = 0; g < 3; ++g) s.lag[g] = (pk >> (3 * g)) & 7;
-  s.since_reset = (pk >> 9) & 3;
-  s.is_heading = (pk >> 11) & 1;
-  s.is_standing = (pk >> 12) & 1;
+}
+
+H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
+  load_phys(W, e, leg, s);
+  load_mdp(W, e, leg, s);
 }
 
 H12_DEV void store_env(const Workspace& W, int e, int leg, const EnvSt& s) {
@@ -740,30 +761,29 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   const uint32_t g = (uint32_t)(A.env_offset + e);
   if (active) {
     EnvSt s;
-    load_env(W, e, leg, s);
+    load_phys(W, e, leg, s);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
-    float a_t[NL], a_t1[NL], a_t2[NL];
+    float a_t2[NL];
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      a_t[k] = jsign(k, sg) * A.actions[(size_t)e * NJ + NL * leg + k];
-      a_t1[k] = s.act[k];
       a_t2[k] = s.act1[k];
       s.act1[k] = s.act[k];
-      s.act[k] = a_t[k];
+      s.act[k] = jsign(k, sg) * A.actions[(size_t)e * NJ + NL * leg + k];
     }
     const int dec = P.decimation;
-    float tau_app[NL], jacc[NL];
+    float tau[NL], jacc[NL];
     float fmax_knee = 0.f, fmax_torso = 0.f, fmax_foot = 0.f, flast_foot = 0.f;
-    const float wgt = 1.f / (float)P.inner;
+    uint32_t cflags = 0;  // foot contact flag of every physics step (ContactSensor replay)
+    const float wgt = frcp((float)P.inner);
     for (int st = 0; st < dec; ++st) {
-      float tau[NL];
       if (P.mode == H12_MODE_ISAACLAB) {
         // DelayedPDActuator: delayed target = CircularBuffer[lag] with lag clamped to pushes-1
         int npush = s.since_reset * dec + st + 1;
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-          int L = min(s.lag[P.dgroup[k]], npush - 1);
-          float a = (L <= st) ? a_t[k] : ((L <= st + dec) ? a_t1[k] : a_t2[k]);
+          const int dg = P.dgroup[k];  // uniform; select instead of a runtime-indexed (scratch) array
+          int L = min(dg == 0 ? s.lag[0] : (dg == 1 ? s.lag[1] : s.lag[2]), npush - 1);
+          float a = (L <= st) ? s.act[k] : ((L <= st + dec) ? s.act1[k] : a_t2[k]);
           float tgt = h12m::Q0[k] + P.action_scale * a;
           float v = P.kp[k] * (tgt - s.lg.q[k]) + P.kd[k] * (0.f - s.lg.qd[k]);
           tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
@@ -771,31 +791,38 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       } else {
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-          float tgt = h12m::Q0[k] + P.action_scale * a_t[k];
+          float tgt = h12m::Q0[k] + P.action_scale * s.act[k];
           float v = P.kp[k] * (tgt - s.lg.q[k]) - P.kd[k] * s.lg.qd[k];
           tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
         }
       }
-      float qd0[NL];
-      for (int k = 0; k < NL; ++k) qd0[k] = s.lg.qd[k];
+      const bool last = st == dec - 1;
+      if (last)
+        for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
-      for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr, wgt);
-      for (int k = 0; k < NL; ++k) { tau_app[k] = tau[k]; jacc[k] = (s.lg.qd[k] - qd0[k]) / P.dt; }
-      // ContactSensor._update_buffers_impl: air / contact time (threshold 1 N, elapsed = dt)
-      float fn = sqrtf(fr.foot[0] * fr.foot[0] + fr.foot[1] * fr.foot[1] + fr.foot[2] * fr.foot[2]) * wgt;
-      bool is_c = fn > P.cthr;
+      for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr);
+      if (last)
+        for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
+      // ContactSensor: net force = mean over the inner steps of the physics step
+      float fn = fsqrt(fr.foot[0] * fr.foot[0] + fr.foot[1] * fr.foot[1] + fr.foot[2] * fr.foot[2]) * wgt;
+      cflags |= (fn > P.cthr ? 1u : 0u) << st;
+      flast_foot = fn;
+      if (st >= dec - 3) {  // net_forces_w_history (history_length 3)
+        fmax_foot = fmaxf(fmax_foot, fn);
+        fmax_knee = fmaxf(fmax_knee, wgt * fsqrt(fr.knee[0] * fr.knee[0] + fr.knee[1] * fr.knee[1] + fr.knee[2] * fr.knee[2]));
+        fmax_torso = fmaxf(fmax_torso, wgt * fsqrt(fr.torso[0] * fr.torso[0] + fr.torso[1] * fr.torso[1] + fr.torso[2] * fr.torso[2]));
+      }
+    }
+    load_mdp(W, e, leg, s);
+    // ContactSensor._update_buffers_impl replayed per physics step (threshold 1 N, elapsed = dt)
+    for (int st = 0; st < dec; ++st) {
+      bool is_c = (cflags >> st) & 1u;
       bool first_c = (s.air > 0.f) && is_c;
       bool first_d = (s.con > 0.f) && !is_c;
       if (first_c) s.last_air = s.air + P.dt;
       s.air = is_c ? 0.f : s.air + P.dt;
       if (first_d) s.last_con = s.con + P.dt;
       s.con = is_c ? s.con + P.dt : 0.f;
-      flast_foot = fn;
-      if (st >= dec - 3) {  // net_forces_w_history (history_length 3)
-        fmax_foot = fmaxf(fmax_foot, fn);
-        fmax_knee = fmaxf(fmax_knee, sqrtf(fr.knee[0] * fr.knee[0] + fr.knee[1] * fr.knee[1] + fr.knee[2] * fr.knee[2]));
-        fmax_torso = fmaxf(fmax_torso, sqrtf(fr.torso[0] * fr.torso[0] + fr.torso[1] * fr.torso[1] + fr.torso[2] * fr.torso[2]));
-      }
     }
     s.eplen += 1;
     // ---- terminations: time_out, illegal_contact (pair-combined)
@@ -811,19 +838,20 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     mv(R, h12m::BASE_COM, cw);
     cross(ww, cw, wxc);
     float vcom[3] = {s.b.vlin[0] + wxc[0], s.b.vlin[1] + wxc[1], s.b.vlin[2] + wxc[2]};
-    float yaw = atan2f(R[1][0], R[0][0]);
-    float sy, cy;
-    sincosf(yaw, &sy, &cy);
+    // yaw frame: heading direction of the body x axis in the world xy-plane
+    float hx = R[0][0], hy = R[1][0];
+    float hn = __builtin_amdgcn_rsqf(hx * hx + hy * hy);
+    float cy = hx * hn, sy = hy * hn;
     float vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
     float terms[H12_NREW];
     float ex = s.cmd[0] - vy0, ey = s.cmd[1] - vy1, ew = s.cmd[2] - ww[2];
-    terms[H12_R_TRACK_LIN_VEL_XY] = expf(-(ex * ex + ey * ey) * P.std2_inv);
-    terms[H12_R_TRACK_ANG_VEL_Z] = expf(-(ew * ew) * P.std2_inv);
+    terms[H12_R_TRACK_LIN_VEL_XY] = __expf(-(ex * ex + ey * ey) * P.std2_inv);
+    terms[H12_R_TRACK_ANG_VEL_Z] = __expf(-(ew * ew) * P.std2_inv);
     terms[H12_R_ANG_VEL_XY_L2] = s.b.wang[0] * s.b.wang[0] + s.b.wang[1] * s.b.wang[1];
     float st_ = 0.f, sa_ = 0.f, sr_ = 0.f, sl_ = 0.f, sd_ = 0.f;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      st_ += tau_app[k] * tau_app[k];
+      st_ += tau[k] * tau[k];
       sa_ += jacc[k] * jacc[k];
       float dr = s.act[k] - s.act1[k];
       sr_ += dr * dr;
@@ -849,8 +877,8 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       float mL = incL ? conL : airL, mR = incR ? conR : airR;
       float r = ((incL + incR) == 1) ? fminf(mL, mR) : 0.f;
       r = fminf(r, P.air_thr);
-      float cn = sqrtf(s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1]);
-      terms[H12_R_FEET_AIR_TIME] = cn > 0.1f ? r : 0.f;
+      float cn2 = s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1];
+      terms[H12_R_FEET_AIR_TIME] = cn2 > 0.01f ? r : 0.f;
     }
     terms[H12_R_FLAT_ORIENTATION_L2] = R[2][0] * R[2][0] + R[2][1] * R[2][1];
     terms[H12_R_DOF_POS_LIMITS] = psum(sl_);
@@ -865,20 +893,20 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
           for (int j = 0; j < 3; ++j) Rf[i][j] = mm[i] * mm[j] * R[i][j];
         float vb[3];
         mtv(R, s.b.vlin, vb);
-        float v6[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
-        for (int i = 0; i < 6; ++i) v6[i] *= s6(i, sg);
-        float csd[NL][2], cbd[NL][6], pAd[NL][6], pd[3] = {0.f, 0.f, 0.f};
-        link_pass1<0>(s.lg, csd, v6, cbd, pAd, Rf, pd);
-        link_pass1<1>(s.lg, csd, v6, cbd, pAd, Rf, pd);
-        link_pass1<2>(s.lg, csd, v6, cbd, pAd, Rf, pd);
-        link_pass1<3>(s.lg, csd, v6, cbd, pAd, Rf, pd);
-        link_pass1<4>(s.lg, csd, v6, cbd, pAd, Rf, pd);
-        link_pass1<5>(s.lg, csd, v6, cbd, pAd, Rf, pd);
+        float v0[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
+        for (int i = 0; i < 6; ++i) v0[i] *= s6(i, sg);
+        float csd[NL][2], vd[NL][6], pd[3] = {0.f, 0.f, 0.f};
+        link_pass1<0>(s.lg, csd, v0, vd, Rf, pd);
+        link_pass1<1>(s.lg, csd, vd[0], vd, Rf, pd);
+        link_pass1<2>(s.lg, csd, vd[1], vd, Rf, pd);
+        link_pass1<3>(s.lg, csd, vd[2], vd, Rf, pd);
+        link_pass1<4>(s.lg, csd, vd[3], vd, Rf, pd);
+        link_pass1<5>(s.lg, csd, vd[4], vd, Rf, pd);
         float vc[3], vw[3];
-        cross(v6, h12m::COM[5], vc);
-        vc[0] += v6[3]; vc[1] += v6[4]; vc[2] += v6[5];
+        cross(vd[5], h12m::COM[5], vc);
+        vc[0] += vd[5][3]; vc[1] += vd[5][4]; vc[2] += vd[5][5];
         mv(Rf, vc, vw);
-        fs = sqrtf(vw[0] * vw[0] + vw[1] * vw[1]);
+        fs = fsqrt(vw[0] * vw[0] + vw[1] * vw[1]);
       }
       terms[H12_R_FEET_SLIDE] = psum(fs);
     }
@@ -897,7 +925,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       A.trunc[e] = (uint8_t)tout;
     }
     if (A.applied_torque)
-      for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau_app[k];
+      for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
     // ---- episode log: wave-reduced, one atomic per value per wave that saw a reset
     if (A.log_acc) {
@@ -994,7 +1022,6 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
   load_env(W, e, leg, s);
   float qr[NL];
   for (int k = 0; k < NL; ++k) qr[k] = jsign(k, sg) * A.q_ref[(size_t)e * NJ + NL * leg + k];
-  const float wgt = 1.f / (float)P.inner;
   for (int st = 0; st < A.n_substeps; ++st) {
     float tau[NL];
     for (int k = 0; k < NL; ++k) {
@@ -1002,7 +1029,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr, wgt);
+    for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr);
   }
   store_env(W, e, leg, s);
 }
@@ -1049,7 +1076,8 @@ int check_model(const h12env_model* m) {
 int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   memset(&P, 0, sizeof P);
   if (int rc = check_model(m)) return rc;
-  if (c->decimation < 1 || c->inner_steps < 1 || !(c->physics_dt > 0)) return set_err(H12_E_ARG, "bad decimation/inner_steps/dt");
+  if (c->decimation < 1 || c->decimation > MAX_DEC || c->inner_steps < 1 || !(c->physics_dt > 0))
+    return set_err(H12_E_ARG, "bad decimation (1..%d) / inner_steps / dt", MAX_DEC);
   if (c->mode != H12_MODE_ISAACLAB && c->mode != H12_MODE_MUJOCO) return set_err(H12_E_ARG, "bad mode %d", c->mode);
   if (c->min_delay < 0 || c->max_delay < c->min_delay || c->max_delay > 7 || c->max_delay > 2 * c->decimation)
     return set_err(H12_E_ARG, "delay range [%d,%d] unsupported", c->min_delay, c->max_delay);
@@ -1123,6 +1151,7 @@ size_t h12env_sizeof_struct(int which) {
     default: return 0;
   }
 }
+
 const char* h12env_last_error(void) { return g_err; }
 
 int h12env_config_default(h12env_config* c) {

@@ -42,7 +42,8 @@ def build(force: bool = False, verbose: bool = True, extra_flags: list[str] | No
                    stdout=subprocess.DEVNULL)
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+    # -fno-slp-vectorize: packed-fp32 SLP code needs register pairs and costs ~30 % extra v_mov here
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared", "-Wall",
            "-Wno-unused-function", "-o", str(OUT), str(CSRC / "h12env.hip")]
     if extra_flags:
         cmd += extra_flags
