@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--pmc-file", type=str, default=None,
                    help="JSON with per-launch HBM bytes from a rocprofv3 --pmc run (fills roofline.traffic)")
     p.add_argument("--profile-only", action="store_true", help="timed loop only (for rocprofv3 runs)")
+    p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
+    p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
 
 
@@ -93,6 +95,10 @@ def main():
     cfg = H12FlatEnvCfg()
     cfg.scene.num_envs = n
     cfg.sim.device = str(dev)
+    if args.decimation:
+        cfg.decimation = args.decimation
+    if args.inner_steps:
+        cfg.sim.inner_steps = args.inner_steps
     env = H12VelocityEnv(cfg, env_offset=rank * n)
     env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)

@@ -107,19 +107,30 @@ H12_DEV void ai_add(AInertia& I, const AInertia& J) {
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) I.B[i][j] += J.B[i][j];
 }
+// symmetric-index helper: position of (i,j) in the (xx yy zz xy xz yz) packing
+H12_DEV constexpr int sidx(int i, int j) {
+  return i == j ? i : ((i + j == 1) ? 3 : ((i + j == 2) ? 4 : 5));
+}
+// S <- R_A S R_A^T for symmetric S: only the (i, j) plane orthogonal to the axis k = A rotates,
+// v_i' = c v_i - s v_j, v_j' = s v_i + c v_j with (i, j) = (y, z), (z, x), (x, y) for A = x, y, z
+template <int A>
+H12_DEV void sym_rotate(float* S, float c, float s) {
+  constexpr int i = (A + 1) % 3, j = (A + 2) % 3, k = A;
+  const float cc = c * c, ss = s * s, cs = c * s;
+  float sii = S[sidx(i, i)], sjj = S[sidx(j, j)], sij = S[sidx(i, j)];
+  float sik = S[sidx(i, k)], sjk = S[sidx(j, k)];
+  S[sidx(i, i)] = cc * sii - 2.f * cs * sij + ss * sjj;
+  S[sidx(j, j)] = ss * sii + 2.f * cs * sij + cc * sjj;
+  S[sidx(i, j)] = cs * (sii - sjj) + (cc - ss) * sij;
+  S[sidx(i, k)] = c * sik - s * sjk;
+  S[sidx(j, k)] = s * sik + c * sjk;
+}
 // rotate every block into parent axes: X_rot^T I X_rot with E^T = R_A(q)
 template <int A>
 H12_DEV void ai_rotate(AInertia& I, float c, float s) {
-  float M[3][3], T[3][3];
-  // A block: R A R^T
-  sym_full(I.A, M);
-  for (int j = 0; j < 3; ++j) { float col[3] = {M[0][j], M[1][j], M[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
-  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); M[i][0] = o[0]; M[i][1] = o[1]; M[i][2] = o[2]; }
-  full_sym(M, I.A);
-  sym_full(I.C, M);
-  for (int j = 0; j < 3; ++j) { float col[3] = {M[0][j], M[1][j], M[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
-  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); M[i][0] = o[0]; M[i][1] = o[1]; M[i][2] = o[2]; }
-  full_sym(M, I.C);
+  float T[3][3];
+  sym_rotate<A>(I.A, c, s);
+  sym_rotate<A>(I.C, c, s);
   // B block: R B R^T
   for (int j = 0; j < 3; ++j) { float col[3] = {I.B[0][j], I.B[1][j], I.B[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
   for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); I.B[i][0] = o[0]; I.B[i][1] = o[1]; I.B[i][2] = o[2]; }
@@ -175,8 +186,9 @@ H12_DEV float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 H12_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 H12_DEV float uab(uint32_t x, float a, float b) { return a + (b - a) * u01(x); }
 
-// lane-pair exchange (lanes 2e and 2e+1 hold the two legs of env e)
-H12_DEV float pair_swap(float x) { return __shfl_xor(x, 1); }
-H12_DEV int pair_swap_i(int x) { return __shfl_xor(x, 1); }
+// lane-pair exchange (lanes 2e and 2e+1 hold the two legs of env e): one DPP quad_perm(1,0,3,2)
+// move (a VALU op) instead of __shfl_xor's ds_bpermute round trip through the LDS crossbar
+H12_DEV int pair_swap_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+H12_DEV float pair_swap(float x) { return __int_as_float(pair_swap_i(__float_as_int(x))); }
 
 }  // namespace h12

@@ -706,27 +706,66 @@ H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, uint32_t g, ui
   }
 }
 
-// cooperative, coalesced write of the block's observation rows: shifted previous row + new frame
-H12_DEV void write_obs_block(const float* obs_prev, float* obs, int e0, int n_rows, const float* lds_frame,
-                             const int* lds_fill, const int* lds_write) {
-  const int total = n_rows * H12_NOBS;
+// column of observation component c (0..44, frame order) in history slot hh of a 450-float row:
+// term-major blocks of 30, 30, 30, 120, 120, 120 floats (CircularBuffer order, oldest slot first)
+H12_DEV int obs_col(int c, int hh) {
+  if (c < 9) { int t = c / 3; return 30 * t + 3 * hh + (c - 3 * t); }
+  int cc = c - 9, t = cc / 12;
+  return 90 + 120 * t + 12 * hh + (cc - 12 * t);
+}
+
+// store-only write of the block's new frames (LDS) into the newest history slot of every written
+// row, and into all slots of the rows whose history is (re)filled.  The shift of the older slots
+// (obs_prev -> obs) is done beforehand by obs_shift_kernel, so no global load sits on this path.
+// Single-wave blocks: the row masks are wave ballots.
+H12_DEV void write_frames(float* obs, int e0, int n_rows, const float* lds_frame, bool write_row, bool fill_row) {
+  const int leg = threadIdx.x & 1;
+  const uint64_t wmask = __ballot(leg == 0 && write_row);
+  const uint64_t fmask = __ballot(leg == 0 && write_row && fill_row);
   const size_t base = (size_t)e0 * H12_NOBS;
+  const int total = n_rows * H12_OBS_FRAME;
   for (int idx = threadIdx.x; idx < total; idx += BLOCK) {
-    int row = idx / H12_NOBS;
-    int col = idx - row * H12_NOBS;
-    if (!lds_write[row]) continue;
-    // column -> (term, history slot, component): term blocks of 30, 30, 30, 120, 120, 120 floats
-    int off, fo, d;
-    if (col < 90) { int t = col / 30; off = 30 * t; fo = 3 * t; d = 3; }
-    else { int t = (col - 90) / 120; off = 90 + 120 * t; fo = 9 + 12 * t; d = 12; }
-    int rel = col - off;
-    int hh = rel / d;
-    int a = rel - hh * d;
-    float v;
-    if (lds_fill[row] || hh == H12_NHIST - 1) v = lds_frame[row * H12_OBS_FRAME + fo + a];
-    else v = obs_prev[base + idx + d];
-    obs[base + idx] = v;
+    int row = idx / H12_OBS_FRAME;
+    int c = idx - row * H12_OBS_FRAME;
+    if ((wmask >> (2 * row)) & 1) obs[base + (size_t)row * H12_NOBS + obs_col(c, H12_NHIST - 1)] = lds_frame[idx];
   }
+  for (uint64_t m = fmask; m; m &= m - 1) {
+    const int row = __builtin_ctzll(m) >> 1;
+    float* dst = obs + base + (size_t)row * H12_NOBS;
+    for (int i = threadIdx.x; i < (H12_NHIST - 1) * H12_OBS_FRAME; i += BLOCK) {
+      int hh = i / H12_OBS_FRAME;
+      int c = i - hh * H12_OBS_FRAME;
+      dst[obs_col(c, hh)] = lds_frame[row * H12_OBS_FRAME + c];
+    }
+  }
+}
+
+// history shift of the observation rows: obs[e, slot h] = obs_prev[e, slot h+1] for h < NHIST-1
+// (CircularBuffer append without the new frame).  Whole rows per block, every load issued before
+// the barrier and every store after it, so obs may alias obs_prev.  Full-chip, coalesced.
+constexpr int SHIFT_BLOCK = 256;
+constexpr int SHIFT_ROWS = 4;
+constexpr int SHIFT_PER_THREAD = (SHIFT_ROWS * H12_NOBS + SHIFT_BLOCK - 1) / SHIFT_BLOCK;
+__global__ void __launch_bounds__(SHIFT_BLOCK) obs_shift_kernel(const float* obs_prev, float* obs, int n) {
+  const int r0 = blockIdx.x * SHIFT_ROWS;
+  const int total = min(SHIFT_ROWS, n - r0) * H12_NOBS;
+  const size_t base = (size_t)r0 * H12_NOBS;
+  float v[SHIFT_PER_THREAD];
+  int dst[SHIFT_PER_THREAD];
+#pragma unroll
+  for (int u = 0; u < SHIFT_PER_THREAD; ++u) {
+    int idx = u * SHIFT_BLOCK + threadIdx.x;
+    int col = idx % H12_NOBS;
+    int d = col < 90 ? 3 : 12;
+    int rel = col < 90 ? col % 30 : (col - 90) % 120;
+    bool ok = idx < total && rel < (H12_NHIST - 1) * d;
+    dst[u] = ok ? idx : -1;
+    v[u] = ok ? obs_prev[base + idx + d] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SHIFT_PER_THREAD; ++u)
+    if (dst[u] >= 0) obs[base + dst[u]] = v[u];
 }
 
 // ------------------------------------------------------------------ kernels
@@ -749,8 +788,6 @@ struct StepArgs {
 
 __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
-  __shared__ int s_fill[ENVS_PER_BLOCK];
-  __shared__ int s_write[ENVS_PER_BLOCK];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
@@ -759,6 +796,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   const bool active = e < W.n;
   const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
   const uint32_t g = (uint32_t)(A.env_offset + e);
+  bool fill_row = false;
   if (active) {
     EnvSt s;
     load_phys(W, e, leg, s);
@@ -953,62 +991,51 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     cmd_update(P, s);
     // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
     obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
-    if (leg == 0) {
-      s_fill[lane_pair] = reset ? 1 : 0;
-      s_write[lane_pair] = 1;
-    }
+    fill_row = reset;
     store_env(W, e, leg, s);
   }
   __syncthreads();
-  if (n_rows > 0) write_obs_block(A.obs_prev, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+  write_frames(A.obs, e0, n_rows, s_frame, active, fill_row);
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, StepArgs A) {
   __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
-  __shared__ int s_fill[ENVS_PER_BLOCK];
-  __shared__ int s_write[ENVS_PER_BLOCK];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
   const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
-  if (leg == 0) { s_write[lane_pair] = 0; s_fill[lane_pair] = 1; }
-  __syncthreads();
-  if (e < W.n && (!A.reset_mask || A.reset_mask[e])) {
+  const bool sel = e < W.n && (!A.reset_mask || A.reset_mask[e]);
+  if (sel) {
     const uint32_t g = (uint32_t)(A.env_offset + e);
     EnvSt s;
     load_env(W, e, leg, s);
     env_reset(P, s, leg, g, A.lo, A.hi);
     obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
-    if (leg == 0) s_write[lane_pair] = 1;
     store_env(W, e, leg, s);
   }
   __syncthreads();
-  if (n_rows > 0) write_obs_block(A.obs, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+  write_frames(A.obs, e0, n_rows, s_frame, sel, true);
 }
 
 // ObservationManager.compute() outside step(): new frame from the current state, history shifted
 // (or filled where fill_mask[e]); RNG counter domain (observe call, 0xFFFFFFFE)
 __global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, StepArgs A) {
   __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
-  __shared__ int s_fill[ENVS_PER_BLOCK];
-  __shared__ int s_write[ENVS_PER_BLOCK];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
   const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
+  bool fill_row = false;
   if (e < W.n) {
     EnvSt s;
     load_env(W, e, leg, s);
     obs_frame(P, s, leg, (uint32_t)(A.env_offset + e), A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
-    if (leg == 0) {
-      s_write[lane_pair] = 1;
-      s_fill[lane_pair] = A.reset_mask ? (int)A.reset_mask[e] : 0;
-    }
+    fill_row = A.reset_mask && A.reset_mask[e];
   }
   __syncthreads();
-  if (n_rows > 0) write_obs_block(A.obs_prev, A.obs, e0, n_rows, s_frame, s_fill, s_write);
+  write_frames(A.obs, e0, n_rows, s_frame, e < W.n, fill_row);
 }
 
 // parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
@@ -1135,6 +1162,11 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
 }
 
 int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
+
+void launch_shift(const Handle* h, const float* obs_prev, float* obs, hipStream_t stream) {
+  hipLaunchKernelGGL(obs_shift_kernel, dim3((h->W.n + SHIFT_ROWS - 1) / SHIFT_ROWS), dim3(SHIFT_BLOCK), 0, stream,
+                     obs_prev, obs, h->W.n);
+}
 
 }  // namespace
 
@@ -1275,6 +1307,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.env_offset = h->env_offset;
   A.lo = (uint32_t)step_index;
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
+  launch_shift(h, obs_prev, out->obs, (hipStream_t)stream);
   hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -1292,6 +1325,7 @@ int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t*
   A.lo = (uint32_t)h->observe_calls;
   A.hi = 0xFFFFFFFEu;
   h->observe_calls++;
+  launch_shift(h, obs_prev, obs, (hipStream_t)stream);
   hipLaunchKernelGGL(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return 0;

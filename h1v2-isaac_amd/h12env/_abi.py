@@ -150,7 +150,7 @@ def load_library(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path is not None else LIB_PATH
+    p = Path(path) if path is not None else Path(os.environ.get("H12ENV_LIB", LIB_PATH))
     if not p.exists():
         raise H12EnvError(f"HIP extension {p} is missing; build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     # torch's bundled libamdhip64.so.7 must be the one the library binds to (same soname):
