@@ -42,6 +42,22 @@ constexpr int BLOCK = 64;
 constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
 constexpr int MAX_DEC = 32;         // contact flags of one env step are kept in a 32-bit mask
 
+// experiment builds only (-DH12_PHASE_PROFILE): per-phase shader-clock cycles of step_kernel, summed
+// over waves (lane 0), read back with h12env_phase_profile.  Not part of the product library.
+#ifdef H12_PHASE_PROFILE
+__device__ unsigned long long g_phase[16];
+#define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter()
+#define PH(i)                                                                       \
+  do {                                                                              \
+    unsigned long long _t = __builtin_readcyclecounter();                           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _ph_t);                \
+    _ph_t = _t;                                                                     \
+  } while (0)
+#else
+#define PH_INIT() (void)0
+#define PH(i) (void)0
+#endif
+
 thread_local char g_err[512] = "";
 int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int set_err(int code, const char* fmt, ...) {
@@ -678,31 +694,24 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
   cmd_resample(P, s, g, lo, hi);
 }
 
-// this lane's part of the new observation frame -> LDS row fr (45 floats, real coordinates)
-H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi, float* fr) {
+// this lane's part of the new (noise-free) observation frame, real coordinates, into the frame
+// scratch laid out [45][n] (coalesced across the wave).  Noise is added by obs_assemble_kernel.
+H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, float* frame) {
   const float sg = leg ? -1.f : 1.f;
-  float noise[32];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    uint32_t r[4];
-    rng(P, g, lo, hi, ST_OBS, b, r);
-    for (int a = 0; a < 4; ++a) noise[4 * b + a] = u01(r[a]);
-  }
-  auto nz = [&](int t, float nmax) { return P.corrupt ? (-nmax + 2.f * nmax * noise[t]) : 0.f; };
   if (leg == 0) {
     float R[3][3];
     quat_R(s.b.quat, R);
-    for (int a = 0; a < 3; ++a) fr[a] = s.b.wang[a] + nz(a, P.n_w);
-    for (int a = 0; a < 3; ++a) fr[3 + a] = -R[2][a] + nz(3 + a, P.n_g);
-    for (int a = 0; a < 3; ++a) fr[6 + a] = s.cmd[a];
+    for (int a = 0; a < 3; ++a) frame[(size_t)a * n + e] = s.b.wang[a];
+    for (int a = 0; a < 3; ++a) frame[(size_t)(3 + a) * n + e] = -R[2][a];
+    for (int a = 0; a < 3; ++a) frame[(size_t)(6 + a) * n + e] = s.cmd[a];
   }
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
     int j = NL * leg + k;
-    fr[9 + j] = js * (s.lg.q[k] - h12m::Q0[k]) + nz(6 + j, P.n_q);
-    fr[21 + j] = js * s.lg.qd[k] + nz(18 + j, P.n_qd);
-    fr[33 + j] = js * s.act[k];
+    frame[(size_t)(9 + j) * n + e] = js * (s.lg.q[k] - h12m::Q0[k]);
+    frame[(size_t)(21 + j) * n + e] = js * s.lg.qd[k];
+    frame[(size_t)(33 + j) * n + e] = js * s.act[k];
   }
 }
 
@@ -714,58 +723,138 @@ H12_DEV int obs_col(int c, int hh) {
   return 90 + 120 * t + 12 * hh + (cc - 12 * t);
 }
 
-// store-only write of the block's new frames (LDS) into the newest history slot of every written
-// row, and into all slots of the rows whose history is (re)filled.  The shift of the older slots
-// (obs_prev -> obs) is done beforehand by obs_shift_kernel, so no global load sits on this path.
-// Single-wave blocks: the row masks are wave ballots.
-H12_DEV void write_frames(float* obs, int e0, int n_rows, const float* lds_frame, bool write_row, bool fill_row) {
-  const int leg = threadIdx.x & 1;
-  const uint64_t wmask = __ballot(leg == 0 && write_row);
-  const uint64_t fmask = __ballot(leg == 0 && write_row && fill_row);
-  const size_t base = (size_t)e0 * H12_NOBS;
-  const int total = n_rows * H12_OBS_FRAME;
-  for (int idx = threadIdx.x; idx < total; idx += BLOCK) {
-    int row = idx / H12_OBS_FRAME;
-    int c = idx - row * H12_OBS_FRAME;
-    if ((wmask >> (2 * row)) & 1) obs[base + (size_t)row * H12_NOBS + obs_col(c, H12_NHIST - 1)] = lds_frame[idx];
-  }
-  for (uint64_t m = fmask; m; m &= m - 1) {
-    const int row = __builtin_ctzll(m) >> 1;
-    float* dst = obs + base + (size_t)row * H12_NOBS;
-    for (int i = threadIdx.x; i < (H12_NHIST - 1) * H12_OBS_FRAME; i += BLOCK) {
-      int hh = i / H12_OBS_FRAME;
-      int c = i - hh * H12_OBS_FRAME;
-      dst[obs_col(c, hh)] = lds_frame[row * H12_OBS_FRAME + c];
-    }
-  }
+// noise index of frame component c (ang_vel 0-2, gravity 3-5, joint_pos 6-17, joint_vel 18-29;
+// command and last action are noise-free: -1)
+H12_DEV int noise_index(int c) { return c < 6 ? c : (c < 9 ? -1 : (c < 33 ? c - 3 : -1)); }
+
+// additive uniform noise of noise index t (ObservationTermCfg noise=Unoise(-n, n)); 0 when off
+H12_DEV float noise_of(const KParams& P, int t, uint32_t r) {
+  float nmax = t < 3 ? P.n_w : (t < 6 ? P.n_g : (t < 18 ? P.n_q : P.n_qd));
+  return P.corrupt ? (-nmax + 2.f * nmax * u01(r)) : 0.f;
 }
 
-// history shift of the observation rows: obs[e, slot h] = obs_prev[e, slot h+1] for h < NHIST-1
-// (CircularBuffer append without the new frame).  Whole rows per block, every load issued before
-// the barrier and every store after it, so obs may alias obs_prev.  Full-chip, coalesced.
-constexpr int SHIFT_BLOCK = 256;
-constexpr int SHIFT_ROWS = 4;
-constexpr int SHIFT_PER_THREAD = (SHIFT_ROWS * H12_NOBS + SHIFT_BLOCK - 1) / SHIFT_BLOCK;
-__global__ void __launch_bounds__(SHIFT_BLOCK) obs_shift_kernel(const float* obs_prev, float* obs, int n) {
-  const int r0 = blockIdx.x * SHIFT_ROWS;
-  const int total = min(SHIFT_ROWS, n - r0) * H12_NOBS;
+// ObservationManager.compute + CircularBuffer.append for a batch of envs, full-chip.  Each block
+// owns ASM_ROWS whole rows: every thread loads its share of the shifted history
+// (obs[e, slot h] = obs_prev[e, slot h + 1], h < 9) and the first ASM_ROWS * 12 threads build the
+// noisy new frame, one component group each (group g < 8 = Philox block g of the noise stream, 4
+// noise indices; g = 8 command; g = 9..11 last action); all loads precede the barrier and all
+// stores follow it, so obs may alias obs_prev.  Rows being (re)filled take the noisy new frame in
+// every slot.  Reset mode writes only rows with sel[e] (all if sel is NULL) and fills them;
+// otherwise every row is written and fill[e] = fill_a[e] | fill_b[e].
+struct AsmArgs {
+  const float* obs_prev;
+  float* obs;
+  const float* frame;
+  const uint8_t* fill_a;
+  const uint8_t* fill_b;
+  const uint8_t* sel;
+  int reset_mode;
+  int n;
+  int64_t env_offset;
+  uint32_t lo, hi;
+};
+constexpr int ASM_BLOCK = 256;
+constexpr int ASM_ROWS = 4;
+constexpr int ASM_HIST = H12_NOBS - H12_OBS_FRAME;  // 405 history slots per row
+constexpr int ASM_PER_THREAD = (ASM_ROWS * ASM_HIST + ASM_BLOCK - 1) / ASM_BLOCK;
+constexpr int ASM_GROUPS = 12;
+static_assert(ASM_ROWS * ASM_GROUPS <= ASM_BLOCK, "one frame group per thread");
+
+H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
+  if (A.reset_mode) {
+    fill = true;
+    return !A.sel || A.sel[e];
+  }
+  fill = (A.fill_a && A.fill_a[e]) || (A.fill_b && A.fill_b[e]);
+  return true;
+}
+
+H12_DEV void obs_rng(const KParams& P, const AsmArgs& A, int e, int blk, uint32_t r[4]) {
+  philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + e), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)blk, A.hi, r);
+}
+
+H12_DEV float noisy_component(const KParams& P, const AsmArgs& A, int e, int c) {
+  float x = A.frame[(size_t)c * A.n + e];
+  int t = noise_index(c);
+  if (t < 0) return x;
+  uint32_t r[4];
+  obs_rng(P, A, e, t >> 2, r);
+  uint32_t rv = (t & 3) == 0 ? r[0] : ((t & 3) == 1 ? r[1] : ((t & 3) == 2 ? r[2] : r[3]));
+  return x + noise_of(P, t, rv);
+}
+
+__global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
+  const int n = A.n;
+  const int r0 = blockIdx.x * ASM_ROWS;
+  const int rows = min(ASM_ROWS, n - r0);
   const size_t base = (size_t)r0 * H12_NOBS;
-  float v[SHIFT_PER_THREAD];
-  int dst[SHIFT_PER_THREAD];
+  float v[ASM_PER_THREAD];
+  int dst[ASM_PER_THREAD];
 #pragma unroll
-  for (int u = 0; u < SHIFT_PER_THREAD; ++u) {
-    int idx = u * SHIFT_BLOCK + threadIdx.x;
-    int col = idx % H12_NOBS;
-    int d = col < 90 ? 3 : 12;
-    int rel = col < 90 ? col % 30 : (col - 90) % 120;
-    bool ok = idx < total && rel < (H12_NHIST - 1) * d;
-    dst[u] = ok ? idx : -1;
-    v[u] = ok ? obs_prev[base + idx + d] : 0.f;
+  for (int u = 0; u < ASM_PER_THREAD; ++u) {
+    int k = u * ASM_BLOCK + threadIdx.x;
+    dst[u] = -1;
+    v[u] = 0.f;
+    if (k < rows * ASM_HIST) {
+      int row = k / ASM_HIST;
+      int kk = k - row * ASM_HIST;
+      int c, col, d;
+      if (kk < 81) {
+        int t = kk / 27, r = kk - 27 * t, hh = r / 3, a = r - 3 * hh;
+        c = 3 * t + a; col = 30 * t + 3 * hh + a; d = 3;
+      } else {
+        int k2 = kk - 81, t = k2 / 108, r = k2 - 108 * t, hh = r / 12, a = r - 12 * hh;
+        c = 9 + 12 * t + a; col = 90 + 120 * t + 12 * hh + a; d = 12;
+      }
+      const int e = r0 + row;
+      bool fill;
+      if (asm_row_written(A, e, fill)) {
+        v[u] = fill ? noisy_component(P, A, e, c) : A.obs_prev[base + (size_t)row * H12_NOBS + col + d];
+        dst[u] = row * H12_NOBS + col;
+      }
+    }
+  }
+  // newest slot: one component group per thread
+  constexpr int hl = H12_NHIST - 1;
+  float fv[4];
+  int fdst[4] = {-1, -1, -1, -1};
+  if ((int)threadIdx.x < rows * ASM_GROUPS) {
+    const int row = threadIdx.x / ASM_GROUPS;
+    const int grp = threadIdx.x - row * ASM_GROUPS;
+    const int e = r0 + row;
+    bool fill;
+    if (asm_row_written(A, e, fill)) {
+      if (grp < 8) {
+        uint32_t r[4];
+        obs_rng(P, A, e, grp, r);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          int t = 4 * grp + a;
+          if (t < 30) {
+            int c = t < 6 ? t : t + 3;
+            fv[a] = A.frame[(size_t)c * n + e] + noise_of(P, t, r[a]);
+            fdst[a] = row * H12_NOBS + obs_col(c, hl);
+          }
+        }
+      } else {
+        const int c0 = grp == 8 ? 6 : 33 + 4 * (grp - 9);
+        const int nc = grp == 8 ? 3 : 4;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          if (a < nc) {
+            fv[a] = A.frame[(size_t)(c0 + a) * n + e];
+            fdst[a] = row * H12_NOBS + obs_col(c0 + a, hl);
+          }
+      }
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < SHIFT_PER_THREAD; ++u)
-    if (dst[u] >= 0) obs[base + dst[u]] = v[u];
+  for (int u = 0; u < ASM_PER_THREAD; ++u)
+    if (dst[u] >= 0) A.obs[base + dst[u]] = v[u];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+    if (fdst[a] >= 0) A.obs[base + fdst[a]] = fv[a];
 }
 
 // ------------------------------------------------------------------ kernels
@@ -781,25 +870,25 @@ struct StepArgs {
   float* foot_force;
   const uint8_t* reset_mask;
   const float* q_ref;  // physics-only hook
+  float* frame;        // [45][n] noise-free observation frame scratch (handle-owned)
   int64_t env_offset;
   uint32_t lo, hi;
   int n_substeps;
 };
 
 __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
-  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
   const bool active = e < W.n;
-  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
   const uint32_t g = (uint32_t)(A.env_offset + e);
-  bool fill_row = false;
+  PH_INIT();
   if (active) {
     EnvSt s;
     load_phys(W, e, leg, s);
+    PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
 #pragma unroll
@@ -851,6 +940,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
         fmax_torso = fmaxf(fmax_torso, wgt * fsqrt(fr.torso[0] * fr.torso[0] + fr.torso[1] * fr.torso[1] + fr.torso[2] * fr.torso[2]));
       }
     }
+    PH(1);
     load_mdp(W, e, leg, s);
     // ContactSensor._update_buffers_impl replayed per physics step (threshold 1 N, elapsed = dt)
     for (int st = 0; st < dec; ++st) {
@@ -864,6 +954,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     }
     s.eplen += 1;
     // ---- terminations: time_out, illegal_contact (pair-combined)
+    PH(2);
     const bool tout = s.eplen >= P.max_len;
     int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
     const int term = ill | pair_swap_i(ill);
@@ -956,6 +1047,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       r += v;
       s.epsum[t] += v;
     }
+    PH(3);
     const bool reset = term || tout;
     if (leg == 0) {
       A.rew[e] = r;
@@ -965,24 +1057,14 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     if (A.applied_torque)
       for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
-    // ---- episode log: wave-reduced, one atomic per value per wave that saw a reset
-    if (A.log_acc) {
-      const bool mine = reset && leg == 0;
-      if (__ballot(mine)) {
-        float lv[15];
-        for (int t = 0; t < H12_NREW; ++t) lv[t] = mine ? s.epsum[t] : 0.f;
-        lv[12] = mine ? 1.f : 0.f;
-        lv[13] = (mine && tout) ? 1.f : 0.f;
-        lv[14] = (mine && term) ? 1.f : 0.f;
-        for (int t = 0; t < 15; ++t) {
-          float x = lv[t];
-          for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-          lv[t] = x;
-        }
-        if ((threadIdx.x & 63) == 0)
-          for (int t = 0; t < 15; ++t) atomicAdd(&A.log_acc[t], lv[t]);
-      }
+    // ---- episode log: the (few) resetting envs add their sums directly (no-return atomics)
+    if (A.log_acc && reset && leg == 0) {
+      for (int t = 0; t < H12_NREW; ++t) atomicAdd(&A.log_acc[t], s.epsum[t]);
+      atomicAdd(&A.log_acc[12], 1.f);
+      if (tout) atomicAdd(&A.log_acc[13], 1.f);
+      if (term) atomicAdd(&A.log_acc[14], 1.f);
     }
+    PH(4);
     if (reset) env_reset(P, s, leg, g, A.lo, A.hi);
     else s.since_reset = min(s.since_reset + 1, 2);
     // ---- CommandTerm.compute(step_dt)
@@ -990,52 +1072,42 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     if (s.cmd_time <= 0.f) cmd_resample(P, s, g, A.lo, A.hi);
     cmd_update(P, s);
     // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
-    obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
-    fill_row = reset;
+    PH(5);
+    obs_frame(P, s, leg, e, W.n, A.frame);
+    PH(6);
     store_env(W, e, leg, s);
+    PH(7);
   }
-  __syncthreads();
-  write_frames(A.obs, e0, n_rows, s_frame, active, fill_row);
 }
 
 __global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, StepArgs A) {
-  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
-  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
   const bool sel = e < W.n && (!A.reset_mask || A.reset_mask[e]);
   if (sel) {
     const uint32_t g = (uint32_t)(A.env_offset + e);
     EnvSt s;
     load_env(W, e, leg, s);
     env_reset(P, s, leg, g, A.lo, A.hi);
-    obs_frame(P, s, leg, g, A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
+    obs_frame(P, s, leg, e, W.n, A.frame);
     store_env(W, e, leg, s);
   }
-  __syncthreads();
-  write_frames(A.obs, e0, n_rows, s_frame, sel, true);
 }
 
 // ObservationManager.compute() outside step(): new frame from the current state, history shifted
 // (or filled where fill_mask[e]); RNG counter domain (observe call, 0xFFFFFFFE)
 __global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, StepArgs A) {
-  __shared__ float s_frame[ENVS_PER_BLOCK * H12_OBS_FRAME];
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
-  const int n_rows = min(ENVS_PER_BLOCK, W.n - e0);
-  bool fill_row = false;
   if (e < W.n) {
     EnvSt s;
     load_env(W, e, leg, s);
-    obs_frame(P, s, leg, (uint32_t)(A.env_offset + e), A.lo, A.hi, &s_frame[lane_pair * H12_OBS_FRAME]);
-    fill_row = A.reset_mask && A.reset_mask[e];
+    obs_frame(P, s, leg, e, W.n, A.frame);
   }
-  __syncthreads();
-  write_frames(A.obs, e0, n_rows, s_frame, e < W.n, fill_row);
 }
 
 // parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
@@ -1070,6 +1142,7 @@ struct Handle {
   int64_t env_offset;
   uint64_t reset_calls, observe_calls;
   double flops_per_env;
+  float* frame;  // [45][n] observation frame scratch between the env kernels and obs_assemble_kernel
 };
 
 bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
@@ -1163,9 +1236,25 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
 
 int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
 
-void launch_shift(const Handle* h, const float* obs_prev, float* obs, hipStream_t stream) {
-  hipLaunchKernelGGL(obs_shift_kernel, dim3((h->W.n + SHIFT_ROWS - 1) / SHIFT_ROWS), dim3(SHIFT_BLOCK), 0, stream,
-                     obs_prev, obs, h->W.n);
+// obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
+int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
+                    const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream) {
+  AsmArgs A = {};
+  A.obs_prev = obs_prev;
+  A.obs = obs;
+  A.frame = h->frame;
+  A.fill_a = fill_a;
+  A.fill_b = fill_b;
+  A.sel = sel;
+  A.reset_mode = reset_mode;
+  A.n = h->W.n;
+  A.env_offset = h->env_offset;
+  A.lo = lo;
+  A.hi = hi;
+  const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
+  hipLaunchKernelGGL(obs_assemble_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 }  // namespace
@@ -1252,6 +1341,12 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->W.F = (float*)state_dev;
   h->W.I = (int32_t*)((float*)state_dev + (size_t)H12_NF_FLOAT * n_envs);
   h->W.n = n_envs;
+  e = hipMalloc(&h->frame, sizeof(float) * H12_OBS_FRAME * (size_t)n_envs);
+  if (e != hipSuccess) {
+    if (h->own) (void)hipFree(state_dev);
+    delete h;
+    return set_err(H12_E_ALLOC, "hipMalloc(frame): %s", hipGetErrorString(e));
+  }
   h->device = device;
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -1268,6 +1363,7 @@ void h12env_destroy(h12env* hh) {
   Handle* h = (Handle*)hh;
   if (!h) return;
   if (h->own && h->W.F) (void)hipFree(h->W.F);
+  if (h->frame) (void)hipFree(h->frame);
   delete h;
 }
 
@@ -1281,10 +1377,11 @@ int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
   A.env_offset = h->env_offset;
   A.lo = (uint32_t)h->reset_calls;
   A.hi = 0xFFFFFFFFu;
+  A.frame = h->frame;
   h->reset_calls++;
   hipLaunchKernelGGL(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
-  return 0;
+  return launch_assemble(h, nullptr, obs, nullptr, nullptr, mask, 1, A.lo, A.hi, (hipStream_t)stream);
 }
 
 int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h12env_step_out* out,
@@ -1307,10 +1404,12 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.env_offset = h->env_offset;
   A.lo = (uint32_t)step_index;
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
-  launch_shift(h, obs_prev, out->obs, (hipStream_t)stream);
+  A.frame = h->frame;
   hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
-  return 0;
+  // fill = terminated | truncated: the envs reset inside the step restart their history
+  return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
+                         (hipStream_t)stream);
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
@@ -1325,10 +1424,10 @@ int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t*
   A.lo = (uint32_t)h->observe_calls;
   A.hi = 0xFFFFFFFEu;
   h->observe_calls++;
-  launch_shift(h, obs_prev, obs, (hipStream_t)stream);
+  A.frame = h->frame;
   hipLaunchKernelGGL(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
-  return 0;
+  return launch_assemble(h, obs_prev, obs, fill_mask, nullptr, nullptr, 0, A.lo, A.hi, (hipStream_t)stream);
 }
 
 int h12env_step_physics(h12env* hh, const float* q_ref, int n_substeps, void* stream) {
@@ -1353,6 +1452,18 @@ void* h12env_field_ptr(h12env* hh, int is_int, int field) {
   if (field < 0 || field >= H12_NF_FLOAT) { set_err(H12_E_ARG, "float field %d out of range", field); return nullptr; }
   return h->W.F + (size_t)field * h->W.n;
 }
+
+#ifdef H12_PHASE_PROFILE
+int h12env_phase_profile(unsigned long long* out16, int clear) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 16));
+  if (clear) {
+    unsigned long long z[16] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z));
+  }
+  return 0;
+}
+#endif
 
 int h12env_num_envs(const h12env* hh) { return hh ? ((const Handle*)hh)->W.n : -1; }
 
