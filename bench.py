@@ -38,11 +38,27 @@ def parse():
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc-file", type=str, default=None,
-                   help="JSON with per-launch HBM bytes from a rocprofv3 --pmc run (fills roofline.traffic)")
+                   help="tools/profile.sh summary with per-launch HBM bytes (default profiles/latest_pmc.json)")
     p.add_argument("--profile-only", action="store_true", help="timed loop only (for rocprofv3 runs)")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
+
+
+def load_pmc(path):
+    """HBM bytes per launch of step_kernel / obs_assemble_kernel from a tools/profile.sh summary, used
+    only if it was measured on the current kernel source (sha256 of csrc/h12env.hip)."""
+    import hashlib
+    p = Path(path) if path else ROOT / "profiles" / "latest_pmc.json"
+    if not p.exists():
+        return None, None, None
+    d = json.loads(p.read_text())
+    src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
+    if d.get("source_sha256") != src:
+        return None, None, f"{p.name}: stale (kernel source changed)"
+    k = d.get("kernels", {})
+    return (k.get("step_kernel", {}).get("hbm_bytes_per_launch"), k.get("obs_assemble_kernel", {}).get("hbm_bytes_per_launch"),
+            f"{p.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH doubled per MI355X_MICROARCH.md)")
 
 
 def cpu_baseline(seconds: float):
@@ -129,26 +145,24 @@ def main():
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * dt / K}))
         return
 
-    # per-launch kernel duration with HIP events on the env's stream (separate pass, so the timed
-    # region above is not perturbed by event records)
-    stream = torch.cuda.current_stream(dev)
+    # per-launch kernel durations with HIP events recorded by the library on the env's stream around
+    # each of its two kernels (separate pass, so the timed region above is not perturbed)
     M = min(K, 200)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(M)]
+    env.set_kernel_timing(True)
     for i in range(M):
-        ev[i][0].record(stream)
         env.step(actions[i % pool])
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-    kern_ms_avg = sum(kern_ms) / len(kern_ms)
-    bytes_env, flops_env = env.step_cost()
+    env_ms, obs_ms, n_timed = env.kernel_times()
+    env.set_kernel_timing(False)
+    kern_ms_avg = env_ms / n_timed
+    obs_ms_avg = obs_ms / n_timed
+    bytes_env, flops_env = env.kernel_cost(0)
+    obs_bytes_env, _ = env.kernel_cost(1)
+    step_bytes_env, _ = env.step_cost()
 
     value = world * n * K / dt
     if rank == 0:
         achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
-        traffic = None
-        if args.pmc_file and Path(args.pmc_file).exists():
-            traffic = json.loads(Path(args.pmc_file).read_text()).get("hbm_bytes_per_launch")
+        traffic, obs_traffic, pmc_src = load_pmc(args.pmc_file)
         out = {
             "metric": METRIC,
             "value": value,
@@ -180,11 +194,21 @@ def main():
                 "traffic": traffic,
                 "kernel": "step_kernel",
                 "kernel_ms_avg": kern_ms_avg,
-                "kernel_ms_p50": kern_ms[len(kern_ms) // 2],
-                "algorithmic_bytes_per_env_step": bytes_env,
+                "algorithmic_bytes_per_launch": bytes_env * n,
+                "traffic_source": pmc_src,
                 "valu_flops_per_env_step": flops_env,
                 "valu_tflops": flops_env * n / (kern_ms_avg * 1e-3) / 1e12,
                 "valu_frac": flops_env * n / (kern_ms_avg * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                "secondary": {
+                    "kernel": "obs_assemble_kernel",
+                    "bound": "hbm",
+                    "kernel_ms_avg": obs_ms_avg,
+                    "achieved": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9,
+                    "frac": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "traffic": obs_traffic,
+                },
+                "step_bytes_per_env": step_bytes_env,
+                "step_achieved_gbs": step_bytes_env * n * K / dt / 1e9,
             },
             "cpu_baseline": None,
         }

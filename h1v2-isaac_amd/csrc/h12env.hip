@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "../../include/h12env.h"
 #include "h12_math.h"
@@ -733,14 +734,14 @@ H12_DEV float noise_of(const KParams& P, int t, uint32_t r) {
   return P.corrupt ? (-nmax + 2.f * nmax * u01(r)) : 0.f;
 }
 
-// ObservationManager.compute + CircularBuffer.append for a batch of envs, full-chip.  Each block
-// owns ASM_ROWS whole rows: every thread loads its share of the shifted history
-// (obs[e, slot h] = obs_prev[e, slot h + 1], h < 9) and the first ASM_ROWS * 12 threads build the
-// noisy new frame, one component group each (group g < 8 = Philox block g of the noise stream, 4
-// noise indices; g = 8 command; g = 9..11 last action); all loads precede the barrier and all
-// stores follow it, so obs may alias obs_prev.  Rows being (re)filled take the noisy new frame in
-// every slot.  Reset mode writes only rows with sel[e] (all if sel is NULL) and fills them;
-// otherwise every row is written and fill[e] = fill_a[e] | fill_b[e].
+// ObservationManager.compute + CircularBuffer.append for a batch of envs, full-chip.  One block owns
+// ASM_ROWS whole rows (4 x 1800 B, 16-byte aligned): the rows are staged through LDS with float4
+// loads, the rows' 8 Philox noise blocks each are drawn once (one wave), and every output float4 is
+// assembled from LDS -- the shifted history obs[e, slot h] = obs_prev[e, slot h + 1] (h < 9), or
+// the noisy new frame in the newest slot and in every slot of a row being (re)filled -- and stored
+// with one float4 store.  All global reads precede the barrier, so obs may alias obs_prev.
+// Reset mode: rows with sel[e] (all if sel is NULL) are filled, the others are rewritten unchanged
+// from obs itself.  Otherwise fill[e] = fill_a[e] | fill_b[e].
 struct AsmArgs {
   const float* obs_prev;
   float* obs;
@@ -749,16 +750,18 @@ struct AsmArgs {
   const uint8_t* fill_b;
   const uint8_t* sel;
   int reset_mode;
+  int vec;  // obs and the source rows are 16-byte aligned
   int n;
   int64_t env_offset;
   uint32_t lo, hi;
 };
 constexpr int ASM_BLOCK = 256;
 constexpr int ASM_ROWS = 4;
-constexpr int ASM_HIST = H12_NOBS - H12_OBS_FRAME;  // 405 history slots per row
-constexpr int ASM_PER_THREAD = (ASM_ROWS * ASM_HIST + ASM_BLOCK - 1) / ASM_BLOCK;
-constexpr int ASM_GROUPS = 12;
-static_assert(ASM_ROWS * ASM_GROUPS <= ASM_BLOCK, "one frame group per thread");
+constexpr int ASM_F4 = ASM_ROWS * H12_NOBS / 4;
+constexpr int ASM_NOISE = 32;  // 8 Philox blocks x 4 uniforms per row (30 used)
+constexpr int ASM_RNG_T0 = 192;  // first thread of the noise wave
+static_assert((ASM_ROWS * H12_NOBS) % 4 == 0, "float4 rows");
+static_assert(ASM_ROWS * H12_OBS_FRAME <= ASM_RNG_T0 && ASM_RNG_T0 + 8 * ASM_ROWS <= ASM_BLOCK, "thread roles");
 
 H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
   if (A.reset_mode) {
@@ -769,92 +772,85 @@ H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
   return true;
 }
 
-H12_DEV void obs_rng(const KParams& P, const AsmArgs& A, int e, int blk, uint32_t r[4]) {
-  philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + e), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)blk, A.hi, r);
-}
-
-H12_DEV float noisy_component(const KParams& P, const AsmArgs& A, int e, int c) {
-  float x = A.frame[(size_t)c * A.n + e];
-  int t = noise_index(c);
-  if (t < 0) return x;
-  uint32_t r[4];
-  obs_rng(P, A, e, t >> 2, r);
-  uint32_t rv = (t & 3) == 0 ? r[0] : ((t & 3) == 1 ? r[1] : ((t & 3) == 2 ? r[2] : r[3]));
-  return x + noise_of(P, t, rv);
+// value of row-local obs column col (0..449): unchanged, shifted history or noisy new frame
+H12_DEV float asm_value(int row, int col, const float* s_hist, const float* s_frame, const float* s_noise,
+                        bool write, bool fill) {
+  const int p = row * H12_NOBS + col;
+  if (!write) return s_hist[p];
+  int c, hh, d;
+  if (col < 90) {
+    int t = col / 30, r = col - 30 * t;
+    hh = r / 3;
+    c = 3 * t + (r - 3 * hh);
+    d = 3;
+  } else {
+    int k = col - 90, t = k / 120, r = k - 120 * t;
+    hh = r / 12;
+    c = 9 + 12 * t + (r - 12 * hh);
+    d = 12;
+  }
+  if (!fill && hh < H12_NHIST - 1) return s_hist[p + d];
+  float x = s_frame[row * H12_OBS_FRAME + c];
+  int tn = noise_index(c);
+  return tn < 0 ? x : x + s_noise[row * ASM_NOISE + tn];
 }
 
 __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
+  __shared__ __attribute__((aligned(16))) float s_hist[ASM_ROWS * H12_NOBS];
+  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];
+  __shared__ float s_noise[ASM_ROWS * ASM_NOISE];
+  __shared__ int s_write[ASM_ROWS], s_fill[ASM_ROWS];
   const int n = A.n;
+  const int tid = threadIdx.x;
   const int r0 = blockIdx.x * ASM_ROWS;
   const int rows = min(ASM_ROWS, n - r0);
+  const bool full = A.vec && rows == ASM_ROWS;
   const size_t base = (size_t)r0 * H12_NOBS;
-  float v[ASM_PER_THREAD];
-  int dst[ASM_PER_THREAD];
-#pragma unroll
-  for (int u = 0; u < ASM_PER_THREAD; ++u) {
-    int k = u * ASM_BLOCK + threadIdx.x;
-    dst[u] = -1;
-    v[u] = 0.f;
-    if (k < rows * ASM_HIST) {
-      int row = k / ASM_HIST;
-      int kk = k - row * ASM_HIST;
-      int c, col, d;
-      if (kk < 81) {
-        int t = kk / 27, r = kk - 27 * t, hh = r / 3, a = r - 3 * hh;
-        c = 3 * t + a; col = 30 * t + 3 * hh + a; d = 3;
-      } else {
-        int k2 = kk - 81, t = k2 / 108, r = k2 - 108 * t, hh = r / 12, a = r - 12 * hh;
-        c = 9 + 12 * t + a; col = 90 + 120 * t + 12 * hh + a; d = 12;
-      }
-      const int e = r0 + row;
-      bool fill;
-      if (asm_row_written(A, e, fill)) {
-        v[u] = fill ? noisy_component(P, A, e, c) : A.obs_prev[base + (size_t)row * H12_NOBS + col + d];
-        dst[u] = row * H12_NOBS + col;
-      }
-    }
+  const float* src = (A.reset_mode ? A.obs : A.obs_prev) + base;
+  if (tid < ASM_ROWS) {
+    bool fill = false;
+    int w = tid < rows ? (int)asm_row_written(A, r0 + tid, fill) : 0;
+    s_write[tid] = w;
+    s_fill[tid] = fill ? 1 : 0;
   }
-  // newest slot: one component group per thread
-  constexpr int hl = H12_NHIST - 1;
-  float fv[4];
-  int fdst[4] = {-1, -1, -1, -1};
-  if ((int)threadIdx.x < rows * ASM_GROUPS) {
-    const int row = threadIdx.x / ASM_GROUPS;
-    const int grp = threadIdx.x - row * ASM_GROUPS;
-    const int e = r0 + row;
-    bool fill;
-    if (asm_row_written(A, e, fill)) {
-      if (grp < 8) {
-        uint32_t r[4];
-        obs_rng(P, A, e, grp, r);
+  if (full) {
+    for (int j = tid; j < ASM_F4; j += ASM_BLOCK)
+      reinterpret_cast<float4*>(s_hist)[j] = reinterpret_cast<const float4*>(src)[j];
+  } else {
+    for (int j = tid; j < rows * H12_NOBS; j += ASM_BLOCK) s_hist[j] = src[j];
+  }
+  if (tid < rows * H12_OBS_FRAME) {
+    int row = tid / H12_OBS_FRAME, c = tid - row * H12_OBS_FRAME;
+    s_frame[tid] = A.frame[(size_t)c * n + r0 + row];
+  } else if (tid >= ASM_RNG_T0 && tid < ASM_RNG_T0 + 8 * rows) {
+    int k = tid - ASM_RNG_T0, row = k >> 3, blk = k & 7;
+    uint32_t r[4];
+    philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + r0 + row), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)blk,
+           A.hi, r);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          int t = 4 * grp + a;
-          if (t < 30) {
-            int c = t < 6 ? t : t + 3;
-            fv[a] = A.frame[(size_t)c * n + e] + noise_of(P, t, r[a]);
-            fdst[a] = row * H12_NOBS + obs_col(c, hl);
-          }
-        }
-      } else {
-        const int c0 = grp == 8 ? 6 : 33 + 4 * (grp - 9);
-        const int nc = grp == 8 ? 3 : 4;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-          if (a < nc) {
-            fv[a] = A.frame[(size_t)(c0 + a) * n + e];
-            fdst[a] = row * H12_NOBS + obs_col(c0 + a, hl);
-          }
-      }
+    for (int a = 0; a < 4; ++a) {
+      int t = 4 * blk + a;
+      s_noise[row * ASM_NOISE + t] = t < 30 ? noise_of(P, t, r[a]) : 0.f;
     }
   }
   __syncthreads();
+  float* dst = A.obs + base;
+  if (full) {
+    for (int j = tid; j < ASM_F4; j += ASM_BLOCK) {
+      float v[4];
 #pragma unroll
-  for (int u = 0; u < ASM_PER_THREAD; ++u)
-    if (dst[u] >= 0) A.obs[base + dst[u]] = v[u];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-    if (fdst[a] >= 0) A.obs[base + fdst[a]] = fv[a];
+      for (int q = 0; q < 4; ++q) {
+        int pp = 4 * j + q, row = pp / H12_NOBS, col = pp - row * H12_NOBS;
+        v[q] = asm_value(row, col, s_hist, s_frame, s_noise, s_write[row], s_fill[row]);
+      }
+      reinterpret_cast<float4*>(dst)[j] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    for (int pp = tid; pp < rows * H12_NOBS; pp += ASM_BLOCK) {
+      int row = pp / H12_NOBS, col = pp - row * H12_NOBS;
+      if (s_write[row]) dst[pp] = asm_value(row, col, s_hist, s_frame, s_noise, true, s_fill[row]);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ kernels
@@ -1143,7 +1139,24 @@ struct Handle {
   uint64_t reset_calls, observe_calls;
   double flops_per_env;
   float* frame;  // [45][n] observation frame scratch between the env kernels and obs_assemble_kernel
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // 3 per timed step: before env kernel, between, after assembly
+  size_t n_timed = 0;
 };
+
+constexpr size_t MAX_TIMED_STEPS = 4096;
+
+void timing_mark(Handle* h, int k, hipStream_t stream) {
+  if (!h->timing || h->n_timed >= MAX_TIMED_STEPS) return;
+  size_t i = 3 * h->n_timed + k;
+  while (h->ev.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) { h->timing = false; return; }
+    h->ev.push_back(e);
+  }
+  (void)hipEventRecord(h->ev[i], stream);
+  if (k == 2) h->n_timed++;
+}
 
 bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
 
@@ -1251,6 +1264,8 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.env_offset = h->env_offset;
   A.lo = lo;
   A.hi = hi;
+  const float* src = reset_mode ? obs : obs_prev;
+  A.vec = (((uintptr_t)obs | (uintptr_t)src) & 15u) == 0;
   const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
   hipLaunchKernelGGL(obs_assemble_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A);
   HIP_TRY(hipGetLastError());
@@ -1364,6 +1379,7 @@ void h12env_destroy(h12env* hh) {
   if (!h) return;
   if (h->own && h->W.F) (void)hipFree(h->W.F);
   if (h->frame) (void)hipFree(h->frame);
+  for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   delete h;
 }
 
@@ -1405,11 +1421,15 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.lo = (uint32_t)step_index;
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   A.frame = h->frame;
+  timing_mark(h, 0, (hipStream_t)stream);
   hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
+  timing_mark(h, 1, (hipStream_t)stream);
   // fill = terminated | truncated: the envs reset inside the step restart their history
-  return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
-                         (hipStream_t)stream);
+  int rc = launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
+                           (hipStream_t)stream);
+  timing_mark(h, 2, (hipStream_t)stream);
+  return rc;
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
@@ -1467,16 +1487,62 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 
 int h12env_num_envs(const h12env* hh) { return hh ? ((const Handle*)hh)->W.n : -1; }
 
-int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_env) {
+int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, double* flops_per_env) {
   const Handle* h = (const Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
-  // compulsory HBM bytes per env step: state read + write, actions, obs (9 old frames read, 10
-  // written), reward / terminated / truncated
-  double state = (double)(H12_NF_FLOAT + H12_NF_INT) * 4.0 * 2.0;
-  double obs = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_NOBS * 4.0;
-  double io = (double)H12_NJ * 4.0 + 4.0 + 2.0;
-  if (bytes_per_env) *bytes_per_env = state + obs + io;
-  if (flops_per_env) *flops_per_env = h->flops_per_env;
+  double bytes, flops;
+  if (kernel == 0) {
+    // state read + write, actions, reward / terminated / truncated, applied torque and foot force
+    // (the ArticulationData / ContactSensor views), the noise-free frame
+    bytes = (double)(H12_NF_FLOAT + H12_NF_INT) * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 +
+            (double)H12_NJ * 4.0 + 2.0 * 4.0 + (double)H12_OBS_FRAME * 4.0;
+    flops = h->flops_per_env;
+  } else if (kernel == 1) {
+    // 9 old frames + the new frame + the two reset flags read, 10 frames written
+    bytes = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_OBS_FRAME * 4.0 + 2.0 + (double)H12_NOBS * 4.0;
+    flops = 30.0 * 3.0 + 8.0 * 10.0 * 6.0;  // noise affine + Philox rounds
+  } else {
+    return set_err(H12_E_ARG, "kernel must be 0 or 1 (got %d)", kernel);
+  }
+  if (bytes_per_env) *bytes_per_env = bytes;
+  if (flops_per_env) *flops_per_env = flops;
+  return 0;
+}
+
+int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_env) {
+  double b0, f0, b1, f1;
+  if (int rc = h12env_kernel_cost(hh, 0, &b0, &f0)) return rc;
+  if (int rc = h12env_kernel_cost(hh, 1, &b1, &f1)) return rc;
+  // the frame round trip between the kernels is not compulsory traffic of the step
+  if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * (double)H12_OBS_FRAME * 4.0;
+  if (flops_per_env) *flops_per_env = f0 + f1;
+  return 0;
+}
+
+int h12env_set_kernel_timing(h12env* hh, int enable) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  h->timing = enable != 0;
+  h->n_timed = 0;
+  return 0;
+}
+
+int h12env_kernel_times(h12env* hh, double* env_ms, double* obs_ms, int* n_steps) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  double a = 0.0, b = 0.0;
+  if (h->n_timed > 0) HIP_TRY(hipEventSynchronize(h->ev[3 * h->n_timed - 1]));
+  for (size_t i = 0; i < h->n_timed; ++i) {
+    float t0 = 0.f, t1 = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t0, h->ev[3 * i], h->ev[3 * i + 1]));
+    HIP_TRY(hipEventElapsedTime(&t1, h->ev[3 * i + 1], h->ev[3 * i + 2]));
+    a += t0;
+    b += t1;
+  }
+  if (env_ms) *env_ms = a;
+  if (obs_ms) *obs_ms = b;
+  if (n_steps) *n_steps = (int)h->n_timed;
+  h->n_timed = 0;
   return 0;
 }
 

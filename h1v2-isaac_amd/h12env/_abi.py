@@ -184,6 +184,12 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_num_envs.restype = C.c_int
     lib.h12env_step_cost.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.h12env_step_cost.restype = C.c_int
+    lib.h12env_kernel_cost.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.h12env_kernel_cost.restype = C.c_int
+    lib.h12env_set_kernel_timing.argtypes = [vp, C.c_int]
+    lib.h12env_set_kernel_timing.restype = C.c_int
+    lib.h12env_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    lib.h12env_kernel_times.restype = C.c_int
     lib.h12env_last_error.argtypes = []
     lib.h12env_last_error.restype = C.c_char_p
     lib.h12env_abi_version.argtypes = []
@@ -209,5 +215,6 @@ def check(lib, rc: int, what: str):
 EXPORTED_SYMBOLS = [
     "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
-    "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct",
+    "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
+    "h12env_set_kernel_timing", "h12env_kernel_times",
 ]

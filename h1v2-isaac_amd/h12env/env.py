@@ -366,3 +366,19 @@ class H12VelocityEnv:
         b, f = C.c_double(), C.c_double()
         self._lib.h12env_step_cost(self._h, C.byref(b), C.byref(f))
         return b.value, f.value
+
+    def kernel_cost(self, kernel: int):
+        """(compulsory HBM bytes, counted FLOPs) per env of kernel 0 (env step) or 1 (obs assembly)."""
+        b, f = C.c_double(), C.c_double()
+        check(self._lib, self._lib.h12env_kernel_cost(self._h, kernel, C.byref(b), C.byref(f)), "h12env_kernel_cost")
+        return b.value, f.value
+
+    def set_kernel_timing(self, enable: bool):
+        """Instrumentation: record HIP events around the two kernels of every step (off by default)."""
+        check(self._lib, self._lib.h12env_set_kernel_timing(self._h, int(enable)), "h12env_set_kernel_timing")
+
+    def kernel_times(self):
+        """(env-kernel ms, obs-kernel ms, timed steps) summed since timing was enabled / last read."""
+        a, b, n = C.c_double(), C.c_double(), C.c_int()
+        check(self._lib, self._lib.h12env_kernel_times(self._h, C.byref(a), C.byref(b), C.byref(n)), "h12env_kernel_times")
+        return a.value, b.value, n.value

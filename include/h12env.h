@@ -204,8 +204,17 @@ int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* str
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);
-/* Algorithmic accounting of one env step for the roofline report. */
+/* Algorithmic accounting of one env step for the roofline report (both kernels of h12env_step). */
 int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_env);
+/* Per-kernel accounting: kernel 0 = the env kernel of h12env_step (physics + MDP), 1 = the observation
+ * assembly kernel (history shift + noise + fills).  Compulsory HBM bytes and counted FLOPs per env. */
+int h12env_kernel_cost(const h12env* h, int kernel, double* bytes_per_env, double* flops_per_env);
+/* Instrumentation (off by default): while enabled, h12env_step records HIP events around its two
+ * kernels on the caller's stream (at most 4096 steps are kept).  h12env_kernel_times synchronises on
+ * the last event, returns the summed milliseconds of each kernel and the number of timed steps, and
+ * clears the record. */
+int h12env_set_kernel_timing(h12env* h, int enable);
+int h12env_kernel_times(h12env* h, double* env_ms, double* obs_ms, int* n_steps);
 const char* h12env_last_error(void);
 int h12env_abi_version(void);
 /* sizeof of the ABI structs as compiled (0 = h12env_model, 1 = h12env_config, 2 = h12env_step_out),
