@@ -40,6 +40,10 @@ def parse():
     p.add_argument("--pmc-file", type=str, default=None,
                    help="tools/profile.sh summary with per-launch HBM bytes (default profiles/latest_pmc.json)")
     p.add_argument("--profile-only", action="store_true", help="timed loop only (for rocprofv3 runs)")
+    p.add_argument("--mode", choices=("env", "train"), default="env",
+                   help="env: the metric (random-action rollout); train: BASELINE configs C3/C4 (PPO iterations "
+                        "of the train.py runner, rollout all-gathered over RCCL when N > 1)")
+    p.add_argument("--iterations", type=int, default=5, help="train mode: timed PPO iterations")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
@@ -91,6 +95,62 @@ def cpu_baseline(seconds: float):
                       f"({dt:.1f} s) of the same random-action Flat-H12 workload, {threads} host threads"}
 
 
+def train_mode(args, world, rank, dev, torch, dist):
+    """C3 / C4: PPO iterations (24 env steps per env + 5 epochs x 4 minibatches) of the rsl_rl-style
+    runner that scripts/train.py drives, with the agent cfg of the Flat task."""
+    sys.path.insert(0, str(ROOT / "h1v2-isaac_amd" / "shims"))
+    from biped_tasks.tasks.agents import H12_12dof_FlatPPORunnerCfg
+    from h12env import H12FlatEnvCfg
+    from h12env.env import H12VelocityEnv
+    from h12env.ppo import OnPolicyRunner
+    from isaaclab_rl.rsl_rl import RslRlVecEnvWrapper
+
+    cfg = H12FlatEnvCfg()
+    cfg.scene.num_envs = args.envs
+    cfg.sim.device = str(dev)
+    env = RslRlVecEnvWrapper(H12VelocityEnv(cfg, env_offset=rank * args.envs))
+    agent = H12_12dof_FlatPPORunnerCfg(device=str(dev))
+    runner = OnPolicyRunner(env, agent.to_dict(), log_dir=None, device=str(dev))
+    import io
+    import contextlib
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        runner.learn(max(1, args.warmup // 25), init_at_random_ep_len=True)
+    coll = learn = 0.0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.iterations):
+        with contextlib.redirect_stdout(io.StringIO()):
+            runner.learn(1)
+        st = runner.last_iteration_stats
+        coll += st["Perf/collection_time"]
+        learn += st["Perf/learning_time"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt, coll, learn], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, coll, learn = (float(x) for x in t.tolist())
+    steps = world * args.envs * agent.num_steps_per_env * args.iterations
+    if rank == 0:
+        print(json.dumps({
+            "metric": "PPO env-steps/sec (train.py loop, collection + learning), Velocity-Flat-H12_12dof",
+            "value": steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": args.iterations,
+            "warmup": max(1, args.warmup // 25), "ms_per_step": 1e3 * dt / args.iterations, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic: on-policy rollouts",
+            "config": {"workload": "C3/C4: PPO iterations, 24 steps/env/iter, 5 epochs x 4 minibatches, "
+                                   "MLP 512-256-128", "envs_per_gpu": args.envs, "global_envs": world * args.envs,
+                       "parallelism": f"env-shard x{world}" + (" + RCCL rollout all-gather + grad all-reduce"
+                                                               if world > 1 else "")},
+            "collection_env_steps_per_s": steps / coll, "collection_s_per_iter": coll / args.iterations,
+            "learning_s_per_iter": learn / args.iterations}), flush=True)
+    env.close()
+
+
 def main():
     args = parse()
     import torch
@@ -103,6 +163,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+
+    if args.mode == "train":
+        train_mode(args, world, rank, dev, torch, dist)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from h12env import H12FlatEnvCfg
     from h12env.env import H12VelocityEnv

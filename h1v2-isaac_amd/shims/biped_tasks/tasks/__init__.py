@@ -1,0 +1,25 @@
+"""Task registration (mirrors biped_tasks/tasks/locomotion/velocity/config/h12_12dof/__init__.py:14-56
+for the tasks this build implements; ids and entry-point keys unchanged)."""
+import gymnasium as gym
+
+from . import agents  # noqa: F401
+
+gym.register(
+    id="Isaac-Velocity-Flat-H12_12dof-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "h12env.cfg:H12FlatEnvCfg",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
+    },
+)
+
+gym.register(
+    id="Isaac-Velocity-Flat-H12_12dof-Play-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": f"{__name__}.play:H12FlatEnvCfg_PLAY",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
+    },
+)
