@@ -34,7 +34,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--envs", type=int, default=4096, help="envs per GPU (the metric is quoted at 4096)")
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU (the metric is quoted at 4096; C5 at 8192)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc-file", type=str, default=None,
@@ -44,6 +44,9 @@ def parse():
                    help="env: the metric (random-action rollout); train: BASELINE configs C3/C4 (PPO iterations "
                         "of the train.py runner, rollout all-gathered over RCCL when N > 1)")
     p.add_argument("--iterations", type=int, default=5, help="train mode: timed PPO iterations")
+    p.add_argument("--task", choices=("flat", "rough", "c5"), default="flat",
+                   help="flat: the metric's task; rough: Isaac-Velocity-Rough-H12_12dof-v0; c5: BASELINE config C5 "
+                        "(rough + per-env friction / torso mass, 8192 envs unless --envs)")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
@@ -153,6 +156,8 @@ def train_mode(args, world, rank, dev, torch, dist):
 
 def main():
     args = parse()
+    if args.envs is None:
+        args.envs = 8192 if args.task == "c5" else 4096
     import torch
     import torch.distributed as dist
 
@@ -172,10 +177,16 @@ def main():
         return
 
     from h12env import H12FlatEnvCfg
+    from h12env.cfg import H12RoughEnvCfg, c5_cfg
     from h12env.env import H12VelocityEnv
 
     n = args.envs
-    cfg = H12FlatEnvCfg()
+    if args.task == "flat":
+        cfg = H12FlatEnvCfg()
+    elif args.task == "rough":
+        cfg = H12RoughEnvCfg()
+    else:
+        cfg = c5_cfg()
     cfg.scene.num_envs = n
     cfg.sim.device = str(dev)
     if args.decimation:
@@ -230,8 +241,14 @@ def main():
     if rank == 0:
         achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
         traffic, obs_traffic, pmc_src = load_pmc(args.pmc_file)
+        metric, workload = METRIC, "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X"
+        if args.task != "flat":
+            metric = f"env-steps/sec at {n} envs, Velocity-Rough-H12_12dof" + (" + friction/mass randomisation (C5)"
+                                                                               if args.task == "c5" else "")
+            workload = f"Isaac-Velocity-Rough-H12_12dof-v0 random-action rollout, {n} envs per MI355X" + (
+                ", CaT startup randomisation (BASELINE C5)" if args.task == "c5" else "")
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -244,7 +261,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic: N(0,1) random actions, reset distribution of the Flat task (seeded)",
             "config": {
-                "workload": "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X",
+                "workload": workload,
                 "envs_per_gpu": n,
                 "global_envs": n * world,
                 "decimation": cfg.decimation,
@@ -279,7 +296,7 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and args.task == "flat":
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
     env.close()

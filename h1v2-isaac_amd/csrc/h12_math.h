@@ -102,6 +102,18 @@ H12_DEV void ai_rigid(AInertia& I, const float* Ibar, const float* mc, float m) 
   I.C[0] = I.C[1] = I.C[2] = m;
   I.C[3] = I.C[4] = I.C[5] = 0.f;
 }
+// add a point mass dm at c (rigidly attached, inertia about the body origin): randomize_rigid_body_mass
+// with recompute_inertia=False adds mass without changing the body's inertia about its COM
+H12_DEV void ai_add_point_mass(AInertia& I, float dm, const float* c) {
+  const float c2 = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+  I.A[0] += dm * (c2 - c[0] * c[0]); I.A[1] += dm * (c2 - c[1] * c[1]); I.A[2] += dm * (c2 - c[2] * c[2]);
+  I.A[3] -= dm * c[0] * c[1]; I.A[4] -= dm * c[0] * c[2]; I.A[5] -= dm * c[1] * c[2];
+  // B = m [c]x with m c -> dm c
+  I.B[0][1] -= dm * c[2]; I.B[0][2] += dm * c[1];
+  I.B[1][0] += dm * c[2]; I.B[1][2] -= dm * c[0];
+  I.B[2][0] -= dm * c[1]; I.B[2][1] += dm * c[0];
+  I.C[0] += dm; I.C[1] += dm; I.C[2] += dm;
+}
 H12_DEV void ai_add(AInertia& I, const AInertia& J) {
   for (int i = 0; i < 6; ++i) { I.A[i] += J.A[i]; I.C[i] += J.C[i]; }
   for (int i = 0; i < 3; ++i)

@@ -42,6 +42,14 @@ constexpr int BLOCK = 64;
 // joint axes per leg link: hip yaw z, hip pitch y, hip roll x, knee y, ankle pitch y, ankle roll x
 constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
 constexpr int MAX_DEC = 32;         // contact flags of one env step are kept in a 32-bit mask
+constexpr int FRAME_ROWS = H12_ROUGH_FRAME + 5;
+// Kernel feature level K (template): 0 = plain flat task (no per-env parameters, plane, 45-row frame:
+// the hot path compiles none of the rough-task code), 1 = extended features on the plane (rough layout,
+// per-env friction / mass; runtime flags), 2 = extended + heightfield.
+template <int K> struct Feat {
+  static constexpr bool ext = K >= 1;
+  static constexpr bool terrain = K == 2;
+};  // frame scratch rows (rough: + base position, yaw cos / sin)
 
 // experiment builds only (-DH12_PHASE_PROFILE): per-phase shader-clock cycles of step_kernel, summed
 // over waves (lane 0), read back with h12env_phase_profile.  Not part of the product library.
@@ -90,6 +98,13 @@ struct KParams {
   float rew_w[H12_NREW];
   float std2_inv, air_thr;
   uint32_t seed_lo, seed_hi;
+  // rough task / terrain / startup randomisation
+  int task, terrain, curriculum, env_mu, env_mass;
+  float n_lin, n_scan, scan_off, scan_clip, scan_res, terrain_size, ep_len_s;
+  const float* t_h;       // heightfield [nx][ny] (device)
+  const float* t_origin;  // [rows][cols][3]
+  int t_nx, t_ny, t_rows, t_cols;
+  float t_x0, t_y0, t_inv_hs;
 };
 static_assert(sizeof(KParams) < 1024, "kernarg budget");
 
@@ -113,6 +128,24 @@ H12_DEV float soft_hi(const KParams& P, int k) {
 // spatial sign of the y-mirror for component i of a motion / force 6-vector (ang x,y,z, lin x,y,z)
 H12_DEV float s6(int i, float sg) { return (i % 2 == 0) ? sg : 1.f; }
 
+// Heightfield ground (real coordinates): height at (x, y) and its slope (dh/dx, dh/dy) on the
+// triangle mesh isaaclab.terrains.utils.convert_height_field_to_mesh builds (cell (ix, iy) split along
+// its (ix, iy) -> (ix+1, iy+1) diagonal).  Outside the grid the edge cells extend (flat border).
+H12_DEV float ground(const KParams& P, float x, float y, float& gx, float& gy) {
+  float u = fminf(fmaxf((x - P.t_x0) * P.t_inv_hs, 0.f), (float)(P.t_nx - 1) - 1e-3f);
+  float v = fminf(fmaxf((y - P.t_y0) * P.t_inv_hs, 0.f), (float)(P.t_ny - 1) - 1e-3f);
+  int ix = (int)u, iy = (int)v;
+  float fu = u - (float)ix, fv = v - (float)iy;
+  const float* hp = P.t_h + (size_t)ix * P.t_ny + iy;
+  float h00 = hp[0], h01 = hp[1], h10 = hp[P.t_ny], h11 = hp[P.t_ny + 1];
+  float a, b;
+  if (fv >= fu) { a = h11 - h01; b = h01 - h00; }  // triangle (00, 11, 01)
+  else { a = h10 - h00; b = h11 - h10; }           // triangle (00, 10, 11)
+  gx = a * P.t_inv_hs;
+  gy = b * P.t_inv_hs;
+  return h00 + fu * a + fv * b;
+}
+
 // ------------------------------------------------------------------ per-lane simulation state
 struct Base {               // shared floating base, REAL coordinates (identical in both lanes)
   float pos[3], quat[4], vlin[3], wang[3];
@@ -121,6 +154,8 @@ struct Leg {                // this lane's leg in the lane frame (mirrored for t
   float q[NL], qd[NL];
   float anc[H12_NFOOT_PTS][2];
   int cmask;                // 4 bits: sole sphere (lane-frame index) in contact
+  float mus, mud;           // sole Coulomb coefficients (per env and foot, or the config's)
+  float dmass;              // mass added at the torso COM (lane 0 applies it)
 };
 struct Forces {             // net contact force of this lane's bodies (lane world frame), summed
   float foot[3], knee[3], torso[3];
@@ -128,29 +163,42 @@ struct Forces {             // net contact force of this lane's bodies (lane wor
 
 // one penalty contact (sphere centre pl in body coords, body world pose Rb/pb, body spatial velocity
 // vb in body coords); adds the body-frame spatial force into f[6]; anchored stiction for sole spheres
-template <bool ANCHOR>
+// sg: the lane's mirror sign (the heightfield is looked up at the real y = sg * y); mus / mud: Coulomb
+// coefficients of this contact (per-env sole friction or the config's)
+template <bool ANCHOR, bool TERRAIN>
 H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
-                            const float* pl, float rad, float* f, float* fw, float* anc, bool was_in) {
+                            const float* pl, float rad, float* f, float* fw, float* anc, bool was_in, float sg,
+                            float mus, float mud) {
   float xw[3];
   mv(Rb, pl, xw);
   xw[0] += pb[0]; xw[1] += pb[1]; xw[2] += pb[2];
-  float depth = rad - xw[2];
+  float nrm[3] = {0.f, 0.f, 1.f}, depth;
+  if constexpr (TERRAIN) {  // unit normal (-h_x, -h_y, 1)/|.| of the ground triangle
+    float gx, gy;
+    float hg = ground(P, xw[0], sg * xw[1], gx, gy);
+    float in = __builtin_amdgcn_rsqf(1.f + gx * gx + gy * gy);
+    nrm[0] = -gx * in; nrm[1] = -sg * gy * in; nrm[2] = in;
+    depth = rad - (xw[2] - hg) * in;
+  } else {
+    depth = rad - xw[2];
+  }
   if (!(depth > 0.f)) return false;
   float vl[3];
   cross(vb, pl, vl);
   vl[0] += vb[3]; vl[1] += vb[4]; vl[2] += vb[5];
   float vw[3];
   mv(Rb, vl, vw);
-  float fn = P.ck * depth - P.cc * vw[2];
+  float vn = TERRAIN ? nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2] : vw[2];
+  float fn = P.ck * depth - P.cc * vn;
   if (!(fn > 0.f)) return false;
   float ft0, ft1;
   if constexpr (ANCHOR) {
     float ax = was_in ? anc[0] : xw[0], ay = was_in ? anc[1] : xw[1];
     ft0 = -P.fk * (xw[0] - ax) - P.fc * vw[0];
     ft1 = -P.fk * (xw[1] - ay) - P.fc * vw[1];
-    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = P.mus * fn;
+    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = mus * fn;
     if (ftn2 > cap * cap) {
-      float sc = P.mud * fn * __builtin_amdgcn_rsqf(ftn2);
+      float sc = mud * fn * __builtin_amdgcn_rsqf(ftn2);
       ft0 *= sc;
       ft1 *= sc;
       float ik = frcp(P.fk);
@@ -162,10 +210,11 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   } else {
     ft0 = -P.fc * vw[0];
     ft1 = -P.fc * vw[1];
-    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = P.mud * fn;
+    float ftn2 = ft0 * ft0 + ft1 * ft1, cap = mud * fn;
     if (ftn2 > cap * cap) { float sc = cap * __builtin_amdgcn_rsqf(ftn2); ft0 *= sc; ft1 *= sc; }
   }
   float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
+  if constexpr (TERRAIN) { Fw[0] += fn * nrm[0]; Fw[1] += fn * nrm[1]; Fw[2] = fn * nrm[2]; }
   mtv(Rb, Fw, fl);
   cross(pl, fl, nl);
   f[0] += nl[0]; f[1] += nl[1]; f[2] += nl[2];
@@ -370,6 +419,7 @@ H12_DEV void link_pass3(const Leg& lg, const float (&cs)[NL][2], const float (&v
 
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
 // lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
+template <int K>
 H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr) {
   const float sg = leg ? -1.f : 1.f;
   float R0[3][3];
@@ -398,7 +448,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     mv(R, h12m::KNEE1, w1);
     const float* pl = (w0[2] <= w1[2]) ? h12m::KNEE0 : h12m::KNEE1;
     float dummy[2];
-    contact_sphere<false>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false);
+    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, P.mus, P.mud);
   }
   link_pass1<4>(lg, cs, v[3], v, R, p);
   link_pass1<5>(lg, cs, v[4], v, R, p);
@@ -413,7 +463,8 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
 #pragma unroll
     for (int q = 0; q < H12_NFOOT_PTS; ++q) {
       bool was = (lg.cmask >> q) & 1;
-      if (contact_sphere<true>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was))
+      if (contact_sphere<true, Feat<K>::terrain>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was, sg, lg.mus,
+                               lg.mud))
         nmask |= 1 << q;
     }
     lg.cmask = nmask;
@@ -450,6 +501,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   if (leg == 0) {
     AInertia Rg;
     ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
+    if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
     ai_add(IA, Rg);
     float hb[6];
     ai_mul(Rg, v0, hb);
@@ -463,7 +515,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dummy[2];
-    contact_sphere<false>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false);
+    contact_sphere<false, Feat<K>::terrain>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, P.mus, P.mud);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
   }
   // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
@@ -526,10 +578,13 @@ struct EnvSt {
   float air, con, last_air, last_con;  // this lane's foot
   float epsum[H12_NREW];
   int eplen, lag[3], since_reset, is_heading, is_standing;
+  float origin[3];                // env origin (terrain tasks)
+  int tcell;                      // terrain level | type << 16
 };
 
 // physics part of the state (loaded before the physics loop)
-H12_DEV void load_phys(const Workspace& W, int e, int leg, EnvSt& s) {
+template <int K>
+H12_DEV void load_phys(const KParams& P, const Workspace& W, int e, int leg, EnvSt& s) {
   const float sg = leg ? -1.f : 1.f;
   for (int i = 0; i < 3; ++i) s.b.pos[i] = ldf(W, H12_F_POS + i, e);
   for (int i = 0; i < 4; ++i) s.b.quat[i] = ldf(W, H12_F_QUAT + i, e);
@@ -557,10 +612,15 @@ H12_DEV void load_phys(const Workspace& W, int e, int leg, EnvSt& s) {
   s.since_reset = (pk >> 9) & 3;
   s.is_heading = (pk >> 11) & 1;
   s.is_standing = (pk >> 12) & 1;
+  const bool mu = Feat<K>::ext && P.env_mu;
+  s.lg.mus = mu ? ldf(W, H12_F_MU + 2 * leg, e) : P.mus;
+  s.lg.mud = mu ? ldf(W, H12_F_MU + 2 * leg + 1, e) : P.mud;
+  s.lg.dmass = (Feat<K>::ext && P.env_mass) ? ldf(W, H12_F_DMASS, e) : 0.f;
 }
 
 // MDP part of the state (loaded after the physics loop)
-H12_DEV void load_mdp(const Workspace& W, int e, int leg, EnvSt& s) {
+template <int K>
+H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvSt& s) {
   for (int i = 0; i < 3; ++i) s.cmd[i] = ldf(W, H12_F_CMD + i, e);
   s.heading = ldf(W, H12_F_HEADING, e);
   s.cmd_time = ldf(W, H12_F_CMD_TIME, e);
@@ -570,15 +630,28 @@ H12_DEV void load_mdp(const Workspace& W, int e, int leg, EnvSt& s) {
   s.last_con = ldf(W, H12_F_LAST_CONTACT + leg, e);
   for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
   s.eplen = W.I[(size_t)H12_I_EPLEN * W.n + e];
+  if (Feat<K>::terrain) {
+    for (int i = 0; i < 3; ++i) s.origin[i] = ldf(W, H12_F_ORIGIN + i, e);
+    s.tcell = W.I[(size_t)H12_I_TERRAIN * W.n + e];
+  } else {
+    s.origin[0] = s.origin[1] = s.origin[2] = 0.f;
+    s.tcell = 0;
+  }
 }
 
-H12_DEV void load_env(const Workspace& W, int e, int leg, EnvSt& s) {
-  load_phys(W, e, leg, s);
-  load_mdp(W, e, leg, s);
+template <int K>
+H12_DEV void load_env(const KParams& P, const Workspace& W, int e, int leg, EnvSt& s) {
+  load_phys<K>(P, W, e, leg, s);
+  load_mdp<K>(P, W, e, leg, s);
 }
 
-H12_DEV void store_env(const Workspace& W, int e, int leg, const EnvSt& s) {
+template <int K>
+H12_DEV void store_env(const KParams& P, const Workspace& W, int e, int leg, const EnvSt& s) {
   const float sg = leg ? -1.f : 1.f;
+  if (Feat<K>::terrain && leg == 0) {
+    for (int i = 0; i < 3; ++i) stf(W, H12_F_ORIGIN + i, e, s.origin[i]);
+    W.I[(size_t)H12_I_TERRAIN * W.n + e] = s.tcell;
+  }
   if (leg == 0) {
     for (int i = 0; i < 3; ++i) stf(W, H12_F_POS + i, e, s.b.pos[i]);
     for (int i = 0; i < 4; ++i) stf(W, H12_F_QUAT + i, e, s.b.quat[i]);
@@ -662,13 +735,34 @@ H12_DEV void cmd_update(const KParams& P, EnvSt& s) {
 }
 
 // _reset_idx: scene reset (delay lags, sensors), reset events, manager resets (cat_env.py:195-248)
+template <int K>
 H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi) {
   uint32_t r0[4], r1[4];
   rng(P, g, lo, hi, ST_RESET, 0, r0);
   rng(P, g, lo, hi, ST_RESET, 1, r1);
-  s.b.pos[0] = uab(r0[0], P.rx0, P.rx1);
-  s.b.pos[1] = uab(r0[1], P.ry0, P.ry1);
-  s.b.pos[2] = P.root_z;
+  if (Feat<K>::terrain && P.curriculum) {
+    // CurriculumManager.compute runs first in _reset_idx, on the pre-reset state:
+    // terrain_levels_vel (velocity/mdp/curriculums.py:21-52) + TerrainImporter.update_env_origins
+    float dx = s.b.pos[0] - s.origin[0], dy = s.b.pos[1] - s.origin[1];
+    float dist = fsqrt(dx * dx + dy * dy);
+    bool up = dist > 0.5f * P.terrain_size;
+    bool down = !up && dist < fsqrt(s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1]) * P.ep_len_s * 0.5f;
+    int lvl = (s.tcell & 0xFFFF) + (up ? 1 : 0) - (down ? 1 : 0);
+    const int typ = s.tcell >> 16;
+    if (lvl >= P.t_rows) {
+      uint32_t r2[4];
+      rng(P, g, lo, hi, ST_RESET, 2, r2);
+      lvl = (int)(r2[0] % (uint32_t)P.t_rows);
+    }
+    lvl = max(lvl, 0);
+    s.tcell = lvl | (typ << 16);
+    const float* o = P.t_origin + 3 * ((size_t)lvl * P.t_cols + typ);
+    s.origin[0] = o[0]; s.origin[1] = o[1]; s.origin[2] = o[2];
+  }
+  // reset_root_state_uniform: default root state + env origin + uniform pose offsets
+  s.b.pos[0] = s.origin[0] + uab(r0[0], P.rx0, P.rx1);
+  s.b.pos[1] = s.origin[1] + uab(r0[1], P.ry0, P.ry1);
+  s.b.pos[2] = s.origin[2] + P.root_z;
   float yaw = uab(r0[2], P.ryaw0, P.ryaw1);
   float sy, cy;
   sincosf(0.5f * yaw, &sy, &cy);
@@ -695,24 +789,53 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
   cmd_resample(P, s, g, lo, hi);
 }
 
+// root (composite COM) linear velocity in world: v_origin + w x (R c); c moves with the added torso mass
+template <int K>
+H12_DEV void base_com_vel(const KParams& P, const EnvSt& s, const float R[3][3], float* vcom) {
+  float c[3] = {h12m::BASE_COM[0], h12m::BASE_COM[1], h12m::BASE_COM[2]};
+  if (Feat<K>::ext && P.env_mass) {
+    float dm = s.lg.dmass, im = frcp(h12m::BASE_M + dm);
+    for (int a = 0; a < 3; ++a) c[a] = (h12m::BASE_MC[a] + dm * h12m::TORSO_COM[a]) * im;
+  }
+  float ww[3], cw[3], wxc[3];
+  mv(R, s.b.wang, ww);
+  mv(R, c, cw);
+  cross(ww, cw, wxc);
+  for (int a = 0; a < 3; ++a) vcom[a] = s.b.vlin[a] + wxc[a];
+}
+
 // this lane's part of the new (noise-free) observation frame, real coordinates, into the frame
-// scratch laid out [45][n] (coalesced across the wave).  Noise is added by obs_assemble_kernel.
+// scratch laid out [rows][n] (coalesced across the wave).  Noise / history / height scan are added by
+// the assembly kernels.  Flat: 45 rows (ang_vel, gravity, command, q-q0, qd, action).  Rough: base_lin_vel
+// first (48 rows), then base position (3) and yaw cos / sin (2) for the height scan.
+template <int K>
 H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, float* frame) {
   const float sg = leg ? -1.f : 1.f;
+  const int o = (Feat<K>::ext && P.task == H12_TASK_ROUGH) ? 3 : 0;
   if (leg == 0) {
     float R[3][3];
     quat_R(s.b.quat, R);
-    for (int a = 0; a < 3; ++a) frame[(size_t)a * n + e] = s.b.wang[a];
-    for (int a = 0; a < 3; ++a) frame[(size_t)(3 + a) * n + e] = -R[2][a];
-    for (int a = 0; a < 3; ++a) frame[(size_t)(6 + a) * n + e] = s.cmd[a];
+    if (o) {
+      float vcom[3], vb[3];
+      base_com_vel<K>(P, s, R, vcom);
+      mtv(R, vcom, vb);
+      for (int a = 0; a < 3; ++a) frame[(size_t)a * n + e] = vb[a];
+      for (int a = 0; a < 3; ++a) frame[(size_t)(H12_ROUGH_FRAME + a) * n + e] = s.b.pos[a];
+      float hx = R[0][0], hy = R[1][0], hn = __builtin_amdgcn_rsqf(hx * hx + hy * hy);
+      frame[(size_t)(H12_ROUGH_FRAME + 3) * n + e] = hx * hn;
+      frame[(size_t)(H12_ROUGH_FRAME + 4) * n + e] = hy * hn;
+    }
+    for (int a = 0; a < 3; ++a) frame[(size_t)(o + a) * n + e] = s.b.wang[a];
+    for (int a = 0; a < 3; ++a) frame[(size_t)(o + 3 + a) * n + e] = -R[2][a];
+    for (int a = 0; a < 3; ++a) frame[(size_t)(o + 6 + a) * n + e] = s.cmd[a];
   }
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
     int j = NL * leg + k;
-    frame[(size_t)(9 + j) * n + e] = js * (s.lg.q[k] - h12m::Q0[k]);
-    frame[(size_t)(21 + j) * n + e] = js * s.lg.qd[k];
-    frame[(size_t)(33 + j) * n + e] = js * s.act[k];
+    frame[(size_t)(o + 9 + j) * n + e] = js * (s.lg.q[k] - h12m::Q0[k]);
+    frame[(size_t)(o + 21 + j) * n + e] = js * s.lg.qd[k];
+    frame[(size_t)(o + 33 + j) * n + e] = js * s.act[k];
   }
 }
 
@@ -853,6 +976,49 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   }
 }
 
+// Rough task observation (no history): one thread per (env, element) of the 235-float row --
+// base_lin_vel, base_ang_vel, projected_gravity, velocity_commands, joint_pos_rel, joint_vel_rel,
+// last_action, height_scan (velocity_env_cfg.py:118-137; noise then clip, as ObservationManager does).
+// Height scan: RayCasterCfg at the torso_link origin (= pelvis origin), attach_yaw_only, grid pattern
+// 1.6 x 1.0 m at 0.1 m (17 x 11 rays, x fastest: meshgrid 'xy' order), rays straight down onto the
+// heightfield; value = sensor z - hit z - 0.5 (isaaclab mdp.height_scan).
+H12_DEV float rough_noise(const KParams& P, const AsmArgs& A, int e, int t) {
+  uint32_t r[4];
+  philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + e), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)(t >> 2), A.hi, r);
+  uint32_t rv = (t & 3) == 0 ? r[0] : ((t & 3) == 1 ? r[1] : ((t & 3) == 2 ? r[2] : r[3]));
+  float nmax = t < 3 ? P.n_lin : (t < 6 ? P.n_w : (t < 9 ? P.n_g : (t < 21 ? P.n_q : (t < 33 ? P.n_qd : P.n_scan))));
+  return P.corrupt ? (-nmax + 2.f * nmax * u01(rv)) : 0.f;
+}
+
+__global__ void __launch_bounds__(ASM_BLOCK) rough_obs_kernel(KParams P, AsmArgs A) {
+  const int n = A.n;
+  const int gid = blockIdx.x * ASM_BLOCK + threadIdx.x;
+  if (gid >= n * H12_NOBS_ROUGH) return;
+  const int e = gid / H12_NOBS_ROUGH;
+  const int k = gid - e * H12_NOBS_ROUGH;
+  if (A.reset_mode && A.sel && !A.sel[e]) return;
+  float v;
+  if (k < H12_ROUGH_FRAME) {
+    v = A.frame[(size_t)k * n + e];
+    int t = k < 9 ? k : ((k >= 12 && k < 36) ? k - 3 : -1);
+    if (t >= 0) v += rough_noise(P, A, e, t);
+  } else {
+    const int r = k - H12_ROUGH_FRAME, iy = r / H12_SCAN_NX, ix = r - iy * H12_SCAN_NX;
+    const float xl = P.scan_res * (float)(ix - (H12_SCAN_NX - 1) / 2), yl = P.scan_res * (float)(iy - (H12_SCAN_NY - 1) / 2);
+    const float px = A.frame[(size_t)H12_ROUGH_FRAME * n + e], py = A.frame[(size_t)(H12_ROUGH_FRAME + 1) * n + e];
+    const float pz = A.frame[(size_t)(H12_ROUGH_FRAME + 2) * n + e];
+    const float cy = A.frame[(size_t)(H12_ROUGH_FRAME + 3) * n + e], sy = A.frame[(size_t)(H12_ROUGH_FRAME + 4) * n + e];
+    float hz = 0.f;
+    if (P.terrain) {
+      float gx, gy;
+      hz = ground(P, px + cy * xl - sy * yl, py + sy * xl + cy * yl, gx, gy);
+    }
+    v = pz - hz - P.scan_off + rough_noise(P, A, e, k - 15);
+    v = fminf(fmaxf(v, -P.scan_clip), P.scan_clip);
+  }
+  A.obs[(size_t)e * H12_NOBS_ROUGH + k] = v;
+}
+
 // ------------------------------------------------------------------ kernels
 struct StepArgs {
   const float* actions;
@@ -872,6 +1038,7 @@ struct StepArgs {
   int n_substeps;
 };
 
+template <int K>
 __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
@@ -883,7 +1050,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   PH_INIT();
   if (active) {
     EnvSt s;
-    load_phys(W, e, leg, s);
+    load_phys<K>(P, W, e, leg, s);
     PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
@@ -923,7 +1090,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
-      for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr);
+      for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr);
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
       // ContactSensor: net force = mean over the inner steps of the physics step
@@ -937,7 +1104,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       }
     }
     PH(1);
-    load_mdp(W, e, leg, s);
+    load_mdp<K>(P, W, e, leg, s);
     // ContactSensor._update_buffers_impl replayed per physics step (threshold 1 N, elapsed = dt)
     for (int st = 0; st < dec; ++st) {
       bool is_c = (cflags >> st) & 1u;
@@ -959,10 +1126,8 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     quat_R(s.b.quat, R);
     float ww[3];
     mv(R, s.b.wang, ww);
-    float cw[3], wxc[3];
-    mv(R, h12m::BASE_COM, cw);
-    cross(ww, cw, wxc);
-    float vcom[3] = {s.b.vlin[0] + wxc[0], s.b.vlin[1] + wxc[1], s.b.vlin[2] + wxc[2]};
+    float vcom[3];
+    base_com_vel<K>(P, s, R, vcom);
     // yaw frame: heading direction of the body x axis in the world xy-plane
     float hx = R[0][0], hy = R[1][0];
     float hn = __builtin_amdgcn_rsqf(hx * hx + hy * hy);
@@ -1061,7 +1226,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       if (term) atomicAdd(&A.log_acc[14], 1.f);
     }
     PH(4);
-    if (reset) env_reset(P, s, leg, g, A.lo, A.hi);
+    if (reset) env_reset<K>(P, s, leg, g, A.lo, A.hi);
     else s.since_reset = min(s.since_reset + 1, 2);
     // ---- CommandTerm.compute(step_dt)
     s.cmd_time -= P.step_dt;
@@ -1069,13 +1234,14 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     cmd_update(P, s);
     // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
     PH(5);
-    obs_frame(P, s, leg, e, W.n, A.frame);
+    obs_frame<K>(P, s, leg, e, W.n, A.frame);
     PH(6);
-    store_env(W, e, leg, s);
+    store_env<K>(P, W, e, leg, s);
     PH(7);
   }
 }
 
+template <int K>
 __global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
@@ -1085,15 +1251,16 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, St
   if (sel) {
     const uint32_t g = (uint32_t)(A.env_offset + e);
     EnvSt s;
-    load_env(W, e, leg, s);
-    env_reset(P, s, leg, g, A.lo, A.hi);
-    obs_frame(P, s, leg, e, W.n, A.frame);
-    store_env(W, e, leg, s);
+    load_env<K>(P, W, e, leg, s);
+    env_reset<K>(P, s, leg, g, A.lo, A.hi);
+    obs_frame<K>(P, s, leg, e, W.n, A.frame);
+    store_env<K>(P, W, e, leg, s);
   }
 }
 
 // ObservationManager.compute() outside step(): new frame from the current state, history shifted
 // (or filled where fill_mask[e]); RNG counter domain (observe call, 0xFFFFFFFE)
+template <int K>
 __global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
@@ -1101,12 +1268,13 @@ __global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, 
   const int e = e0 + lane_pair;
   if (e < W.n) {
     EnvSt s;
-    load_env(W, e, leg, s);
-    obs_frame(P, s, leg, e, W.n, A.frame);
+    load_env<K>(P, W, e, leg, s);
+    obs_frame<K>(P, s, leg, e, W.n, A.frame);
   }
 }
 
 // parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
+template <int K>
 __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
@@ -1114,7 +1282,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
   const int e = blockIdx.x * ENVS_PER_BLOCK + lane_pair;
   if (e >= W.n) return;
   EnvSt s;
-  load_env(W, e, leg, s);
+  load_env<K>(P, W, e, leg, s);
   float qr[NL];
   for (int k = 0; k < NL; ++k) qr[k] = jsign(k, sg) * A.q_ref[(size_t)e * NJ + NL * leg + k];
   for (int st = 0; st < A.n_substeps; ++st) {
@@ -1124,9 +1292,9 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step(P, leg, s.b, s.lg, tau, P.h, fr);
+    for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr);
   }
-  store_env(W, e, leg, s);
+  store_env<K>(P, W, e, leg, s);
 }
 
 // ------------------------------------------------------------------ host side
@@ -1181,7 +1349,8 @@ int check_model(const h12env_model* m) {
     }
   if (!close(m->base_mass, h12m::BASE_M) || !close(m->base_com[0], h12m::BASE_COM[0]) ||
       !close(m->base_com[2], h12m::BASE_COM[2]) || !close(m->foot_radius, h12m::FOOT_R) ||
-      !close(m->knee_radius, h12m::KNEE_R))
+      !close(m->knee_radius, h12m::KNEE_R) || !close(m->torso_com[0], h12m::TORSO_COM[0]) ||
+      !close(m->torso_com[1], h12m::TORSO_COM[1]) || !close(m->torso_com[2], h12m::TORSO_COM[2]))
     return set_err(H12_E_ARG, "base / contact geometry differs from the compiled H1-2 model");
   return 0;
 }
@@ -1244,10 +1413,39 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.air_thr = c->air_time_threshold;
   P.seed_lo = (uint32_t)c->seed;
   P.seed_hi = (uint32_t)(c->seed >> 32);
+  if (c->task != H12_TASK_FLAT && c->task != H12_TASK_ROUGH) return set_err(H12_E_ARG, "bad task %d", c->task);
+  if (c->terrain_curriculum && !c->terrain) return set_err(H12_E_ARG, "terrain_curriculum needs terrain = 1");
+  if (c->task == H12_TASK_ROUGH && !(c->scan_resolution > 0)) return set_err(H12_E_ARG, "scan_resolution must be > 0");
+  P.task = c->task;
+  P.terrain = c->terrain;
+  P.curriculum = c->terrain_curriculum;
+  P.env_mu = c->per_env_friction;
+  P.env_mass = c->per_env_mass;
+  P.n_lin = c->noise_lin_vel;
+  P.n_scan = c->noise_height_scan;
+  P.scan_off = c->scan_offset;
+  P.scan_clip = c->scan_clip;
+  P.scan_res = c->scan_resolution;
+  P.terrain_size = c->terrain_size;
+  P.ep_len_s = (float)c->max_episode_length * P.step_dt;
   return 0;
 }
 
 int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
+
+// feature level of the env kernels (Feat<K>)
+int feature_level(const KParams& P) {
+  if (P.terrain) return 2;
+  return (P.task != H12_TASK_FLAT || P.env_mu || P.env_mass || P.curriculum) ? 1 : 0;
+}
+#define LAUNCH_K(KERNEL, ...)                                                   \
+  do {                                                                          \
+    switch (feature_level(h->P)) {                                              \
+      case 0: hipLaunchKernelGGL(KERNEL<0>, __VA_ARGS__); break;                \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                \
+      default: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;               \
+    }                                                                           \
+  } while (0)
 
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
@@ -1264,6 +1462,12 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.env_offset = h->env_offset;
   A.lo = lo;
   A.hi = hi;
+  if (h->P.task == H12_TASK_ROUGH) {
+    const int nb = (int)(((size_t)h->W.n * H12_NOBS_ROUGH + ASM_BLOCK - 1) / ASM_BLOCK);
+    hipLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   const float* src = reset_mode ? obs : obs_prev;
   A.vec = (((uintptr_t)obs | (uintptr_t)src) & 15u) == 0;
   const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
@@ -1323,6 +1527,29 @@ int h12env_config_default(h12env_config* c) {
   c->track_std = 0.5f; c->air_time_threshold = 0.4f; c->soft_limit_factor = 0.9f;
   c->illegal_contact_knees = 1; c->illegal_contact_torso = 1;
   c->seed = 42;
+  c->task = H12_TASK_FLAT;
+  c->noise_lin_vel = 0.1f; c->noise_height_scan = 0.1f;
+  c->scan_offset = 0.5f; c->scan_clip = 1.f; c->scan_resolution = 0.1f; c->terrain_size = 8.f;
+  return 0;
+}
+
+int h12env_set_terrain(h12env* hh, const float* heights, int nx, int ny, float hscale, float x0, float y0,
+                       const float* origins, int rows, int cols) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!heights || nx < 2 || ny < 2 || !(hscale > 0)) return set_err(H12_E_ARG, "heights (nx, ny >= 2, hscale > 0) required");
+  if ((origins == nullptr) != (rows <= 0 || cols <= 0) || rows > 0xFFFF || cols > 0x7FFF)
+    return set_err(H12_E_ARG, "origins need rows, cols in 1..32767");
+  if (h->P.curriculum && !origins) return set_err(H12_E_ARG, "the terrain curriculum needs the origins table");
+  h->P.t_h = heights;
+  h->P.t_nx = nx;
+  h->P.t_ny = ny;
+  h->P.t_inv_hs = 1.f / hscale;
+  h->P.t_x0 = x0;
+  h->P.t_y0 = y0;
+  h->P.t_origin = origins;
+  h->P.t_rows = rows;
+  h->P.t_cols = cols;
   return 0;
 }
 
@@ -1356,7 +1583,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->W.F = (float*)state_dev;
   h->W.I = (int32_t*)((float*)state_dev + (size_t)H12_NF_FLOAT * n_envs);
   h->W.n = n_envs;
-  e = hipMalloc(&h->frame, sizeof(float) * H12_OBS_FRAME * (size_t)n_envs);
+  e = hipMalloc(&h->frame, sizeof(float) * FRAME_ROWS * (size_t)n_envs);
   if (e != hipSuccess) {
     if (h->own) (void)hipFree(state_dev);
     delete h;
@@ -1387,6 +1614,7 @@ int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
   if (!obs) return set_err(H12_E_ARG, "obs is required");
+  if (h->P.terrain && !h->P.t_h) return set_err(H12_E_STATE, "terrain = 1 but h12env_set_terrain was not called");
   StepArgs A = {};
   A.obs = obs;
   A.reset_mask = mask;
@@ -1395,7 +1623,7 @@ int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
   A.hi = 0xFFFFFFFFu;
   A.frame = h->frame;
   h->reset_calls++;
-  hipLaunchKernelGGL(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  LAUNCH_K(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return launch_assemble(h, nullptr, obs, nullptr, nullptr, mask, 1, A.lo, A.hi, (hipStream_t)stream);
 }
@@ -1404,8 +1632,10 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
                 int64_t step_index, void* stream) {
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
-  if (!actions || !obs_prev || !out || !out->obs || !out->rew || !out->terminated || !out->truncated)
-    return set_err(H12_E_ARG, "actions, obs_prev, obs, rew, terminated, truncated are required");
+  if (!actions || !out || !out->obs || !out->rew || !out->terminated || !out->truncated)
+    return set_err(H12_E_ARG, "actions, obs, rew, terminated, truncated are required");
+  if (!obs_prev && h->P.task == H12_TASK_FLAT) return set_err(H12_E_ARG, "obs_prev is required (history source)");
+  if (h->P.terrain && !h->P.t_h) return set_err(H12_E_STATE, "terrain = 1 but h12env_set_terrain was not called");
   if (step_index < 1) return set_err(H12_E_ARG, "step_index must be >= 1 (got %lld)", (long long)step_index);
   StepArgs A = {};
   A.actions = actions;
@@ -1422,7 +1652,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   A.frame = h->frame;
   timing_mark(h, 0, (hipStream_t)stream);
-  hipLaunchKernelGGL(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  LAUNCH_K(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   timing_mark(h, 1, (hipStream_t)stream);
   // fill = terminated | truncated: the envs reset inside the step restart their history
@@ -1435,7 +1665,8 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
-  if (!obs_prev || !obs) return set_err(H12_E_ARG, "obs_prev and obs are required");
+  if (!obs || (!obs_prev && h->P.task == H12_TASK_FLAT)) return set_err(H12_E_ARG, "obs_prev and obs are required");
+  if (h->P.terrain && !h->P.t_h) return set_err(H12_E_STATE, "terrain = 1 but h12env_set_terrain was not called");
   StepArgs A = {};
   A.obs_prev = obs_prev;
   A.obs = obs;
@@ -1445,7 +1676,7 @@ int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t*
   A.hi = 0xFFFFFFFEu;
   h->observe_calls++;
   A.frame = h->frame;
-  hipLaunchKernelGGL(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  LAUNCH_K(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return launch_assemble(h, obs_prev, obs, fill_mask, nullptr, nullptr, 0, A.lo, A.hi, (hipStream_t)stream);
 }
@@ -1457,7 +1688,7 @@ int h12env_step_physics(h12env* hh, const float* q_ref, int n_substeps, void* st
   StepArgs A = {};
   A.q_ref = q_ref;
   A.n_substeps = n_substeps;
-  hipLaunchKernelGGL(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  LAUNCH_K(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -1490,17 +1721,26 @@ int h12env_num_envs(const h12env* hh) { return hh ? ((const Handle*)hh)->W.n : -
 int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, double* flops_per_env) {
   const Handle* h = (const Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
+  const KParams& P = h->P;
+  const bool rough = P.task == H12_TASK_ROUGH;
   double bytes, flops;
   if (kernel == 0) {
-    // state read + write, actions, reward / terminated / truncated, applied torque and foot force
-    // (the ArticulationData / ContactSensor views), the noise-free frame
-    bytes = (double)(H12_NF_FLOAT + H12_NF_INT) * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 +
-            (double)H12_NJ * 4.0 + 2.0 * 4.0 + (double)H12_OBS_FRAME * 4.0;
+    // state fields the kernel reads and writes, actions, reward / terminated / truncated, applied torque
+    // and foot force (the ArticulationData / ContactSensor views), the noise-free frame
+    double fields = 104.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0);
+    bytes = fields * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 + (double)H12_NJ * 4.0 + 2.0 * 4.0 +
+            (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
     flops = h->flops_per_env;
   } else if (kernel == 1) {
-    // 9 old frames + the new frame + the two reset flags read, 10 frames written
-    bytes = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_OBS_FRAME * 4.0 + 2.0 + (double)H12_NOBS * 4.0;
-    flops = 30.0 * 3.0 + 8.0 * 10.0 * 6.0;  // noise affine + Philox rounds
+    if (rough) {
+      // frame read, one height sample per ray, the 235-float row written
+      bytes = (double)FRAME_ROWS * 4.0 + (double)H12_NSCAN * 4.0 + (double)H12_NOBS_ROUGH * 4.0;
+      flops = 55.0 * 10.0 * 6.0 + (double)H12_NSCAN * 20.0;
+    } else {
+      // 9 old frames + the new frame + the two reset flags read, 10 frames written
+      bytes = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_OBS_FRAME * 4.0 + 2.0 + (double)H12_NOBS * 4.0;
+      flops = 30.0 * 3.0 + 8.0 * 10.0 * 6.0;  // noise affine + Philox rounds
+    }
   } else {
     return set_err(H12_E_ARG, "kernel must be 0 or 1 (got %d)", kernel);
   }
@@ -1514,7 +1754,8 @@ int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_
   if (int rc = h12env_kernel_cost(hh, 0, &b0, &f0)) return rc;
   if (int rc = h12env_kernel_cost(hh, 1, &b1, &f1)) return rc;
   // the frame round trip between the kernels is not compulsory traffic of the step
-  if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * (double)H12_OBS_FRAME * 4.0;
+  const double fr = (((const Handle*)hh)->P.task == H12_TASK_ROUGH ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
+  if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * fr;
   if (flops_per_env) *flops_per_env = f0 + f1;
   return 0;
 }

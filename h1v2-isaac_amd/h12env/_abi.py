@@ -16,18 +16,25 @@ NOBS = OBS_FRAME * NHIST
 NFOOT_PTS = 4
 NREW = 12
 NLOG = 16
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
+TASK_FLAT = 0
+TASK_ROUGH = 1
+ROUGH_FRAME = 48
+SCAN_NX, SCAN_NY = 17, 11
+NSCAN = SCAN_NX * SCAN_NY
+NOBS_ROUGH = ROUGH_FRAME + NSCAN
 
 # state field offsets (H12_F_* / H12_I_*)
 F = dict(POS=(0, 3), QUAT=(3, 4), VLIN=(7, 3), WANG=(10, 3), Q=(13, 12), QD=(25, 12), ACT=(37, 12),
          ACT_PREV=(49, 12), CMD=(61, 3), HEADING=(64, 1), CMD_TIME=(65, 1), AIR=(66, 2), CONTACT=(68, 2),
-         LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16))
-NF_FLOAT = 102
-I = dict(EPLEN=(0, 1), PACK=(1, 1))
-NF_INT = 2
+         LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16), ORIGIN=(102, 3), MU=(105, 4),
+         DMASS=(109, 1))
+NF_FLOAT = 110
+I = dict(EPLEN=(0, 1), PACK=(1, 1), TERRAIN=(2, 1))
+NF_INT = 3
 
 REWARD_TERMS = [
     "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "ang_vel_xy_l2", "dof_torques_l2", "dof_acc_l2",
@@ -67,6 +74,7 @@ class H12Model(C.Structure):
         ("torso_center", f32 * 3),
         ("torso_half", f32 * 3),
         ("gravity", f32),
+        ("torso_com", f32 * 3),
     ]
 
 
@@ -119,6 +127,17 @@ class H12Config(C.Structure):
         ("illegal_contact_knees", i32),
         ("illegal_contact_torso", i32),
         ("seed", C.c_uint64),
+        ("task", i32),
+        ("terrain", i32),
+        ("terrain_curriculum", i32),
+        ("per_env_friction", i32),
+        ("per_env_mass", i32),
+        ("noise_lin_vel", f32),
+        ("noise_height_scan", f32),
+        ("scan_offset", f32),
+        ("scan_clip", f32),
+        ("scan_resolution", f32),
+        ("terrain_size", f32),
     ]
 
 
@@ -176,6 +195,8 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_step.restype = C.c_int
     lib.h12env_observe.argtypes = [vp, vp, vp, vp, vp]
     lib.h12env_observe.restype = C.c_int
+    lib.h12env_set_terrain.argtypes = [vp, vp, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, vp, C.c_int, C.c_int]
+    lib.h12env_set_terrain.restype = C.c_int
     lib.h12env_step_physics.argtypes = [vp, vp, C.c_int, vp]
     lib.h12env_step_physics.restype = C.c_int
     lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
@@ -216,5 +237,5 @@ EXPORTED_SYMBOLS = [
     "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
-    "h12env_set_kernel_timing", "h12env_kernel_times",
+    "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain",
 ]

@@ -19,7 +19,7 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass, field, replace
 
-from ._abi import ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NJ, NREW, REWARD_TERMS, H12Config
+from ._abi import ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NJ, NREW, REWARD_TERMS, TASK_FLAT, TASK_ROUGH, H12Config
 from .model import DEFAULT_JOINT_POS
 
 
@@ -41,10 +41,48 @@ class SimCfg:
 
 
 @dataclass
+class TerrainGeneratorCfg:
+    """ROUGH_TERRAINS_CFG (biped_tasks/utils/mdp/terrains.py:11-28): one HfRandomUniform sub-terrain type."""
+    size: tuple = (8.0, 8.0)
+    border_width: float = 20.0
+    num_rows: int = 10
+    num_cols: int = 20
+    horizontal_scale: float = 0.1
+    vertical_scale: float = 0.005
+    slope_threshold: float = 0.75
+    curriculum: bool = True
+    # HfRandomUniformTerrainCfg
+    noise_range: tuple = (0.0, 0.02)
+    noise_step: float = 0.005
+    sub_border_width: float = 0.25
+
+
+@dataclass
+class TerrainCfg:
+    """TerrainImporterCfg (velocity_env_cfg.py:40-56)."""
+    terrain_type: str = "plane"            # "plane" | "generator"
+    terrain_generator: TerrainGeneratorCfg | None = None
+    max_init_terrain_level: int | None = 5
+    static_friction: float = 1.0           # ground material, multiply-combined
+    dynamic_friction: float = 1.0
+
+
+@dataclass
+class HeightScannerCfg:
+    """RayCasterCfg at torso_link, offset z 20, yaw only, GridPatternCfg(0.1, (1.6, 1.0)) (velocity_env_cfg.py:58-66)."""
+    prim_path: str = "{ENV_REGEX_NS}/Robot/torso_link"
+    resolution: float = 0.1
+    size: tuple = (1.6, 1.0)
+    attach_yaw_only: bool = True
+
+
+@dataclass
 class SceneCfg:
     num_envs: int = 4096
     env_spacing: float = 2.5
     lazy_sensor_update: bool = True
+    terrain: TerrainCfg = field(default_factory=TerrainCfg)
+    height_scanner: HeightScannerCfg | None = None
 
 
 @dataclass
@@ -120,13 +158,17 @@ class PolicyObsCfg:
     enable_corruption: bool = True
     concatenate_terms: bool = True
     history_length: int = 10
-    # term order preserved (velocity_env_cfg.py:124-132; base_lin_vel and height_scan removed for Flat)
+    # term order preserved (velocity_env_cfg.py:118-137; base_lin_vel and height_scan removed for Flat)
+    base_lin_vel: Unoise | None = None
     base_ang_vel: Unoise = field(default_factory=lambda: Unoise(-0.2, 0.2))
     projected_gravity: Unoise = field(default_factory=lambda: Unoise(-0.05, 0.05))
     velocity_commands: None = None
     joint_pos: Unoise = field(default_factory=lambda: Unoise(-0.01, 0.01))
     joint_vel: Unoise = field(default_factory=lambda: Unoise(-1.5, 1.5))
     actions: None = None
+    height_scan: Unoise | None = None
+    height_scan_clip: tuple = (-1.0, 1.0)
+    height_scan_offset: float = 0.5
 
 
 @dataclass
@@ -164,10 +206,18 @@ class RewardsCfg:
         object.__setattr__(self, "_terms", terms or _rewards())
 
     def __getattr__(self, name):
+        if name.startswith("__") or name == "_terms":
+            raise AttributeError(name)
         try:
             return self._terms[name]
         except KeyError as e:
             raise AttributeError(name) from e
+
+    def __getstate__(self):
+        return {"_terms": self._terms}
+
+    def __setstate__(self, st):
+        object.__setattr__(self, "_terms", st["_terms"])
 
     def __setattr__(self, name, value):
         if name not in self._terms:
@@ -195,7 +245,29 @@ class EventsCfg:
     reset_base_pose_range: dict = field(default_factory=lambda: {"x": (-0.5, 0.5), "y": (-0.5, 0.5), "yaw": (-3.14, 3.14)})
     reset_joints_position_range: tuple = (1.0, 1.0)
     push_robot: None = None
-    add_base_mass: None = None
+    # startup randomisation (randomize_rigid_body_material / _mass, velocity_env_cfg.py:146-166,
+    # cat_env_cfg.py:231-249); None = the constant material of the Flat task / no added mass
+    physics_material: "MaterialEventCfg | None" = None
+    add_base_mass: "MassEventCfg | None" = None
+
+
+@dataclass
+class MaterialEventCfg:
+    static_friction_range: tuple = (0.8, 0.8)
+    dynamic_friction_range: tuple = (0.6, 0.6)
+    num_buckets: int = 64
+
+
+@dataclass
+class MassEventCfg:
+    body_names: str = ".*torso_link"
+    mass_distribution_params: tuple = (0.0, 6.0)
+    operation: str = "add"
+
+
+@dataclass
+class CurriculumCfg:
+    terrain_levels: bool = False  # terrain_levels_vel (velocity_env_cfg.py:271-275)
 
 
 @dataclass
@@ -215,7 +287,13 @@ class H12FlatEnvCfg:
     rewards: RewardsCfg = field(default_factory=RewardsCfg)
     terminations: TerminationsCfg = field(default_factory=TerminationsCfg)
     events: EventsCfg = field(default_factory=EventsCfg)
+    curriculum: CurriculumCfg = field(default_factory=CurriculumCfg)
     fix_base: bool = False
+
+    @property
+    def task(self) -> int:
+        """Rough layout (235-float obs with height scan) when the scene has a height scanner."""
+        return TASK_ROUGH if self.scene.height_scanner is not None else TASK_FLAT
 
     @property
     def step_dt(self) -> float:
@@ -284,8 +362,32 @@ class H12FlatEnvCfg:
         c.reset_y[:] = pr["y"]
         c.reset_yaw[:] = pr["yaw"]
         po = self.observations.policy
-        if po.history_length != 10:
-            raise ValueError("the kernel's observation history is fixed at 10 frames")
+        c.task = self.task
+        if c.task == TASK_FLAT and po.history_length != 10:
+            raise ValueError("the flat kernel's observation history is fixed at 10 frames")
+        if c.task == TASK_ROUGH:
+            if po.history_length not in (0, 1, None):
+                raise ValueError("the rough observation has no history (history_length 0)")
+            if po.base_lin_vel is None or po.height_scan is None:
+                raise ValueError("the rough layout needs base_lin_vel and height_scan terms")
+            c.noise_lin_vel = po.base_lin_vel.n_max
+            c.noise_height_scan = po.height_scan.n_max
+            c.scan_offset = po.height_scan_offset
+            c.scan_clip = po.height_scan_clip[1]
+            hs = self.scene.height_scanner
+            if tuple(hs.size) != (1.6, 1.0) or abs(hs.resolution - 0.1) > 1e-9:
+                raise ValueError("the kernel's height scan grid is 17 x 11 rays at 0.1 m")
+            c.scan_resolution = hs.resolution
+        else:
+            if po.base_lin_vel is not None or po.height_scan is not None:
+                raise ValueError("base_lin_vel / height_scan need the rough layout (scene.height_scanner)")
+            c.noise_lin_vel, c.noise_height_scan, c.scan_offset, c.scan_clip, c.scan_resolution = 0.1, 0.1, 0.5, 1.0, 0.1
+        t = self.scene.terrain
+        c.terrain = 1 if t.terrain_type == "generator" else 0
+        c.terrain_curriculum = int(bool(self.curriculum.terrain_levels) and c.terrain == 1)
+        c.terrain_size = t.terrain_generator.size[0] if t.terrain_generator is not None else 8.0
+        c.per_env_friction = int(self.events.physics_material is not None)
+        c.per_env_mass = int(self.events.add_base_mass is not None)
         c.enable_corruption = int(po.enable_corruption)
         c.noise_ang_vel = po.base_ang_vel.n_max
         c.noise_gravity = po.projected_gravity.n_max
@@ -301,6 +403,60 @@ class H12FlatEnvCfg:
         c.seed = (self.seed if self.seed is not None else 0) & 0xFFFFFFFFFFFFFFFF
         assert len(REWARD_TERMS) == NREW and NJ == 12
         return c
+
+
+@dataclass
+class H12RoughEnvCfg(H12FlatEnvCfg):
+    """Isaac-Velocity-Rough-H12_12dof-v0 (H12_12dof_RoughEnvCfg, rough_env_cfg.py:128-188 on
+    LocomotionVelocityRoughEnvCfg): generated heightfield + terrain curriculum, height scanner, base_lin_vel
+    in the 235-float observation (no history), rough reward weights, lin_vel_y command 0."""
+
+    def __post_init__(self):
+        self.scene.terrain = TerrainCfg(terrain_type="generator", terrain_generator=TerrainGeneratorCfg(),
+                                        max_init_terrain_level=5)
+        self.scene.height_scanner = HeightScannerCfg()
+        po = self.observations.policy
+        po.history_length = 0
+        po.base_lin_vel = Unoise(-0.1, 0.1)
+        po.height_scan = Unoise(-0.1, 0.1)
+        self.curriculum.terrain_levels = True
+        r = self.rewards
+        r.feet_air_time.weight = 0.25              # rough_env_cfg.py:97-105
+        r.dof_torques_l2.weight = -1.5e-7          # :177
+        r.dof_acc_l2.weight = -1.25e-7             # :179
+        r.action_rate_l2.weight = -0.005           # :178
+        r.flat_orientation_l2.weight = -1.0        # :176
+        self.commands.base_velocity.ranges.lin_vel_x = (0.0, 1.0)   # :186-188
+        self.commands.base_velocity.ranges.lin_vel_y = (0.0, 0.0)
+        self.commands.base_velocity.ranges.ang_vel_z = (-1.0, 1.0)
+
+
+@dataclass
+class H12RoughEnvCfg_PLAY(H12RoughEnvCfg):
+    """rough_env_cfg.py:191-214: 50 envs, 40 s episodes, random initial levels, 5 x 5 terrain, no noise."""
+
+    def __post_init__(self):
+        super().__post_init__()
+        self.scene.num_envs = 50
+        self.episode_length_s = 40.0
+        self.scene.terrain.max_init_terrain_level = None
+        g = self.scene.terrain.terrain_generator
+        g.num_rows, g.num_cols, g.curriculum = 5, 5, False
+        self.commands.base_velocity.ranges.lin_vel_x = (1.0, 1.0)
+        self.commands.base_velocity.ranges.lin_vel_y = (0.0, 0.0)
+        self.commands.base_velocity.ranges.ang_vel_z = (-1.0, 1.0)
+        self.commands.base_velocity.ranges.heading = (0.0, 0.0)
+        self.observations.policy.enable_corruption = False
+
+
+def c5_cfg(num_envs: int = 8192) -> H12RoughEnvCfg:
+    """BASELINE config C5: the rough task with CaT's startup randomisation (cat_env_cfg.py:231-249):
+    sole friction U(0.1, 1.25) in 64 buckets, torso mass + U(0, 6) kg, 8192 envs."""
+    c = H12RoughEnvCfg()
+    c.scene.num_envs = num_envs
+    c.events.physics_material = MaterialEventCfg((0.1, 1.25), (0.1, 1.25), 64)
+    c.events.add_base_mass = MassEventCfg(".*torso_link", (0.0, 6.0), "add")
+    return c
 
 
 def mujoco_cfg(**kw) -> H12FlatEnvCfg:

@@ -23,7 +23,7 @@ import torch
 
 from . import _abi
 from ._abi import F as FIELDS
-from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, REWARD_TERMS, H12StepOut, check, load_library
+from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, NOBS_ROUGH, REWARD_TERMS, TASK_ROUGH, H12StepOut, check, load_library
 from .cfg import H12FlatEnvCfg
 from .model import body_names, build_model, joint_names
 
@@ -46,12 +46,13 @@ class _LazyLog(dict):
     """extras["log"]: IsaacLab's Episode_Reward/* and Episode_Termination/* values, materialised on
     first access from the step's device-side accumulator (no host sync inside step())."""
 
-    def __init__(self, acc: torch.Tensor, max_episode_length_s: float):
+    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, extra: dict | None = None):
         super().__init__()
         self._acc = acc
         self._T = max_episode_length_s
+        self._extra = extra or {}
         self._keys = [f"Episode_Reward/{t}" for t in REWARD_TERMS] + [
-            "Episode_Termination/time_out", "Episode_Termination/base_contact"]
+            "Episode_Termination/time_out", "Episode_Termination/base_contact"] + list(self._extra)
         self._done = False
 
     def _fill(self):
@@ -60,8 +61,10 @@ class _LazyLog(dict):
         a = self._acc
         n = a[12].clamp(min=1.0)
         vals = torch.cat([a[:12] / n / self._T, a[13:15]])
-        for i, k in enumerate(self._keys):
+        for i, k in enumerate(self._keys[:14]):
             dict.__setitem__(self, k, vals[i])
+        for k, f in self._extra.items():
+            dict.__setitem__(self, k, f())
         self._done = True
 
     def __getitem__(self, k):
@@ -94,10 +97,12 @@ class _LazyLog(dict):
 class _ObservationManager:
     def __init__(self, env):
         self._env = env
-        self.group_obs_dim = {"policy": (NOBS,)}
+        self.group_obs_dim = {"policy": (env.obs_dim,)}
         self.group_obs_concatenate = {"policy": True}
-        self.active_terms = {"policy": ["base_ang_vel", "projected_gravity", "velocity_commands", "joint_pos",
-                                        "joint_vel", "actions"]}
+        terms = ["base_ang_vel", "projected_gravity", "velocity_commands", "joint_pos", "joint_vel", "actions"]
+        if env.obs_dim == NOBS_ROUGH:
+            terms = ["base_lin_vel"] + terms + ["height_scan"]
+        self.active_terms = {"policy": terms}
 
     def compute(self):
         return {"policy": self._env._obs[self._env._k]}
@@ -146,7 +151,9 @@ class _ArticulationData:
 
     @property
     def root_pos_w(self):
-        return self._env._field("POS").T + self._env.scene.env_origins
+        e = self._env
+        # terrain tasks keep world positions in the workspace; the plane keeps env-local ones
+        return e._field("POS").T if e.terrain is not None else e._field("POS").T + e.scene.env_origins
 
     @property
     def root_quat_w(self):
@@ -191,7 +198,8 @@ class H12VelocityEnv:
         self._fstate = self._state.view(torch.float32)[: NF_FLOAT * self.num_envs].view(NF_FLOAT, self.num_envs)
         self._istate = self._state.view(torch.int32)[NF_FLOAT * self.num_envs:].view(NF_INT, self.num_envs)
         n = self.num_envs
-        self._obs = [torch.zeros(n, NOBS, device=self.device), torch.zeros(n, NOBS, device=self.device)]
+        self.obs_dim = NOBS_ROUGH if self._ccfg.task == TASK_ROUGH else NOBS
+        self._obs = [torch.zeros(n, self.obs_dim, device=self.device), torch.zeros(n, self.obs_dim, device=self.device)]
         self._k = 0
         self.reward_buf = torch.zeros(n, device=self.device)
         self.reset_terminated = torch.zeros(n, dtype=torch.bool, device=self.device)
@@ -202,8 +210,13 @@ class H12VelocityEnv:
         self._out = H12StepOut()
         self.common_step_counter = 0
         self.extras: dict = {}
-        self.scene = SimpleNamespace(env_origins=env_origins_grid(n, self.cfg.scene.env_spacing, self.device),
-                                     num_envs=n)
+        self.terrain = None
+        self._apply_startup()
+        if self.terrain is not None:
+            origins = self._field("ORIGIN").T  # moved in-kernel by the terrain curriculum
+        else:
+            origins = env_origins_grid(n, self.cfg.scene.env_spacing, self.device)
+        self.scene = SimpleNamespace(env_origins=origins, num_envs=n, terrain=self.terrain)
         self.observation_manager = _ObservationManager(self)
         self.action_manager = _ActionManager(self)
         self._data = _ArticulationData(self)
@@ -257,18 +270,48 @@ class H12VelocityEnv:
             import numpy as np
 
             self.single_observation_space = gym.spaces.Dict(
-                {"policy": gym.spaces.Box(low=-np.inf, high=np.inf, shape=(NOBS,))})
+                {"policy": gym.spaces.Box(low=-np.inf, high=np.inf, shape=(self.obs_dim,))})
             self.single_action_space = gym.spaces.Box(low=-np.inf, high=np.inf, shape=(NJ,))
             self.observation_space = gym.vector.utils.batch_space(self.single_observation_space, self.num_envs)
             self.action_space = gym.vector.utils.batch_space(self.single_action_space, self.num_envs)
         except Exception:  # gymnasium is optional for the hot path
-            self.single_observation_space = {"policy": (NOBS,)}
+            self.single_observation_space = {"policy": (self.obs_dim,)}
             self.single_action_space = (NJ,)
-            self.observation_space = {"policy": (self.num_envs, NOBS)}
+            self.observation_space = {"policy": (self.num_envs, self.obs_dim)}
             self.action_space = (self.num_envs, NJ)
 
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ rough task: terrain + startup events
+    def _apply_startup(self):
+        """Terrain (TerrainGenerator + TerrainImporter curriculum origins) and mode="startup" events,
+        computed on the host by h12env.startup and written into the workspace once."""
+        from .startup import startup_state
+
+        st = startup_state(self.cfg, self.num_envs, self.env_offset)
+        self.terrain = st.terrain
+        for name, val in st.fields.items():
+            self._field(name).copy_(torch.from_numpy(val).to(self.device))
+        if st.terrain_cell is not None:
+            self._istate[_abi.I["TERRAIN"][0]].copy_(torch.from_numpy(st.terrain_cell).to(self.device))
+        if self.terrain is not None:
+            self._t_heights = torch.from_numpy(self.terrain.heights).to(self.device)
+            self._t_origins = torch.from_numpy(self.terrain.origins).to(self.device)
+            self._bind_terrain()
+
+    def _bind_terrain(self):
+        t = self.terrain
+        if t is None:
+            return
+        rows, cols = t.origins.shape[:2]
+        check(self._lib, self._lib.h12env_set_terrain(self._h, C.c_void_p(self._t_heights.data_ptr()), t.shape[0],
+                                                       t.shape[1], t.hscale, t.x0, t.y0,
+                                                       C.c_void_p(self._t_origins.data_ptr()), rows, cols),
+              "h12env_set_terrain")
+
+    def terrain_levels(self) -> torch.Tensor:
+        return (self._istate[_abi.I["TERRAIN"][0]] & 0xFFFF).float()
 
     # ------------------------------------------------------------------ gym API
     def seed(self, seed: int = -1) -> int:
@@ -281,6 +324,7 @@ class H12VelocityEnv:
                                                  C.c_void_p(self._state.data_ptr()), C.byref(h)), "h12env_create")
         self._lib.h12env_destroy(self._h)
         self._h = h
+        self._bind_terrain()
         return int(seed)
 
     def reset(self, seed: int | None = None, env_ids=None, options=None):
@@ -322,7 +366,8 @@ class H12VelocityEnv:
                                    self.common_step_counter, self._stream())
         if rc:
             check(self._lib, rc, "h12env_step")
-        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s), "time_outs": self.reset_time_outs}
+        extra = {"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()} if self.terrain is not None else None
+        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, extra), "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
         return {"policy": obs_out}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
 

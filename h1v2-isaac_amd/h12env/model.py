@@ -61,6 +61,7 @@ def build_model() -> H12Model:
         m.knee_p1[a] = d["knee"]["p1"][a]
         m.torso_center[a] = d["torso_box"]["center"][a]
         m.torso_half[a] = d["torso_box"]["half"][a]
+        m.torso_com[a] = d["torso_link"]["com"][a]
     m.knee_radius = d["knee"]["radius"]
     m.gravity = d["gravity"]
     assert len(d["joints"]) == NJ

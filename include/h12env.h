@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 1
+#define H12ENV_ABI_VERSION 2
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length (flat_env_cfg.py:26) */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -48,6 +48,13 @@ extern "C" {
 #define H12_NFOOT_PTS 4    /* sole contact spheres per foot (URDF rods, h12_12dof.urdf:168-191) */
 #define H12_NREW 12        /* active reward terms of the Flat task */
 #define H12_NLOG 16        /* log accumulator: 12 episode sums, count, 2 termination counts, spare */
+/* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:128-188): no history, base_lin_vel
+ * first, height scan last (velocity_env_cfg.py:118-137) */
+#define H12_ROUGH_FRAME 48 /* lin_vel 3, ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
+#define H12_SCAN_NX 17     /* GridPatternCfg(resolution 0.1, size (1.6, 1.0)), velocity_env_cfg.py:60-66 */
+#define H12_SCAN_NY 11
+#define H12_NSCAN (H12_SCAN_NX * H12_SCAN_NY) /* 187 */
+#define H12_NOBS_ROUGH (H12_ROUGH_FRAME + H12_NSCAN) /* 235 */
 
 /* error codes */
 #define H12_OK 0
@@ -59,6 +66,10 @@ extern "C" {
 /* simulation modes */
 #define H12_MODE_ISAACLAB 0 /* explicit PD once per physics step with per-group delay + effort clip */
 #define H12_MODE_MUJOCO 1   /* PD every substep, no delay, MJCF actuatorfrcrange clamp (sim2sim) */
+
+/* tasks (observation layout) */
+#define H12_TASK_FLAT 0     /* 450-float term-major 10-frame history (flat_env_cfg.py:25-27) */
+#define H12_TASK_ROUGH 1    /* 235 floats: 48-float frame + 187-ray height scan, no history */
 
 /* reward term order (RewardManager order of the merged Flat cfg; weights in h12env_config.rew_w) */
 enum {
@@ -99,6 +110,8 @@ typedef struct h12env_model {
   float knee_radius;
   float torso_center[3], torso_half[3]; /* torso collision box in base frame */
   float gravity;                 /* 9.81 */
+  float torso_com[3];            /* torso_link COM in base frame (h12_12dof.xml:144): where the
+                                    randomize_rigid_body_mass event adds mass (cat_env_cfg.py:240-249) */
 } h12env_model;
 
 /* Task / simulation configuration. h12env_config_default() fills the Flat-H12_12dof values. */
@@ -137,6 +150,18 @@ typedef struct h12env_config {
   float soft_limit_factor;     /* 0.9 (h12.py:56) */
   int32_t illegal_contact_knees, illegal_contact_torso; /* bodies with colliders among the list */
   uint64_t seed;
+  /* rough task / terrain / startup randomisation (ABI 2) */
+  int32_t task;                /* H12_TASK_* */
+  int32_t terrain;             /* 0 plane z = 0, 1 heightfield (h12env_set_terrain) */
+  int32_t terrain_curriculum;  /* terrain_levels_vel on reset (velocity/mdp/curriculums.py:21-52) */
+  int32_t per_env_friction;    /* sole friction from H12_F_MU (randomize_rigid_body_material buckets) */
+  int32_t per_env_mass;        /* added torso mass from H12_F_DMASS (randomize_rigid_body_mass) */
+  float noise_lin_vel;         /* 0.1 (velocity_env_cfg.py:118) */
+  float noise_height_scan;     /* 0.1 (velocity_env_cfg.py:131-136) */
+  float scan_offset;           /* 0.5: height = sensor z - hit z - offset (isaaclab mdp.height_scan) */
+  float scan_clip;             /* 1.0 */
+  float scan_resolution;       /* 0.1 m grid spacing */
+  float terrain_size;          /* 8.0 m sub-terrain edge (terrains.py:12) */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */
@@ -158,18 +183,22 @@ enum {
   H12_F_LAST_CONTACT = 72, /* 2 last_contact_time */
   H12_F_EPSUM = 74,     /* 12 episode reward sums */
   H12_F_ANCHOR = 86,    /* 16 sole-sphere stiction anchors: [foot][pt][x,y] world (env-local) */
-  H12_NF_FLOAT = 102
+  H12_F_ORIGIN = 102,   /* 3  env origin (terrain origin of the env's level / type; 0 on the plane) */
+  H12_F_MU = 105,       /* 4  static, dynamic friction of the left / right sole (per_env_friction) */
+  H12_F_DMASS = 109,    /* 1  mass added at the torso COM (per_env_mass) */
+  H12_NF_FLOAT = 110
 };
 enum {
   H12_I_EPLEN = 0,      /* episode_length_buf (int32) */
   H12_I_PACK = 1,       /* bits 0-8 lags (3 x 3 bits), 9-10 steps since reset (sat. 2), 11 heading env,
                            12 standing env, 13-20 sole-sphere contact flags (bit 13 + 4*foot + pt) */
-  H12_NF_INT = 2
+  H12_I_TERRAIN = 2,    /* terrain level (bits 0-15) and terrain type / column (bits 16-31) */
+  H12_NF_INT = 3
 };
 
 /* Optional per-step outputs; any pointer may be NULL. */
 typedef struct h12env_step_out {
-  float* obs;              /* N x 450 (required) */
+  float* obs;              /* N x 450 (flat) or N x 235 (rough) (required) */
   float* rew;              /* N       (required) */
   uint8_t* terminated;     /* N       (required) */
   uint8_t* truncated;      /* N       (required) */
@@ -198,6 +227,13 @@ int h12env_step(h12env* h, const float* actions, const float* obs_prev, const h1
  * env's history (obs_prev -> obs, may alias); fill_mask[i] != 0 fills env i's history with the frame
  * (the first push after a reset).  fill_mask may be NULL. */
 int h12env_observe(h12env* h, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream);
+/* Heightfield terrain (cfg.terrain = 1), device arrays owned by the caller and kept alive while the
+ * handle uses them: heights[ix * ny + iy] is the ground height at (x0 + ix*hscale, y0 + iy*hscale),
+ * triangulated like isaaclab.terrains.utils.convert_height_field_to_mesh (cells split along the
+ * (ix, iy) -> (ix+1, iy+1) diagonal); origins[(level * cols + type) * 3 + k] are the sub-terrain
+ * origins the curriculum moves envs between.  Replaces TerrainImporter (velocity_env_cfg.py:40-56). */
+int h12env_set_terrain(h12env* h, const float* heights, int nx, int ny, float hscale, float x0, float y0,
+                       const float* origins, int rows, int cols);
 /* Parity hook: n_substeps physics steps with a held joint target q_ref (N x 12) using the
  * configured mode (PD, limits, contact), no MDP.  Mirrors H12Mujoco.step. */
 int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* stream);

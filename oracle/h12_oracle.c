@@ -44,6 +44,41 @@ static void rng_block(uint64_t seed, int64_t env, uint32_t ctr_lo, uint32_t ctr_
   orc_philox(seed, (uint32_t)env, ctr_lo, ((uint32_t)stream << 16) | (uint32_t)block, ctr_hi, out);
 }
 
+/* ------------------------------------------------------------------ terrain */
+static struct {
+  const float* h;
+  int nx, ny, rows, cols;
+  double hs, x0, y0;
+  const float* origins;
+} g_terrain;
+
+void orc_set_terrain(const float* heights, int nx, int ny, double hscale, double x0, double y0,
+                     const float* origins, int rows, int cols) {
+  g_terrain.h = heights; g_terrain.nx = nx; g_terrain.ny = ny; g_terrain.hs = hscale;
+  g_terrain.x0 = x0; g_terrain.y0 = y0; g_terrain.origins = origins; g_terrain.rows = rows; g_terrain.cols = cols;
+}
+
+/* triangle mesh of isaaclab.terrains.utils.convert_height_field_to_mesh: cell (ix, iy) split along
+ * its (ix, iy)-(ix+1, iy+1) diagonal; barycentric height on the containing triangle */
+double orc_ground(const h12env_config* c, double x, double y, double* gx, double* gy) {
+  if (!c->terrain || !g_terrain.h) { *gx = *gy = 0; return 0; }
+  double u = (x - g_terrain.x0) / g_terrain.hs, v = (y - g_terrain.y0) / g_terrain.hs;
+  double umax = g_terrain.nx - 1 - 1e-3, vmax = g_terrain.ny - 1 - 1e-3;
+  u = u < 0 ? 0 : (u > umax ? umax : u);
+  v = v < 0 ? 0 : (v > vmax ? vmax : v);
+  int ix = (int)u, iy = (int)v;
+  double fu = u - ix, fv = v - iy;
+  const float* hp = g_terrain.h + (size_t)ix * g_terrain.ny + iy;
+  double h00 = hp[0], h01 = hp[1], h10 = hp[g_terrain.ny], h11 = hp[g_terrain.ny + 1], a, b;
+  if (fv >= fu) { a = h11 - h01; b = h01 - h00; }
+  else { a = h10 - h00; b = h11 - h10; }
+  *gx = a / g_terrain.hs;
+  *gy = b / g_terrain.hs;
+  return h00 + fu * a + fv * b;
+}
+
+int orc_obs_dim(const h12env_config* c) { return c->task == H12_TASK_ROUGH ? H12_NOBS_ROUGH : H12_NOBS; }
+
 /* ------------------------------------------------------------------ small linear algebra */
 typedef double m3[3][3];
 static void cross3(const double a[3], const double b[3], double o[3]) {
@@ -174,6 +209,13 @@ static void kinematics(const h12env_model* m, const orc_phys* s, kin_t* k) {
   quat_to_R(s->quat, k->R[0]);
   memcpy(k->p[0], s->pos, sizeof(double) * 3);
   rb_inertia(m->base_mass, m->base_com, m->base_inertia, k->I[0]);
+  if (s->env_params && s->dmass != 0.0) { /* point mass at the torso COM (randomize_rigid_body_mass) */
+    m6 Ip;
+    const float zero6[6] = {0, 0, 0, 0, 0, 0};
+    rb_inertia(s->dmass, m->torso_com, zero6, Ip);
+    for (int a = 0; a < 6; ++a)
+      for (int b2 = 0; b2 < 6; ++b2) k->I[0][a][b2] += Ip[a][b2];
+  }
   double vb[3];
   m3tv(k->R[0], s->vlin, vb);
   k->v[0][0] = s->wang[0]; k->v[0][1] = s->wang[1]; k->v[0][2] = s->wang[2];
@@ -207,18 +249,22 @@ static void kinematics(const h12env_model* m, const orc_phys* s, kin_t* k) {
  * along when slipping); for knee / torso a viscous term capped at mu_dynamic.  Accumulates the
  * spatial force (body coords) into fext[b] and the world force into fw.  Returns 1 in contact. */
 static int contact_point(const h12env_config* c, const kin_t* k, int b, const double pl[3], double rad,
-                         double fext[NB][6], double fw[3], const double* anc_in, int was_in, double* anc_out) {
+                         double fext[NB][6], double fw[3], const double* anc_in, int was_in, double* anc_out,
+                         double mus, double mud) {
   double xw[3];
   m3v(k->R[b], pl, xw);
   for (int a = 0; a < 3; ++a) xw[a] += k->p[b][a];
-  double depth = rad - xw[2];
+  double gx, gy, hg = orc_ground(c, xw[0], xw[1], &gx, &gy);
+  double in = 1.0 / sqrt(1.0 + gx * gx + gy * gy), nrm[3] = {-gx * in, -gy * in, in};
+  double depth = rad - (xw[2] - hg) * in;
   if (depth <= 0) return 0;
   double vl[3];
   cross3(k->v[b], pl, vl);
   for (int a = 0; a < 3; ++a) vl[a] += k->v[b][3 + a];
   double vw[3];
   m3v(k->R[b], vl, vw);
-  double fn = c->contact_k * depth - c->contact_c * vw[2];
+  double vn = nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2];
+  double fn = c->contact_k * depth - c->contact_c * vn;
   if (fn <= 0) return 0;
   double ft0, ft1;
   if (anc_out) {
@@ -226,8 +272,8 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
     ft0 = -c->friction_k * (xw[0] - ax) - c->friction_c * vw[0];
     ft1 = -c->friction_k * (xw[1] - ay) - c->friction_c * vw[1];
     double ftn = sqrt(ft0 * ft0 + ft1 * ft1);
-    if (ftn > c->mu_static * fn) {
-      double sc = c->mu_dynamic * fn / ftn;
+    if (ftn > mus * fn) {
+      double sc = mud * fn / ftn;
       ft0 *= sc;
       ft1 *= sc;
       ax = xw[0] + ft0 / c->friction_k;
@@ -238,10 +284,11 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   } else {
     ft0 = -c->friction_c * vw[0];
     ft1 = -c->friction_c * vw[1];
-    double ftn = sqrt(ft0 * ft0 + ft1 * ft1), cap = c->mu_dynamic * fn;
+    double ftn = sqrt(ft0 * ft0 + ft1 * ft1), cap = mud * fn;
     if (ftn > cap) { ft0 *= cap / ftn; ft1 *= cap / ftn; }
   }
-  double F[3] = {ft0, ft1, fn}, fl[3], nl[3];
+  /* normal force along the ground normal, tangential (stiction / drag) force in world xy */
+  double F[3] = {ft0 + fn * nrm[0], ft1 + fn * nrm[1], fn * nrm[2]}, fl[3], nl[3];
   m3tv(k->R[b], F, fl);
   cross3(pl, fl, nl);
   for (int a = 0; a < 3; ++a) { fext[b][a] += nl[a]; fext[b][3 + a] += fl[a]; fw[a] += F[a]; }
@@ -262,7 +309,9 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
       int bit = 4 * f + p;
       double tmp[2];
       double* out = next_anchor ? next_anchor[f][p] : tmp;
-      if (contact_point(c, k, b, pl, m->foot_radius, fext, r.foot_force[f], s->anchor[f][p], (s->cmask >> bit) & 1, out))
+      double mus = s->env_params ? s->mu[f][0] : c->mu_static, mud = s->env_params ? s->mu[f][1] : c->mu_dynamic;
+      if (contact_point(c, k, b, pl, m->foot_radius, fext, r.foot_force[f], s->anchor[f][p], (s->cmask >> bit) & 1, out,
+                        mus, mud))
         mask |= 1 << bit;
     }
     /* knee capsule: lower end point of the segment in world z */
@@ -271,7 +320,8 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
     double w0[3], w1[3];
     m3v(k->R[bk], a0, w0);
     m3v(k->R[bk], a1, w1);
-    contact_point(c, k, bk, (w0[2] <= w1[2]) ? a0 : a1, m->knee_radius, fext, r.knee_force[f], 0, 0, 0);
+    contact_point(c, k, bk, (w0[2] <= w1[2]) ? a0 : a1, m->knee_radius, fext, r.knee_force[f], 0, 0, 0,
+                  c->mu_static, c->mu_dynamic);
   }
   /* torso box (welded to the base): lowest corner */
   double corner[3];
@@ -279,7 +329,7 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
     double sg = k->R[0][2][a] > 0 ? -1.0 : 1.0;
     corner[a] = m->torso_center[a] + sg * m->torso_half[a];
   }
-  contact_point(c, k, 0, corner, 0.0, fext, r.torso_force, 0, 0, 0);
+  contact_point(c, k, 0, corner, 0.0, fext, r.torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic);
   if (rep) *rep = r;
   if (next_mask) *next_mask = mask;
 }
@@ -496,6 +546,11 @@ int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy
     m3v(k.R[b], cl, cw);
     pe += mass * m->gravity * (k.p[b][2] + cw[2]);
   }
+  if (s->env_params && s->dmass != 0.0) { /* added torso point mass: kinetic part is in k.I[0] */
+    double ct[3] = {m->torso_com[0], m->torso_com[1], m->torso_com[2]}, cw[3];
+    m3v(k.R[0], ct, cw);
+    pe += s->dmass * m->gravity * (k.p[0][2] + cw[2]);
+  }
   for (int j = 0; j < NJ; ++j) ke += 0.5 * m->armature[j] * s->qd[j] * s->qd[j];
   *energy = ke + pe;
   return 0;
@@ -576,7 +631,26 @@ typedef struct orc_env {
   orc_phys p;
   double act[NJ], act_prev[NJ], cmd[3], heading, cmd_time, air[2], con[2], last_air[2], last_con[2], epsum[H12_NREW];
   int eplen, lag[3], since_reset, is_heading, is_standing;
+  double origin[3];
+  int32_t tcell; /* terrain level | type << 16 */
 } orc_env;
+
+/* per-env startup parameters and terrain cell (fields used by the configured features only) */
+static void env_load_extra(const h12env_config* c, const float* F, const int32_t* I, int n, int i, orc_env* e) {
+  e->p.env_params = c->per_env_friction || c->per_env_mass;
+  for (int f = 0; f < 2; ++f) {
+    e->p.mu[f][0] = c->per_env_friction ? F[(size_t)(H12_F_MU + 2 * f) * n + i] : c->mu_static;
+    e->p.mu[f][1] = c->per_env_friction ? F[(size_t)(H12_F_MU + 2 * f + 1) * n + i] : c->mu_dynamic;
+  }
+  e->p.dmass = c->per_env_mass ? F[(size_t)H12_F_DMASS * n + i] : 0.0;
+  for (int a = 0; a < 3; ++a) e->origin[a] = c->terrain ? F[(size_t)(H12_F_ORIGIN + a) * n + i] : 0.0;
+  e->tcell = (c->terrain && I) ? I[(size_t)H12_I_TERRAIN * n + i] : 0;
+}
+static void env_store_extra(const h12env_config* c, float* F, int32_t* I, int n, int i, const orc_env* e) {
+  if (!c->terrain) return;
+  for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_ORIGIN + a) * n + i] = (float)e->origin[a];
+  I[(size_t)H12_I_TERRAIN * n + i] = e->tcell;
+}
 
 static void env_load(const float* F, const int32_t* I, int n, int i, orc_env* e) {
 #define LD(dst, fld, cnt) for (int a = 0; a < (cnt); ++a) (dst)[a] = F[(size_t)((fld) + a) * n + i]
@@ -656,10 +730,36 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   uint32_t r0[4], r1[4];
   rng_block(c->seed, g, lo, hi, ST_RESET, 0, r0);
   rng_block(c->seed, g, lo, hi, ST_RESET, 1, r1);
+  if (c->terrain_curriculum && g_terrain.origins) {
+    /* terrain_levels_vel (velocity/mdp/curriculums.py:21-52) on the pre-reset state, then
+     * TerrainImporter.update_env_origins (solvers of the last level go to a random one) */
+    double dx = e->p.pos[0] - e->origin[0], dy = e->p.pos[1] - e->origin[1];
+    double dist = sqrt(dx * dx + dy * dy);
+    double ep_s = c->max_episode_length * c->physics_dt * c->decimation;
+    int up = dist > 0.5 * c->terrain_size;
+    int down = !up && dist < sqrt(e->cmd[0] * e->cmd[0] + e->cmd[1] * e->cmd[1]) * ep_s * 0.5;
+    int lvl = (e->tcell & 0xFFFF) + up - down, typ = e->tcell >> 16;
+    if (lvl >= g_terrain.rows) {
+      uint32_t r2[4];
+      rng_block(c->seed, g, lo, hi, ST_RESET, 2, r2);
+      lvl = (int)(r2[0] % (uint32_t)g_terrain.rows);
+    }
+    if (lvl < 0) lvl = 0;
+    e->tcell = lvl | (typ << 16);
+    const float* o = g_terrain.origins + 3 * ((size_t)lvl * g_terrain.cols + typ);
+    for (int a = 0; a < 3; ++a) e->origin[a] = o[a];
+  }
+  /* keep the per-env startup parameters across the state reset */
+  int32_t ep = e->p.env_params;
+  double mu[2][2], dm = e->p.dmass;
+  memcpy(mu, e->p.mu, sizeof mu);
   memset(&e->p, 0, sizeof e->p);
-  e->p.pos[0] = uab(r0[0], c->reset_x[0], c->reset_x[1]);
-  e->p.pos[1] = uab(r0[1], c->reset_y[0], c->reset_y[1]);
-  e->p.pos[2] = m->root_height;
+  e->p.env_params = ep;
+  memcpy(e->p.mu, mu, sizeof mu);
+  e->p.dmass = dm;
+  e->p.pos[0] = e->origin[0] + (double)(float)uab(r0[0], c->reset_x[0], c->reset_x[1]);
+  e->p.pos[1] = e->origin[1] + (double)(float)uab(r0[1], c->reset_y[0], c->reset_y[1]);
+  e->p.pos[2] = e->origin[2] + m->root_height;
   double yaw = uab(r0[2], c->reset_yaw[0], c->reset_yaw[1]);
   e->p.quat[0] = cos(0.5 * (float)yaw);
   e->p.quat[3] = sin(0.5 * (float)yaw);
@@ -732,6 +832,61 @@ static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* 
   }
 }
 
+/* root (composite COM) linear velocity in world; the COM moves with the added torso mass */
+static void base_com_vel(const h12env_model* m, const orc_phys* p, const m3 R, double vcom[3]) {
+  double c[3], M = m->base_mass + (p->env_params ? p->dmass : 0.0);
+  for (int a = 0; a < 3; ++a)
+    c[a] = (m->base_mass * m->base_com[a] + (p->env_params ? p->dmass * m->torso_com[a] : 0.0)) / M;
+  double wb[3] = {p->wang[0], p->wang[1], p->wang[2]}, ww[3], cw[3], wxc[3];
+  m3v(R, wb, ww);
+  m3v(R, c, cw);
+  cross3(ww, cw, wxc);
+  for (int a = 0; a < 3; ++a) vcom[a] = p->vlin[a] + wxc[a];
+}
+
+/* Rough task observation row (velocity_env_cfg.py:118-137): base_lin_vel, base_ang_vel, projected_gravity,
+ * velocity_commands, joint_pos_rel, joint_vel_rel, last_action, height_scan; noise then clip.  Height scan:
+ * 17 x 11 rays at 0.1 m around the torso_link origin (= pelvis origin), yaw-aligned, x fastest;
+ * value = sensor z - ground z - 0.5 (isaaclab mdp.height_scan). */
+static void obs_row_rough(const h12env_model* m, const h12env_config* c, const orc_env* e, int64_t g, uint32_t lo,
+                          uint32_t hi, float* out) {
+  m3 R;
+  quat_to_R(e->p.quat, R);
+  double v[H12_NOBS_ROUGH];
+  double vcom[3], vb[3], gw[3] = {0, 0, -1}, gb[3];
+  base_com_vel(m, &e->p, R, vcom);
+  m3tv(R, vcom, vb);
+  m3tv(R, gw, gb);
+  int k = 0;
+  for (int a = 0; a < 3; ++a) v[k++] = vb[a];
+  for (int a = 0; a < 3; ++a) v[k++] = e->p.wang[a];
+  for (int a = 0; a < 3; ++a) v[k++] = gb[a];
+  for (int a = 0; a < 3; ++a) v[k++] = e->cmd[a];
+  for (int j = 0; j < NJ; ++j) v[k++] = e->p.q[j] - m->q_default[j];
+  for (int j = 0; j < NJ; ++j) v[k++] = e->p.qd[j];
+  for (int j = 0; j < NJ; ++j) v[k++] = e->act[j];
+  double hx = R[0][0], hy = R[1][0], hn = sqrt(hx * hx + hy * hy), cy = hx / hn, sy = hy / hn;
+  for (int iy = 0; iy < H12_SCAN_NY; ++iy)
+    for (int ix = 0; ix < H12_SCAN_NX; ++ix) {
+      double xl = c->scan_resolution * (ix - (H12_SCAN_NX - 1) / 2), yl = c->scan_resolution * (iy - (H12_SCAN_NY - 1) / 2);
+      double gx, gy;
+      double hz = orc_ground(c, e->p.pos[0] + cy * xl - sy * yl, e->p.pos[1] + sy * xl + cy * yl, &gx, &gy);
+      v[k++] = e->p.pos[2] - hz - c->scan_offset;
+    }
+  for (int kk = 0; kk < H12_NOBS_ROUGH; ++kk) {
+    int t = kk < 9 ? kk : ((kk >= 12 && kk < 36) ? kk - 3 : (kk >= H12_ROUGH_FRAME ? kk - 15 : -1));
+    if (t >= 0 && c->enable_corruption) {
+      uint32_t r[4];
+      rng_block(c->seed, g, lo, hi, ST_OBS, t >> 2, r);
+      double nmax = t < 3 ? c->noise_lin_vel : t < 6 ? c->noise_ang_vel : t < 9 ? c->noise_gravity
+                  : t < 21 ? c->noise_joint_pos : t < 33 ? c->noise_joint_vel : c->noise_height_scan;
+      v[kk] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)u01(r[t & 3]));
+    }
+    if (kk >= H12_ROUGH_FRAME) v[kk] = v[kk] < -c->scan_clip ? -c->scan_clip : (v[kk] > c->scan_clip ? c->scan_clip : v[kk]);
+    out[kk] = (float)v[kk];
+  }
+}
+
 /* DelayBuffer = CircularBuffer(max_delay + 1)[lag] (circular_buffer.py:139-170) with one push per
  * physics step and a constant target within an env step: the delayed target of substep s is the
  * target of env step t - src.  The first push after a reset fills the ring (:131-135), which the
@@ -754,6 +909,11 @@ int orc_env_observe(const h12env_model* m, const h12env_config* c, int n, int64_
   for (int i = 0; i < n; ++i) {
     orc_env e;
     env_load(F, I, n, i, &e);
+    env_load_extra(c, F, I, n, i, &e);
+    if (c->task == H12_TASK_ROUGH) {
+      obs_row_rough(m, c, &e, env_offset + i, lo, hi, obs + (size_t)i * H12_NOBS_ROUGH);
+      continue;
+    }
     double fr[H12_OBS_FRAME];
     obs_frame(m, c, &e, env_offset + i, lo, hi, fr);
     obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, fill_mask ? fill_mask[i] : 0);
@@ -767,13 +927,19 @@ int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t 
   for (int i = 0; i < n; ++i) {
     if (mask && !mask[i]) continue;
     orc_env e;
-    memset(&e, 0, sizeof e);
+    env_load(F, I, n, i, &e); /* the pre-reset state feeds the terrain curriculum */
+    env_load_extra(c, F, I, n, i, &e);
     int64_t g = env_offset + i;
     env_reset_one(m, c, &e, g, lo, hi);
-    double fr[H12_OBS_FRAME];
-    obs_frame(m, c, &e, g, lo, hi, fr);
-    obs_write(fr, 0, obs + (size_t)i * H12_NOBS, 1);
+    if (c->task == H12_TASK_ROUGH) {
+      obs_row_rough(m, c, &e, g, lo, hi, obs + (size_t)i * H12_NOBS_ROUGH);
+    } else {
+      double fr[H12_OBS_FRAME];
+      obs_frame(m, c, &e, g, lo, hi, fr);
+      obs_write(fr, 0, obs + (size_t)i * H12_NOBS, 1);
+    }
     env_store(F, I, n, i, &e);
+    env_store_extra(c, F, I, n, i, &e);
   }
   return 0;
 }
@@ -795,6 +961,7 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
   for (int i = 0; i < n; ++i) {
     orc_env e;
     env_load(F, I, n, i, &e);
+    env_load_extra(c, F, I, n, i, &e);
     const int64_t g = env_offset + i;
     double a_t[NJ], a_t1[NJ], a_t2[NJ];
     for (int j = 0; j < NJ; ++j) {
@@ -868,11 +1035,8 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
     m3v(R, wb, ww);
     double gw[3] = {0, 0, -1}, gb[3];
     m3tv(R, gw, gb);
-    /* root (COM) linear velocity in world: v_origin + w x (R c) */
-    double cw[3], bc[3] = {m->base_com[0], m->base_com[1], m->base_com[2]}, wxc[3], vcom[3];
-    m3v(R, bc, cw);
-    cross3(ww, cw, wxc);
-    for (int a = 0; a < 3; ++a) vcom[a] = e.p.vlin[a] + wxc[a];
+    double vcom[3];
+    base_com_vel(m, &e.p, R, vcom);
     double yaw = atan2(R[1][0], R[0][0]);
     double cy = cos(yaw), sy = sin(yaw);
     double vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
@@ -963,10 +1127,15 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
     e.cmd_time -= step_dt;
     if (e.cmd_time <= 0) cmd_resample(c, &e, g, lo, hi);
     cmd_update(c, &e);
-    double fr[H12_OBS_FRAME];
-    obs_frame(m, c, &e, g, lo, hi, fr);
-    obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, reset);
+    if (c->task == H12_TASK_ROUGH) {
+      obs_row_rough(m, c, &e, g, lo, hi, obs + (size_t)i * H12_NOBS_ROUGH);
+    } else {
+      double fr[H12_OBS_FRAME];
+      obs_frame(m, c, &e, g, lo, hi, fr);
+      obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, reset);
+    }
     env_store(F, I, n, i, &e);
+    env_store_extra(c, F, I, n, i, &e);
   }
   return err;
 }
@@ -987,6 +1156,7 @@ int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, f
     for (int j = 0; j < NJ; ++j) { e.p.q[j] = F[(size_t)(H12_F_Q + j) * n + i]; e.p.qd[j] = F[(size_t)(H12_F_QD + j) * n + i]; }
     for (int a = 0; a < 16; ++a) (&e.p.anchor[0][0][0])[a] = F[(size_t)(H12_F_ANCHOR + a) * n + i];
     e.p.cmask = *cmask;
+    env_load_extra(c, F, I, n, i, &e);
     for (int t = 0; t < n_substeps; ++t) {
       double tau[NJ];
       for (int j = 0; j < NJ; ++j) {

@@ -13,7 +13,9 @@
  *   - the explicit delayed PD actuator (packages/biped_assets/biped_assets/robots/h12.py:58-112;
  *     delay indexing = CircularBuffer.__getitem__, .../utils/history/circular_buffer.py:139-170);
  *   - the MDP terms of Isaac-Velocity-Flat-H12_12dof-v0 (rewards, terminations, resets,
- *     commands, observations + 10-frame history) as restated in SURVEY.md §8(a).
+ *     commands, observations + 10-frame history) as restated in SURVEY.md §8(a);
+ *   - the rough task's additions (heightfield contact, height scan, base_lin_vel, terrain
+ *     curriculum, per-env friction / added torso mass) as restated in DESIGN.md (row f2).
  *
  * Parity status: the algorithm of record (PhysX / MuJoCo / IsaacLab managers) is not present
  * in this container, so physics parity against it is UNPINNED; the oracle itself is pinned
@@ -34,6 +36,9 @@ typedef struct orc_phys {
   double pos[3], quat[4], vlin[3], wang[3], q[H12_NJ], qd[H12_NJ];
   double anchor[2][H12_NFOOT_PTS][2]; /* sole-sphere stiction anchors (world x, y) */
   int32_t cmask;                      /* bit 4f+p: sole sphere p of foot f was in contact */
+  int32_t env_params;                 /* 1: mu / dmass below apply (per-env startup randomisation) */
+  double mu[2][2];                    /* static, dynamic friction of the left / right sole */
+  double dmass;                       /* mass added at the torso COM */
 } orc_phys;
 
 /* per physics-step contact report */
@@ -85,6 +90,15 @@ int orc_env_observe(const h12env_model* m, const h12env_config* c, int n, int64_
 int orc_delay_source(int lag, int since_reset, int substep, int decimation);
 /* One history update of a 450-float observation row (term-major, oldest -> newest). */
 void orc_history_write(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill);
+
+/* Heightfield used while c->terrain = 1 (same layout as h12env_set_terrain; host arrays, kept alive by the
+ * caller).  Process-global: the oracle is single-terrain test infrastructure. */
+void orc_set_terrain(const float* heights, int nx, int ny, double hscale, double x0, double y0,
+                     const float* origins, int rows, int cols);
+/* Ground height and slope at (x, y) (plane z = 0 when c->terrain = 0). */
+double orc_ground(const h12env_config* c, double x, double y, double* gx, double* gy);
+/* Observation row length of the configured task: 450 (flat) or 235 (rough). */
+int orc_obs_dim(const h12env_config* c);
 
 /* RNG shared by both sides (Philox4x32-10). */
 void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]);

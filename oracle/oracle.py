@@ -16,7 +16,7 @@ HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent
 sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 
-from h12env._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, H12Config, H12Model  # noqa: E402
+from h12env._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, NOBS_ROUGH, TASK_ROUGH, H12Config, H12Model  # noqa: E402
 
 LIB = HERE / "liboracle.so"
 
@@ -24,7 +24,8 @@ LIB = HERE / "liboracle.so"
 class Phys(C.Structure):
     _fields_ = [("pos", C.c_double * 3), ("quat", C.c_double * 4), ("vlin", C.c_double * 3),
                 ("wang", C.c_double * 3), ("q", C.c_double * NJ), ("qd", C.c_double * NJ),
-                ("anchor", C.c_double * 16), ("cmask", C.c_int32)]
+                ("anchor", C.c_double * 16), ("cmask", C.c_int32), ("env_params", C.c_int32),
+                ("mu", C.c_double * 4), ("dmass", C.c_double)]
 
     def to_numpy(self) -> np.ndarray:
         """37 physics coordinates + 16 anchors + contact mask (as float)."""
@@ -84,6 +85,10 @@ def lib():
         L.orc_history_write.restype = None
         L.orc_philox.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
         L.orc_philox.restype = None
+        L.orc_set_terrain.argtypes = [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, vp, C.c_int, C.c_int]
+        L.orc_set_terrain.restype = None
+        L.orc_ground.argtypes = [Cf, C.c_double, C.c_double, dp, dp]
+        L.orc_ground.restype = C.c_double
         _lib = L
     return _lib
 
@@ -161,6 +166,25 @@ def mujoco_rollout(model, cfg, state, q_ref, n_steps, contact=False, algo=0):
     return s.to_numpy(), traj
 
 
+_terrain_keepalive = None
+
+
+def set_terrain(heights, hscale, x0, y0, origins=None):
+    """Install the heightfield the oracle uses while cfg.terrain = 1 (process-global)."""
+    global _terrain_keepalive
+    h = np.ascontiguousarray(heights, dtype=np.float32)
+    o = None if origins is None else np.ascontiguousarray(origins, dtype=np.float32)
+    _terrain_keepalive = (h, o)
+    rows, cols = (0, 0) if o is None else o.shape[:2]
+    lib().orc_set_terrain(_p(h), h.shape[0], h.shape[1], float(hscale), float(x0), float(y0), _p(o), rows, cols)
+
+
+def ground(cfg, x, y):
+    gx, gy = np.zeros(1), np.zeros(1)
+    h = lib().orc_ground(C.byref(cfg), float(x), float(y), _d(gx), _d(gy))
+    return h, gx[0], gy[0]
+
+
 class OracleEnv:
     """Batched oracle env on the same SoA workspace layout as libh12env."""
 
@@ -168,7 +192,7 @@ class OracleEnv:
         self.model, self.cfg, self.n, self.env_offset = model, cfg, n, env_offset
         self.F = np.zeros((NF_FLOAT, n), dtype=np.float32)
         self.I = np.zeros((NF_INT, n), dtype=np.int32)
-        self.obs = np.zeros((n, NOBS), dtype=np.float32)
+        self.obs = np.zeros((n, NOBS_ROUGH if cfg.task == TASK_ROUGH else NOBS), dtype=np.float32)
         self.reset_counter = 0
         self.observe_counter = 0
 

@@ -1,0 +1,110 @@
+"""GPU parity of the rough task (row f2) through the C-ABI against the oracle: heightfield contact, the
+235-float observation with the height scan, the in-kernel terrain curriculum, per-env friction and added
+torso mass (BASELINE config C5's randomisation).  Tolerances as in test_gpu_parity.py: observations
+rtol 1e-5 at reset; physics / MDP steps >= 99 % of envs at 2e-3 (fp32 vs fp64 can flip a contact or
+slip decision near its threshold); integer state (terrain cells, lags, counters) bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from h12env._abi import F as FIELDS
+from h12env._abi import I as IFIELDS
+from h12env._abi import NOBS_ROUGH
+from h12env.cfg import H12RoughEnvCfg, c5_cfg
+from h12env.env import H12VelocityEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def make(cfg, n):
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    g = cfg.scene.terrain.terrain_generator
+    g.num_rows, g.num_cols, g.border_width = 6, 8, 5.0
+    env = H12VelocityEnv(cfg)
+    t = env.terrain
+    O.set_terrain(t.heights, t.hscale, t.x0, t.y0, t.origins)
+    ref = O.OracleEnv(env._model, env._ccfg, n)
+    ref.F[:] = env._fstate.cpu().numpy()
+    ref.I[:] = env._istate.cpu().numpy()
+    return env, ref
+
+
+def close_rows(a, b, tol=2e-3):
+    return (np.abs(a - b) <= tol * np.maximum(1, np.abs(b))).all(axis=1)
+
+
+@pytest.mark.parametrize("c5", [False, True])
+def test_rough_reset_and_steps_match_oracle(gpu, c5):
+    n = 256
+    cfg = c5_cfg(n) if c5 else H12RoughEnvCfg()
+    env, ref = make(cfg, n)
+    obs, _ = env.reset()
+    r = ref.reset()
+    assert obs["policy"].shape == (n, NOBS_ROUGH)
+    np.testing.assert_allclose(obs["policy"].cpu().numpy(), r, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(env._fstate.cpu().numpy(), ref.F, rtol=1e-6, atol=1e-6)
+    assert (env._istate.cpu().numpy() == ref.I).all()
+    rng = np.random.default_rng(21)
+    for t in range(1, 4):
+        a = rng.normal(size=(n, 12)).astype(np.float32)
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(a).cuda())
+        r_obs, r_rew, r_term, r_trunc, _ = ref.step(a, t)
+        ok = close_rows(obs["policy"].cpu().numpy(), r_obs)
+        assert ok.mean() >= 0.99, (t, ok.mean())
+        assert (term.cpu().numpy() == r_term).mean() >= 0.99
+        assert (trunc.cpu().numpy() == r_trunc).all()
+        okr = np.abs(rew.cpu().numpy() - r_rew) <= 1e-3 * np.maximum(1, np.abs(r_rew))
+        assert okr.mean() >= 0.99, (t, okr.mean())
+    env.close()
+
+
+def test_rough_physics_on_heightfield(gpu):
+    n = 512
+    env, ref = make(H12RoughEnvCfg(), n)
+    env.reset()
+    ref.reset()
+    rng = np.random.default_rng(22)
+    q_ref = (np.asarray(env._model.q_default)[None] + rng.normal(size=(n, 12)) * 0.3).astype(np.float32)
+    for _ in range(8):
+        env.step_physics(torch.from_numpy(q_ref).cuda(), 1)
+        ref.step_physics(q_ref, 1)
+    g = env._fstate.cpu().numpy()
+    ok = np.ones(n, bool)
+    for k in ("POS", "QUAT", "VLIN", "WANG", "Q", "QD"):
+        o, c = FIELDS[k]
+        a, b = g[o:o + c], ref.F[o:o + c]
+        assert np.isfinite(a).all()
+        ok &= (np.abs(a - b) / np.maximum(1, np.abs(b).max(axis=0, keepdims=True)) < 2e-3).all(axis=0)
+    assert ok.mean() >= 0.99, ok.mean()
+    env.close()
+
+
+def test_curriculum_in_kernel_matches_oracle(gpu):
+    n = 64
+    env, ref = make(H12RoughEnvCfg(), n)
+    env.reset()
+    ref.reset()
+    rng = np.random.default_rng(23)
+    F = env._fstate.cpu().numpy()
+    o, p, cmd = FIELDS["ORIGIN"][0], FIELDS["POS"][0], FIELDS["CMD"][0]
+    # random walked distances (0..6 m) and commands: a mix of up / down / stay / wrap-around
+    ang = rng.uniform(0, 2 * np.pi, n)
+    d = rng.uniform(0, 6, n)
+    F[p] = F[o] + d * np.cos(ang)
+    F[p + 1] = F[o + 1] + d * np.sin(ang)
+    F[cmd] = rng.uniform(0, 1, n)
+    env._fstate.copy_(torch.from_numpy(F))
+    ref.F[:] = F
+    env.reset()
+    ref.reset()
+    gi = env._istate.cpu().numpy()
+    assert (gi[IFIELDS["TERRAIN"][0]] == ref.I[IFIELDS["TERRAIN"][0]]).all()
+    np.testing.assert_allclose(env._fstate.cpu().numpy()[o:o + 3], ref.F[o:o + 3], atol=1e-6)
+    lv = gi[IFIELDS["TERRAIN"][0]] & 0xFFFF
+    assert len(np.unique(lv)) > 1
+    log = env.step(torch.zeros(n, 12, device="cuda"))[4]["log"]
+    lv2 = env._istate.cpu().numpy()[IFIELDS["TERRAIN"][0]] & 0xFFFF
+    assert "Curriculum/terrain_levels" in log and float(log["Curriculum/terrain_levels"]) == pytest.approx(lv2.mean())
+    env.close()

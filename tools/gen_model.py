@@ -194,6 +194,8 @@ def main():
                  "p0": (knee[0] + np.array([0, 0, knee_L / 2])).tolist(),
                  "p1": (knee[0] - np.array([0, 0, knee_L / 2])).tolist(), "radius": knee_r},
         "torso_box": {"center": torso[0].tolist(), "half": (box / 2).tolist()},
+        # torso_link is welded to the pelvis at the pelvis origin (no pos attribute, h12_12dof.xml:143)
+        "torso_link": {"pos": [0.0, 0.0, 0.0], "com": inertial_of(pelvis.find(".//body[@name='torso_link']"))[1].tolist()},
         "gravity": 9.81,
     }
     OUT.parent.mkdir(parents=True, exist_ok=True)
