@@ -5,6 +5,26 @@ import gymnasium as gym
 from . import agents  # noqa: F401
 
 gym.register(
+    id="Isaac-Velocity-Rough-H12_12dof-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "h12env.cfg:H12RoughEnvCfg",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_RoughPPORunnerCfg",
+    },
+)
+
+gym.register(
+    id="Isaac-Velocity-Rough-H12_12dof-Play-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "h12env.cfg:H12RoughEnvCfg_PLAY",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_RoughPPORunnerCfg",
+    },
+)
+
+gym.register(
     id="Isaac-Velocity-Flat-H12_12dof-v0",
     entry_point="isaaclab.envs:ManagerBasedRLEnv",
     disable_env_checker=True,

@@ -47,3 +47,16 @@ def test_train_flat_task_two_iterations(gpu, tmp_path, monkeypatch):
             obs, rew, dones, _ = env.step(policy(obs))
     assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
     env.close()
+
+
+def test_train_rough_task_one_iteration(gpu, tmp_path, monkeypatch):
+    import train
+
+    monkeypatch.chdir(tmp_path)
+    rc = train.main(["--task", "Isaac-Velocity-Rough-H12_12dof-v0", "--headless", "--num_envs", "256",
+                     "--max_iterations", "1", "env.scene.terrain.terrain_generator.num_rows=4",
+                     "env.scene.terrain.terrain_generator.num_cols=4"])
+    assert rc == 0
+    run = next((tmp_path / "logs" / "rsl_rl" / "h12_12dof_rough").iterdir())
+    x = json.loads((run / "metrics.jsonl").read_text().splitlines()[-1])
+    assert "Curriculum/terrain_levels" in x
