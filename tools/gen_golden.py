@@ -114,12 +114,35 @@ def gen_deploy_obs(rng):
                         action_in=a_in, action_out=a_out, action_scale=0.5)
 
 
+def gen_deploy_env_yaml():
+    """deploy_env_yaml.json: the shipped deploy configs (scripts/deploy/policies/*/env.yaml, read as YAML
+    data) -- top-level keys, observation entries, and the 12 leg joints' kp / kd / default_joint_pos."""
+    import json
+
+    import yaml
+
+    out = {}
+    for p in sorted((REF.parent / "scripts" / "deploy" / "policies").glob("*/env.yaml")):
+        d = yaml.safe_load(p.read_text())
+        legs = [j for j in d["joints"] if j["enabled"]]
+        out[p.parent.name] = {"keys": list(d.keys()), "observations": d["observations"],
+                              "history_length": d["history_length"], "action_scale": d["action_scale"],
+                              "control_dt": d["control_dt"], "command_ranges": d["command_ranges"],
+                              "leg_joints": legs}
+    (OUT / "deploy_env_yaml.json").write_text(json.dumps(out, indent=1))
+
+
 def main():
+    if sys.argv[1:] == ["--env-yaml"]:
+        OUT.mkdir(parents=True, exist_ok=True)
+        gen_deploy_env_yaml()
+        return
     OUT.mkdir(parents=True, exist_ok=True)
     rng = np.random.default_rng(20251121)
     gen_circular_buffer(rng)
     gen_delay_buffer(rng)
     gen_deploy_obs(rng)
+    gen_deploy_env_yaml()
     for f in sorted(OUT.glob("*.npz")):
         print(f, f.stat().st_size, "bytes")
 
