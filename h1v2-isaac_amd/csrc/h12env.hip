@@ -858,11 +858,12 @@ H12_DEV float noise_of(const KParams& P, int t, uint32_t r) {
 }
 
 // ObservationManager.compute + CircularBuffer.append for a batch of envs, full-chip.  One block owns
-// ASM_ROWS whole rows (4 x 1800 B, 16-byte aligned): the rows are staged through LDS with float4
-// loads, the rows' 8 Philox noise blocks each are drawn once (one wave), and every output float4 is
-// assembled from LDS -- the shifted history obs[e, slot h] = obs_prev[e, slot h + 1] (h < 9), or
-// the noisy new frame in the newest slot and in every slot of a row being (re)filled -- and stored
-// with one float4 store.  All global reads precede the barrier, so obs may alias obs_prev.
+// ASM_ROWS whole rows (4 x 1800 B, 16-byte aligned): the rows are staged into LDS by LDS-DMA
+// (global_load_lds_dwordx4), the frame's component-major rows are read alongside, each row's 8 Philox noise blocks
+// are drawn once (one thread each) and added to the frame in LDS, and every output float4 is assembled
+// from LDS through a column table -- the shifted history obs[e, slot h] = obs_prev[e, slot h + 1]
+// (h < 9), or the noisy new frame in the newest slot and in every slot of a row being (re)filled -- and
+// stored with one float4 store.  All global reads precede the first barrier, so obs may alias obs_prev.
 // Reset mode: rows with sel[e] (all if sel is NULL) are filled, the others are rewritten unchanged
 // from obs itself.  Otherwise fill[e] = fill_a[e] | fill_b[e].
 struct AsmArgs {
@@ -879,27 +880,30 @@ struct AsmArgs {
   uint32_t lo, hi;
 };
 constexpr int ASM_BLOCK = 256;
-constexpr int ASM_ROWS = 4;
+#ifndef H12_ASM_ROWS
+#define H12_ASM_ROWS 4
+#endif
+constexpr int ASM_ROWS = H12_ASM_ROWS;  // rows per block (the frame's [45][n] rows are read in 4*ROWS-byte segments)
 constexpr int ASM_F4 = ASM_ROWS * H12_NOBS / 4;
-constexpr int ASM_NOISE = 32;  // 8 Philox blocks x 4 uniforms per row (30 used)
-constexpr int ASM_RNG_T0 = 192;  // first thread of the noise wave
 static_assert((ASM_ROWS * H12_NOBS) % 4 == 0, "float4 rows");
-static_assert(ASM_ROWS * H12_OBS_FRAME <= ASM_RNG_T0 && ASM_RNG_T0 + 8 * ASM_ROWS <= ASM_BLOCK, "thread roles");
+static_assert(ASM_ROWS * 8 <= ASM_BLOCK, "one Philox block per thread");
 
 H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
+  // no short-circuit on the byte loads: both are issued together (uniform pointer checks only)
+  const int sel = A.sel ? (int)A.sel[e] : 1;
+  const int fa = A.fill_a ? (int)A.fill_a[e] : 0;
+  const int fb = A.fill_b ? (int)A.fill_b[e] : 0;
   if (A.reset_mode) {
     fill = true;
-    return !A.sel || A.sel[e];
+    return sel != 0;
   }
-  fill = (A.fill_a && A.fill_a[e]) || (A.fill_b && A.fill_b[e]);
+  fill = (fa | fb) != 0;
   return true;
 }
 
-// value of row-local obs column col (0..449): unchanged, shifted history or noisy new frame
-H12_DEV float asm_value(int row, int col, const float* s_hist, const float* s_frame, const float* s_noise,
-                        bool write, bool fill) {
-  const int p = row * H12_NOBS + col;
-  if (!write) return s_hist[p];
+// column table entry of row-local column col: frame component c (bits 0-7), history shift d (bits 8-15),
+// newest-slot flag (bit 16)
+H12_DEV uint32_t asm_col_entry(int col) {
   int c, hh, d;
   if (col < 90) {
     int t = col / 30, r = col - 30 * t;
@@ -912,16 +916,16 @@ H12_DEV float asm_value(int row, int col, const float* s_hist, const float* s_fr
     c = 9 + 12 * t + (r - 12 * hh);
     d = 12;
   }
-  if (!fill && hh < H12_NHIST - 1) return s_hist[p + d];
-  float x = s_frame[row * H12_OBS_FRAME + c];
-  int tn = noise_index(c);
-  return tn < 0 ? x : x + s_noise[row * ASM_NOISE + tn];
+  return (uint32_t)c | ((uint32_t)d << 8) | (hh == H12_NHIST - 1 ? (1u << 16) : 0u);
 }
 
+constexpr int ASM_CHUNKS = (ASM_F4 + 63) / 64;  // 1 KB LDS-DMA chunks (64 lanes x 16 B) per block
+
 __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
-  __shared__ __attribute__((aligned(16))) float s_hist[ASM_ROWS * H12_NOBS];
-  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];
-  __shared__ float s_noise[ASM_ROWS * ASM_NOISE];
+  __shared__ __attribute__((aligned(16))) float s_hist[ASM_CHUNKS * 64 * 4];
+  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];  // noisy new frames
+  __shared__ float s_noise[ASM_ROWS * 32];
+  __shared__ uint32_t s_col[H12_NOBS];
   __shared__ int s_write[ASM_ROWS], s_fill[ASM_ROWS];
   const int n = A.n;
   const int tid = threadIdx.x;
@@ -930,48 +934,88 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   const bool full = A.vec && rows == ASM_ROWS;
   const size_t base = (size_t)r0 * H12_NOBS;
   const float* src = (A.reset_mode ? A.obs : A.obs_prev) + base;
-  if (tid < ASM_ROWS) {
-    bool fill = false;
-    int w = tid < rows ? (int)asm_row_written(A, r0 + tid, fill) : 0;
-    s_write[tid] = w;
-    s_fill[tid] = fill ? 1 : 0;
-  }
+  // phase 1: all global reads (rows -> LDS, raw frames, flags), noise draws, column table
+  // every global load is issued before the first LDS write (one memory round trip per wave; indices
+  // are clamped instead of guarded so the loads stay unconditional and batched); the Philox draws run
+  // while they are in flight
+  bool fill_flag = false;
+  const int fe = r0 + min(tid, rows - 1);
+  const bool write_flag = asm_row_written(A, fe, fill_flag) && tid < rows;
+  constexpr int NFR = (ASM_ROWS * H12_OBS_FRAME + ASM_BLOCK - 1) / ASM_BLOCK;
+  float fv[NFR];
   if (full) {
-    for (int j = tid; j < ASM_F4; j += ASM_BLOCK)
-      reinterpret_cast<float4*>(s_hist)[j] = reinterpret_cast<const float4*>(src)[j];
-  } else {
-    for (int j = tid; j < rows * H12_NOBS; j += ASM_BLOCK) s_hist[j] = src[j];
+    // rows -> LDS by LDS-DMA (global_load_lds_dwordx4): no register round trip, drained at the barrier
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int ch = wave; ch < ASM_CHUNKS; ch += ASM_BLOCK / 64) {
+      const float4* g = reinterpret_cast<const float4*>(src) + min(ch * 64 + lane, ASM_F4 - 1);
+      __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(s_hist + ch * 256),
+                                       16, 0, 0);
+    }
   }
-  if (tid < rows * H12_OBS_FRAME) {
-    int row = tid / H12_OBS_FRAME, c = tid - row * H12_OBS_FRAME;
-    s_frame[tid] = A.frame[(size_t)c * n + r0 + row];
-  } else if (tid >= ASM_RNG_T0 && tid < ASM_RNG_T0 + 8 * rows) {
-    int k = tid - ASM_RNG_T0, row = k >> 3, blk = k & 7;
+#pragma unroll
+  for (int u = 0; u < NFR; ++u) {
+    int k = min(u * ASM_BLOCK + tid, ASM_ROWS * H12_OBS_FRAME - 1);
+    int c = k / ASM_ROWS, row = min(k - c * ASM_ROWS, rows - 1);  // component-major: ROWS envs per component
+    fv[u] = A.frame[(size_t)c * n + r0 + row];
+  }
+  for (int col = tid; col < H12_NOBS; col += ASM_BLOCK) s_col[col] = asm_col_entry(col);
+  if (tid < ASM_ROWS) {
+    s_write[tid] = write_flag ? 1 : 0;
+    s_fill[tid] = fill_flag ? 1 : 0;
+  }
+  if (tid < 8 * rows) {
+    int row = tid >> 3, blk = tid & 7;
     uint32_t r[4];
     philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + r0 + row), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)blk,
            A.hi, r);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       int t = 4 * blk + a;
-      s_noise[row * ASM_NOISE + t] = t < 30 ? noise_of(P, t, r[a]) : 0.f;
+      s_noise[row * 32 + t] = t < 30 ? noise_of(P, t, r[a]) : 0.f;
     }
   }
+  if (!full) {
+    for (int j = tid; j < rows * H12_NOBS; j += ASM_BLOCK) s_hist[j] = src[j];
+  }
+#pragma unroll
+  for (int u = 0; u < NFR; ++u) {
+    int k = u * ASM_BLOCK + tid;
+    int c = k / ASM_ROWS, row = k - c * ASM_ROWS;
+    if (k < ASM_ROWS * H12_OBS_FRAME) s_frame[row * H12_OBS_FRAME + c] = fv[u];
+  }
   __syncthreads();
+  // phase 2: noisy frames
+  for (int k = tid; k < ASM_ROWS * H12_OBS_FRAME; k += ASM_BLOCK) {
+    int row = k / H12_OBS_FRAME, c = k - row * H12_OBS_FRAME;
+    int tn = noise_index(c);
+    if (tn >= 0) s_frame[k] += s_noise[row * 32 + tn];
+  }
+  __syncthreads();
+  // phase 3: assemble + store (obs may alias obs_prev: every read of these rows happened in phase 1)
   float* dst = A.obs + base;
+  auto value = [&](int row, int col) -> float {
+    const uint32_t t = s_col[col];
+    const int p = row * H12_NOBS + col;
+    if (!s_write[row]) return s_hist[p];
+    if (!s_fill[row] && !(t & (1u << 16))) return s_hist[p + (int)((t >> 8) & 0xFF)];
+    return s_frame[row * H12_OBS_FRAME + (int)(t & 0xFF)];
+  };
   if (full) {
     for (int j = tid; j < ASM_F4; j += ASM_BLOCK) {
       float v[4];
+      const int p0 = 4 * j, row0 = p0 / H12_NOBS, col0 = p0 - row0 * H12_NOBS;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        int pp = 4 * j + q, row = pp / H12_NOBS, col = pp - row * H12_NOBS;
-        v[q] = asm_value(row, col, s_hist, s_frame, s_noise, s_write[row], s_fill[row]);
+        int col = col0 + q, row = row0;
+        if (col >= H12_NOBS) { col -= H12_NOBS; row += 1; }  // a float4 may straddle two rows (450 % 4 = 2)
+        v[q] = value(row, col);
       }
       reinterpret_cast<float4*>(dst)[j] = make_float4(v[0], v[1], v[2], v[3]);
     }
   } else {
     for (int pp = tid; pp < rows * H12_NOBS; pp += ASM_BLOCK) {
       int row = pp / H12_NOBS, col = pp - row * H12_NOBS;
-      if (s_write[row]) dst[pp] = asm_value(row, col, s_hist, s_frame, s_noise, true, s_fill[row]);
+      if (s_write[row]) dst[pp] = value(row, col);
     }
   }
 }
