@@ -44,6 +44,7 @@ def parse():
                    help="env: the metric (random-action rollout); train: BASELINE configs C3/C4 (PPO iterations "
                         "of the train.py runner, rollout all-gathered over RCCL when N > 1)")
     p.add_argument("--iterations", type=int, default=5, help="train mode: timed PPO iterations")
+    p.add_argument("--precision", choices=("fp32", "bf16"), default="fp32", help="train mode: learning-phase GEMM precision")
     p.add_argument("--task", choices=("flat", "rough", "c5"), default="flat",
                    help="flat: the metric's task; rough: Isaac-Velocity-Rough-H12_12dof-v0; c5: BASELINE config C5 "
                         "(rough + per-env friction / torso mass, 8192 envs unless --envs)")
@@ -113,7 +114,9 @@ def train_mode(args, world, rank, dev, torch, dist):
     cfg.sim.device = str(dev)
     env = RslRlVecEnvWrapper(H12VelocityEnv(cfg, env_offset=rank * args.envs))
     agent = H12_12dof_FlatPPORunnerCfg(device=str(dev))
-    runner = OnPolicyRunner(env, agent.to_dict(), log_dir=None, device=str(dev))
+    tcfg = agent.to_dict()
+    tcfg["algorithm"]["precision"] = args.precision
+    runner = OnPolicyRunner(env, tcfg, log_dir=None, device=str(dev))
     import io
     import contextlib
 
@@ -144,7 +147,8 @@ def train_mode(args, world, rank, dev, torch, dist):
             "metric": "PPO env-steps/sec (train.py loop, collection + learning), Velocity-Flat-H12_12dof",
             "value": steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": args.iterations,
             "warmup": max(1, args.warmup // 25), "ms_per_step": 1e3 * dt / args.iterations, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic: on-policy rollouts",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "f32 env / bf16 learner",
+            "data": "synthetic: on-policy rollouts",
             "config": {"workload": "C3/C4: PPO iterations, 24 steps/env/iter, 5 epochs x 4 minibatches, "
                                    "MLP 512-256-128", "envs_per_gpu": args.envs, "global_envs": world * args.envs,
                        "parallelism": f"env-shard x{world}" + (" + RCCL rollout all-gather + grad all-reduce"

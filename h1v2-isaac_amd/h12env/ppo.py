@@ -215,11 +215,14 @@ class PPO:
     def __init__(self, policy, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998, lam=0.95,
                  value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu",
-                 normalize_advantage_per_mini_batch=False, shard: D.Shard | None = None, **kwargs):
+                 normalize_advantage_per_mini_batch=False, shard: D.Shard | None = None, precision: str = "fp32",
+                 **kwargs):
         self.policy = policy.to(device)
         self.actor_critic = self.policy  # rsl_rl < 2.3 name
         self.device = device
-        self.optimizer = torch.optim.Adam(self.policy.parameters(), lr=learning_rate)
+        # fused Adam (one kernel for all parameters) on the GPU; plain Adam on CPU
+        fused = str(device).startswith("cuda")
+        self.optimizer = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, fused=fused)
         self.learning_rate = learning_rate
         self.num_learning_epochs = num_learning_epochs
         self.num_mini_batches = num_mini_batches
@@ -233,6 +236,11 @@ class PPO:
         self.shard = shard or D.Shard(0, 1, 0, 0)
         self.storage: RolloutStorage | None = None
         self._update_count = 0
+        # "bf16": autocast the learning-phase forward/backward GEMMs to bf16 MFMA (the reference trains with
+        # TF32 matmuls enabled on NVIDIA, train.py:70-71; gfx950 has no TF32); "fp32": exact fp32
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be fp32 or bf16, got {precision!r}")
+        self.precision = precision
 
     def init_storage(self, num_envs, num_steps, obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_steps, obs_shape[0],
@@ -297,7 +305,9 @@ class PPO:
         mb = n_total // self.num_mini_batches
         world, rank = self.shard.world, self.shard.rank
         gen = torch.Generator(device=self.device)
-        mean_value_loss = mean_surrogate_loss = mean_entropy = 0.0
+        # loss statistics stay on the device until the end of the update (one host sync per minibatch, for
+        # the KL-adaptive learning rate, instead of four)
+        stats = torch.zeros(3, device=self.device)
         n_updates = 0
         for epoch in range(self.num_learning_epochs):
             # identical permutation on every rank (shared seed per epoch); each rank takes its share
@@ -318,9 +328,14 @@ class PPO:
                 old_mu, old_sigma = b["mu"][idx], b["sigma"][idx]
                 if self.normalize_advantage_per_mini_batch:
                     advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
-                self.policy.act(obs)
+                with torch.autocast(device_type="cuda", dtype=torch.bfloat16,
+                                    enabled=self.precision == "bf16" and str(self.device).startswith("cuda")):
+                    self.policy.act(obs)
+                    value = self.policy.evaluate(critic_obs).float()
+                if self.precision == "bf16":  # distribution statistics in fp32
+                    self.policy.distribution = Normal(self.policy.distribution.mean.float(),
+                                                      self.policy.distribution.stddev.float())
                 log_prob = self.policy.get_actions_log_prob(actions)
-                value = self.policy.evaluate(critic_obs)
                 mu, sigma, entropy = self.policy.action_mean, self.policy.action_std, self.policy.entropy
                 if self.desired_kl is not None and self.schedule == "adaptive":
                     with torch.inference_mode():
@@ -354,14 +369,12 @@ class PPO:
                 self._allreduce_grads()
                 nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                 self.optimizer.step()
-                mean_value_loss += value_loss.item()
-                mean_surrogate_loss += surrogate_loss.item()
-                mean_entropy += entropy.mean().item()
+                stats += torch.stack([value_loss.detach(), surrogate_loss.detach(), entropy.mean().detach()])
                 n_updates += 1
         self._update_count += 1
         self.storage.clear()
-        return {"value_function": mean_value_loss / n_updates, "surrogate": mean_surrogate_loss / n_updates,
-                "entropy": mean_entropy / n_updates}
+        v, sl, en = (stats / n_updates).tolist()
+        return {"value_function": v, "surrogate": sl, "entropy": en}
 
     def broadcast_parameters(self):
         if self.shard.world > 1:
