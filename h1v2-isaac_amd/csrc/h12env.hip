@@ -105,6 +105,17 @@ struct KParams {
   const float* t_origin;  // [rows][cols][3]
   int t_nx, t_ny, t_rows, t_cols;
   float t_x0, t_y0, t_inv_hs;
+  // Rsl task (rsl_env_cfg.py): reward terms 12-19, deadzone commands, pushes, history / scales
+  int rsl;                // reward terms 12-19 are weighted (computed only then)
+  float cmd_T1;           // resampling_time_range upper bound
+  int dz;                 // UniformVelocityCommandWithDeadzone
+  float dz_v, flip_p;
+  int* dz_cnt;            // 3 rotating deadzone counters (handle-owned)
+  int push;               // push_by_setting_velocity interval event
+  float push_t0, push_t1, push_x0, push_x1, push_y0, push_y1;
+  int hist;               // observation history length (flat layout)
+  float oscale[6];        // per-term observation scale
+  float h_target, cf_thr;
 };
 static_assert(sizeof(KParams) < 1024, "kernarg budget");
 
@@ -114,7 +125,7 @@ struct Workspace {
   int n;
 };
 
-enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3 };
+enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3, ST_PUSH = 4 };
 
 // joint-angle sign of leg link k in the lane's frame (x / z joints flip under the y-mirror)
 H12_DEV float jsign(int k, float sg) { return AX[k] == 1 ? 1.f : sg; }
@@ -574,7 +585,7 @@ struct EnvSt {
   Base b;
   Leg lg;                         // lane frame
   float act[NL], act1[NL];        // a_t, a_{t-1} of this leg (lane frame)
-  float cmd[3], heading, cmd_time;
+  float cmd[3], heading, cmd_time, push_t;
   float air, con, last_air, last_con;  // this lane's foot
   float epsum[H12_NREW];
   int eplen, lag[3], since_reset, is_heading, is_standing;
@@ -628,7 +639,10 @@ H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvS
   s.con = ldf(W, H12_F_CONTACT + leg, e);
   s.last_air = ldf(W, H12_F_LAST_AIR + leg, e);
   s.last_con = ldf(W, H12_F_LAST_CONTACT + leg, e);
-  for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
+  for (int t = 0; t < H12_NREW_FLAT; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
+  for (int t = H12_NREW_FLAT; t < H12_NREW; ++t)
+    s.epsum[t] = (Feat<K>::ext && P.rsl) ? ldf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e) : 0.f;
+  s.push_t = (Feat<K>::ext && P.push) ? ldf(W, H12_F_PUSH_TIME, e) : 0.f;
   s.eplen = W.I[(size_t)H12_I_EPLEN * W.n + e];
   if (Feat<K>::terrain) {
     for (int i = 0; i < 3; ++i) s.origin[i] = ldf(W, H12_F_ORIGIN + i, e);
@@ -660,7 +674,10 @@ H12_DEV void store_env(const KParams& P, const Workspace& W, int e, int leg, con
     for (int i = 0; i < 3; ++i) stf(W, H12_F_CMD + i, e, s.cmd[i]);
     stf(W, H12_F_HEADING, e, s.heading);
     stf(W, H12_F_CMD_TIME, e, s.cmd_time);
-    for (int t = 0; t < H12_NREW; ++t) stf(W, H12_F_EPSUM + t, e, s.epsum[t]);
+    for (int t = 0; t < H12_NREW_FLAT; ++t) stf(W, H12_F_EPSUM + t, e, s.epsum[t]);
+    if (Feat<K>::ext && P.rsl)
+      for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) stf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e, s.epsum[t]);
+    if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
     W.I[(size_t)H12_I_EPLEN * W.n + e] = s.eplen;
   }
 #pragma unroll
@@ -708,22 +725,32 @@ H12_DEV float wrap_pi(float x) {
   return r > PI_F ? r - TWO_PI : r;
 }
 
-// UniformVelocityCommand._resample_command (upstream; in-repo twin utils/mdp/commands.py:19-59)
-H12_DEV void cmd_resample(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi) {
+// CommandTerm._resample: UniformVelocityCommand._resample_command (upstream; in-repo twin
+// utils/mdp/commands.py:19-59) + time_left ~ U(resampling_time_range).  blk: first of the two Philox blocks
+// (0: reset / time-out resample, 3: the deadzone's re-activation resample of the same step)
+H12_DEV void cmd_resample(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi, int blk = 0) {
   uint32_t r0[4], r1[4];
-  rng(P, g, lo, hi, ST_CMD, 0, r0);
-  rng(P, g, lo, hi, ST_CMD, 1, r1);
+  rng(P, g, lo, hi, ST_CMD, blk, r0);
+  rng(P, g, lo, hi, ST_CMD, blk + 1, r1);
   s.cmd[0] = uab(r0[0], P.cmd_x0, P.cmd_x1);
   s.cmd[1] = uab(r0[1], P.cmd_y0, P.cmd_y1);
   s.cmd[2] = uab(r0[2], P.cmd_w0, P.cmd_w1);
   s.heading = uab(r0[3], P.cmd_h0, P.cmd_h1);
   s.is_heading = u01(r1[0]) <= P.rel_head;
   s.is_standing = u01(r1[1]) <= P.rel_stand;
-  s.cmd_time = P.cmd_T;
+  s.cmd_time = uab(r1[2], P.cmd_T, P.cmd_T1);
 }
 
-// UniformVelocityCommand._update_command (heading control, standing envs)
-H12_DEV void cmd_update(const KParams& P, EnvSt& s) {
+// UniformVelocityCommand._update_command (heading control, standing envs), or with P.dz the Rsl/CaT
+// UniformVelocityCommandWithDeadzone._update_command (utils/mdp/commands.py:41-96): keep half of the envs
+// in the deadzone |cmd_xy| < v_dz -- with too few, each active env is zeroed with probability
+// (target - count) / (n - count); with too many, each deadzone env is resampled with probability
+// (count - target) / count -- which is the per-env marginal of the reference's randperm selection.  The
+// count is the previous step's (dz_prev; a grid-wide count of this step would need a second pass); for
+// the shipped velocity_deadzone = 0 it is 0 and the rule is exact.  Then cmd_z flips sign with
+// probability physics_dt / episode_length_s.  Standing envs are not zeroed in this class.
+template <int K>
+H12_DEV void cmd_update(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi, int dz_prev, int n) {
   if (s.is_heading) {
     float R[3][3];
     quat_R(s.b.quat, R);
@@ -731,7 +758,37 @@ H12_DEV void cmd_update(const KParams& P, EnvSt& s) {
     float w = P.head_k * wrap_pi(s.heading - hw);
     s.cmd[2] = fminf(fmaxf(w, P.cmd_w0), P.cmd_w1);
   }
+  if (Feat<K>::ext && P.dz) {
+    uint32_t r[4];
+    rng(P, g, lo, hi, ST_CMD, 2, r);
+    const int target = n / 2;
+    const bool in_dz = s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1] < P.dz_v * P.dz_v;
+    // Bernoulli(num / den) on the 24-bit uniform u: u * den < num * 2^24, exact in integers
+    const uint64_t u24 = r[0] >> 8;
+    if (dz_prev < target) {
+      if (!in_dz && u24 * (uint64_t)(n - dz_prev) < ((uint64_t)(target - dz_prev) << 24)) s.cmd[0] = s.cmd[1] = 0.f;
+    } else if (dz_prev > target) {
+      if (in_dz && u24 * (uint64_t)dz_prev < ((uint64_t)(dz_prev - target) << 24)) cmd_resample(P, s, g, lo, hi, 3);
+    }
+    if (u01(r[1]) < P.flip_p) s.cmd[2] = -s.cmd[2];
+    return;
+  }
   if (s.is_standing) s.cmd[0] = s.cmd[1] = s.cmd[2] = 0.f;
+}
+
+// push_by_setting_velocity as an interval event (EventManager.apply(mode="interval"), rsl_env_cfg.py:262-273):
+// time_left -= step_dt; at < 1e-6 a new interval is drawn and U(range) is added to the root x / y velocity
+template <int K>
+H12_DEV void push_event(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi) {
+  if (!(Feat<K>::ext && P.push)) return;
+  s.push_t -= P.step_dt;
+  if (s.push_t < 1e-6f) {
+    uint32_t r[4];
+    rng(P, g, lo, hi, ST_PUSH, 0, r);
+    s.push_t = uab(r[2], P.push_t0, P.push_t1);
+    s.b.vlin[0] += uab(r[0], P.push_x0, P.push_x1);
+    s.b.vlin[1] += uab(r[1], P.push_y0, P.push_y1);
+  }
 }
 
 // _reset_idx: scene reset (delay lags, sensors), reset events, manager resets (cat_env.py:195-248)
@@ -786,6 +843,11 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
   s.air = s.con = s.last_air = s.last_con = 0.f;
   for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = 0.f;
   s.eplen = 0;
+  if (Feat<K>::ext && P.push) {  // EventManager.reset: a new push interval for the reset envs
+    uint32_t r3[4];
+    rng(P, g, lo, hi, ST_RESET, 3, r3);
+    s.push_t = uab(r3[0], P.push_t0, P.push_t1);
+  }
   cmd_resample(P, s, g, lo, hi);
 }
 
@@ -839,17 +901,11 @@ H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, 
   }
 }
 
-// column of observation component c (0..44, frame order) in history slot hh of a 450-float row:
-// term-major blocks of 30, 30, 30, 120, 120, 120 floats (CircularBuffer order, oldest slot first)
-H12_DEV int obs_col(int c, int hh) {
-  if (c < 9) { int t = c / 3; return 30 * t + 3 * hh + (c - 3 * t); }
-  int cc = c - 9, t = cc / 12;
-  return 90 + 120 * t + 12 * hh + (cc - 12 * t);
-}
-
 // noise index of frame component c (ang_vel 0-2, gravity 3-5, joint_pos 6-17, joint_vel 18-29;
 // command and last action are noise-free: -1)
 H12_DEV int noise_index(int c) { return c < 6 ? c : (c < 9 ? -1 : (c < 33 ? c - 3 : -1)); }
+// observation term of frame component c: ang_vel 0, gravity 1, command 2, q-q0 3, qd 4, action 5
+H12_DEV int term_index(int c) { return c < 9 ? c / 3 : 3 + (c - 9) / 12; }
 
 // additive uniform noise of noise index t (ObservationTermCfg noise=Unoise(-n, n)); 0 when off
 H12_DEV float noise_of(const KParams& P, int t, uint32_t r) {
@@ -884,8 +940,7 @@ constexpr int ASM_BLOCK = 256;
 #define H12_ASM_ROWS 4
 #endif
 constexpr int ASM_ROWS = H12_ASM_ROWS;  // rows per block (the frame's [45][n] rows are read in 4*ROWS-byte segments)
-constexpr int ASM_F4 = ASM_ROWS * H12_NOBS / 4;
-static_assert((ASM_ROWS * H12_NOBS) % 4 == 0, "float4 rows");
+static_assert((ASM_ROWS * H12_OBS_FRAME) % 4 == 0, "float4 rows for every history length");
 static_assert(ASM_ROWS * 8 <= ASM_BLOCK, "one Philox block per thread");
 
 H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
@@ -901,38 +956,43 @@ H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
   return true;
 }
 
-// column table entry of row-local column col: frame component c (bits 0-7), history shift d (bits 8-15),
+// column table entry of row-local column col of a 45 x NH row (term-major blocks of 3NH, 3NH, 3NH, 12NH,
+// 12NH, 12NH floats, oldest slot first): frame component c (bits 0-7), history shift d (bits 8-15),
 // newest-slot flag (bit 16)
+template <int NH>
 H12_DEV uint32_t asm_col_entry(int col) {
   int c, hh, d;
-  if (col < 90) {
-    int t = col / 30, r = col - 30 * t;
+  if (col < 9 * NH) {
+    int t = col / (3 * NH), r = col - 3 * NH * t;
     hh = r / 3;
     c = 3 * t + (r - 3 * hh);
     d = 3;
   } else {
-    int k = col - 90, t = k / 120, r = k - 120 * t;
+    int k = col - 9 * NH, t = k / (12 * NH), r = k - 12 * NH * t;
     hh = r / 12;
     c = 9 + 12 * t + (r - 12 * hh);
     d = 12;
   }
-  return (uint32_t)c | ((uint32_t)d << 8) | (hh == H12_NHIST - 1 ? (1u << 16) : 0u);
+  return (uint32_t)c | ((uint32_t)d << 8) | (hh == NH - 1 ? (1u << 16) : 0u);
 }
 
-constexpr int ASM_CHUNKS = (ASM_F4 + 63) / 64;  // 1 KB LDS-DMA chunks (64 lanes x 16 B) per block
-
+// NH: history length (10 Flat, 6 Rsl); the row is 45 * NH floats
+template <int NH>
 __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
+  constexpr int ROW = H12_OBS_FRAME * NH;
+  constexpr int ASM_F4 = ASM_ROWS * ROW / 4;
+  constexpr int ASM_CHUNKS = (ASM_F4 + 63) / 64;  // 1 KB LDS-DMA chunks (64 lanes x 16 B) per block
   __shared__ __attribute__((aligned(16))) float s_hist[ASM_CHUNKS * 64 * 4];
-  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];  // noisy new frames
+  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];  // noisy, scaled new frames
   __shared__ float s_noise[ASM_ROWS * 32];
-  __shared__ uint32_t s_col[H12_NOBS];
+  __shared__ uint32_t s_col[ROW];
   __shared__ int s_write[ASM_ROWS], s_fill[ASM_ROWS];
   const int n = A.n;
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * ASM_ROWS;
   const int rows = min(ASM_ROWS, n - r0);
   const bool full = A.vec && rows == ASM_ROWS;
-  const size_t base = (size_t)r0 * H12_NOBS;
+  const size_t base = (size_t)r0 * ROW;
   const float* src = (A.reset_mode ? A.obs : A.obs_prev) + base;
   // phase 1: all global reads (rows -> LDS, raw frames, flags), noise draws, column table
   // every global load is issued before the first LDS write (one memory round trip per wave; indices
@@ -958,7 +1018,7 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
     int c = k / ASM_ROWS, row = min(k - c * ASM_ROWS, rows - 1);  // component-major: ROWS envs per component
     fv[u] = A.frame[(size_t)c * n + r0 + row];
   }
-  for (int col = tid; col < H12_NOBS; col += ASM_BLOCK) s_col[col] = asm_col_entry(col);
+  for (int col = tid; col < ROW; col += ASM_BLOCK) s_col[col] = asm_col_entry<NH>(col);
   if (tid < ASM_ROWS) {
     s_write[tid] = write_flag ? 1 : 0;
     s_fill[tid] = fill_flag ? 1 : 0;
@@ -975,7 +1035,7 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
     }
   }
   if (!full) {
-    for (int j = tid; j < rows * H12_NOBS; j += ASM_BLOCK) s_hist[j] = src[j];
+    for (int j = tid; j < rows * ROW; j += ASM_BLOCK) s_hist[j] = src[j];
   }
 #pragma unroll
   for (int u = 0; u < NFR; ++u) {
@@ -984,18 +1044,20 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
     if (k < ASM_ROWS * H12_OBS_FRAME) s_frame[row * H12_OBS_FRAME + c] = fv[u];
   }
   __syncthreads();
-  // phase 2: noisy frames
+  // phase 2: noisy frames, then the term scale (ObservationManager: noise, clip, scale)
   for (int k = tid; k < ASM_ROWS * H12_OBS_FRAME; k += ASM_BLOCK) {
     int row = k / H12_OBS_FRAME, c = k - row * H12_OBS_FRAME;
     int tn = noise_index(c);
-    if (tn >= 0) s_frame[k] += s_noise[row * 32 + tn];
+    float v = s_frame[k];
+    if (tn >= 0) v += s_noise[row * 32 + tn];
+    s_frame[k] = v * P.oscale[term_index(c)];
   }
   __syncthreads();
   // phase 3: assemble + store (obs may alias obs_prev: every read of these rows happened in phase 1)
   float* dst = A.obs + base;
   auto value = [&](int row, int col) -> float {
     const uint32_t t = s_col[col];
-    const int p = row * H12_NOBS + col;
+    const int p = row * ROW + col;
     if (!s_write[row]) return s_hist[p];
     if (!s_fill[row] && !(t & (1u << 16))) return s_hist[p + (int)((t >> 8) & 0xFF)];
     return s_frame[row * H12_OBS_FRAME + (int)(t & 0xFF)];
@@ -1003,18 +1065,18 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   if (full) {
     for (int j = tid; j < ASM_F4; j += ASM_BLOCK) {
       float v[4];
-      const int p0 = 4 * j, row0 = p0 / H12_NOBS, col0 = p0 - row0 * H12_NOBS;
+      const int p0 = 4 * j, row0 = p0 / ROW, col0 = p0 - row0 * ROW;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         int col = col0 + q, row = row0;
-        if (col >= H12_NOBS) { col -= H12_NOBS; row += 1; }  // a float4 may straddle two rows (450 % 4 = 2)
+        if (col >= ROW) { col -= ROW; row += 1; }  // a float4 may straddle two rows (450 % 4 = 2)
         v[q] = value(row, col);
       }
       reinterpret_cast<float4*>(dst)[j] = make_float4(v[0], v[1], v[2], v[3]);
     }
   } else {
-    for (int pp = tid; pp < rows * H12_NOBS; pp += ASM_BLOCK) {
-      int row = pp / H12_NOBS, col = pp - row * H12_NOBS;
+    for (int pp = tid; pp < rows * ROW; pp += ASM_BLOCK) {
+      int row = pp / ROW, col = pp - row * ROW;
       if (s_write[row]) dst[pp] = value(row, col);
     }
   }
@@ -1080,6 +1142,7 @@ struct StepArgs {
   int64_t env_offset;
   uint32_t lo, hi;
   int n_substeps;
+  int dz_slot;  // deadzone counter read this step (P.dz_cnt[dz_slot]); +1 is counted into, +2 zeroed
 };
 
 template <int K>
@@ -1092,6 +1155,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   const bool active = e < W.n;
   const uint32_t g = (uint32_t)(A.env_offset + e);
   PH_INIT();
+  if (Feat<K>::ext && P.dz && blockIdx.x == 0 && threadIdx.x == 0) P.dz_cnt[(A.dz_slot + 2) % 3] = 0;
   if (active) {
     EnvSt s;
     load_phys<K>(P, W, e, leg, s);
@@ -1245,9 +1309,36 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       terms[H12_R_FEET_SLIDE] = psum(fs);
     }
     terms[H12_R_JOINT_DEV_HIP] = psum(sd_);
+    // terms of the Rsl table (rsl_env_cfg.py:279-407), base-frame tracking and the extra penalties
+    constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+    if (Feat<K>::ext) {
+      for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) terms[t] = 0.f;
+      if (P.rsl) {
+        float vb[3];
+        mtv(R, vcom, vb);  // root_lin_vel_b (composite COM velocity in the base frame)
+        float bx = s.cmd[0] - vb[0], by = s.cmd[1] - vb[1], bw = s.cmd[2] - s.b.wang[2];
+        terms[H12_R_TRACK_LIN_VEL_XY_BASE] = __expf(-(bx * bx + by * by) * P.std2_inv);
+        terms[H12_R_TRACK_ANG_VEL_Z_BASE] = __expf(-(bw * bw) * P.std2_inv);
+        float dh = s.b.pos[2] - P.h_target;
+        terms[H12_R_BASE_HEIGHT_L2] = dh * dh;
+        float sv_ = 0.f, sh_ = 0.f;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) sv_ += s.lg.qd[k] * s.lg.qd[k];
+#pragma unroll
+        for (int k = 0; k < 3; k += 2) {  // hip yaw (0), hip roll (2) soft limits
+          float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
+          sh_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
+        }
+        terms[H12_R_JOINT_VEL_L2] = psum(sv_);
+        terms[H12_R_JOINT_DEV_ANKLE] = psum(fabsf(s.lg.q[4] - h12m::Q0[4]) + fabsf(s.lg.q[5] - h12m::Q0[5]));
+        terms[H12_R_DOF_POS_LIMITS_HIP] = psum(sh_);
+        terms[H12_R_CONTACT_FORCES] = psum(fmaxf(fmax_foot - P.cf_thr, 0.f));
+        terms[H12_R_LIN_VEL_Z_L2] = vb[2] * vb[2];
+      }
+    }
     float r = 0.f;
 #pragma unroll
-    for (int t = 0; t < H12_NREW; ++t) {
+    for (int t = 0; t < NT; ++t) {
       float v = terms[t] * P.rew_w[t] * P.step_dt;
       r += v;
       s.epsum[t] += v;
@@ -1264,10 +1355,10 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
     // ---- episode log: the (few) resetting envs add their sums directly (no-return atomics)
     if (A.log_acc && reset && leg == 0) {
-      for (int t = 0; t < H12_NREW; ++t) atomicAdd(&A.log_acc[t], s.epsum[t]);
-      atomicAdd(&A.log_acc[12], 1.f);
-      if (tout) atomicAdd(&A.log_acc[13], 1.f);
-      if (term) atomicAdd(&A.log_acc[14], 1.f);
+      for (int t = 0; t < NT; ++t) atomicAdd(&A.log_acc[t], s.epsum[t]);
+      atomicAdd(&A.log_acc[H12_NREW], 1.f);
+      if (tout) atomicAdd(&A.log_acc[H12_NREW + 1], 1.f);
+      if (term) atomicAdd(&A.log_acc[H12_NREW + 2], 1.f);
     }
     PH(4);
     if (reset) env_reset<K>(P, s, leg, g, A.lo, A.hi);
@@ -1275,7 +1366,15 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     // ---- CommandTerm.compute(step_dt)
     s.cmd_time -= P.step_dt;
     if (s.cmd_time <= 0.f) cmd_resample(P, s, g, A.lo, A.hi);
-    cmd_update(P, s);
+    if (Feat<K>::ext && P.dz) {
+      cmd_update<K>(P, s, g, A.lo, A.hi, P.dz_cnt[A.dz_slot], W.n);
+      if (leg == 0 && s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1] < P.dz_v * P.dz_v)
+        atomicAdd(&P.dz_cnt[(A.dz_slot + 1) % 3], 1);
+    } else {
+      cmd_update<K>(P, s, g, A.lo, A.hi, 0, W.n);
+    }
+    // ---- interval events
+    push_event<K>(P, s, g, A.lo, A.hi);
     // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
     PH(5);
     obs_frame<K>(P, s, leg, e, W.n, A.frame);
@@ -1351,6 +1450,8 @@ struct Handle {
   uint64_t reset_calls, observe_calls;
   double flops_per_env;
   float* frame;  // [45][n] observation frame scratch between the env kernels and obs_assemble_kernel
+  int* dz_cnt = nullptr;  // 3 rotating deadzone counters (UniformVelocityCommandWithDeadzone)
+  uint64_t dz_step = 0;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 3 per timed step: before env kernel, between, after assembly
   size_t n_timed = 0;
@@ -1472,6 +1573,30 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.scan_res = c->scan_resolution;
   P.terrain_size = c->terrain_size;
   P.ep_len_s = (float)c->max_episode_length * P.step_dt;
+  // Rsl task
+  if (!(c->cmd_resample_time_max >= c->cmd_resample_time))
+    return set_err(H12_E_ARG, "cmd_resample_time_max must be >= cmd_resample_time");
+  P.cmd_T1 = c->cmd_resample_time_max;
+  P.rsl = 0;
+  for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) P.rsl |= c->rew_w[t] != 0.f;
+  P.dz = c->cmd_deadzone;
+  P.dz_v = c->velocity_deadzone;
+  P.flip_p = c->ang_flip_prob;
+  P.push = c->push_enable;
+  if (P.push && !(c->push_interval[1] >= c->push_interval[0] && c->push_interval[0] > 0))
+    return set_err(H12_E_ARG, "push_interval must be 0 < lo <= hi");
+  P.push_t0 = c->push_interval[0]; P.push_t1 = c->push_interval[1];
+  P.push_x0 = c->push_vel_x[0]; P.push_x1 = c->push_vel_x[1];
+  P.push_y0 = c->push_vel_y[0]; P.push_y1 = c->push_vel_y[1];
+  if (c->task == H12_TASK_FLAT && (c->history_length < 1 || c->history_length > H12_NHIST))
+    return set_err(H12_E_ARG, "history_length %d out of 1..%d", c->history_length, H12_NHIST);
+  P.hist = c->task == H12_TASK_FLAT ? c->history_length : 1;
+  for (int t = 0; t < 6; ++t) P.oscale[t] = c->obs_scale[t];
+  if (c->task == H12_TASK_ROUGH)
+    for (int t = 0; t < 6; ++t)
+      if (c->obs_scale[t] != 1.f) return set_err(H12_E_ARG, "observation scales need the flat layout");
+  P.h_target = c->base_height_target;
+  P.cf_thr = c->contact_force_threshold;
   return 0;
 }
 
@@ -1480,7 +1605,7 @@ int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_
 // feature level of the env kernels (Feat<K>)
 int feature_level(const KParams& P) {
   if (P.terrain) return 2;
-  return (P.task != H12_TASK_FLAT || P.env_mu || P.env_mass || P.curriculum) ? 1 : 0;
+  return (P.task != H12_TASK_FLAT || P.env_mu || P.env_mass || P.curriculum || P.rsl || P.dz || P.push) ? 1 : 0;
 }
 #define LAUNCH_K(KERNEL, ...)                                                   \
   do {                                                                          \
@@ -1515,7 +1640,14 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   const float* src = reset_mode ? obs : obs_prev;
   A.vec = (((uintptr_t)obs | (uintptr_t)src) & 15u) == 0;
   const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
-  hipLaunchKernelGGL(obs_assemble_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A);
+#define H12_ASM_CASE(NH) \
+  case NH: hipLaunchKernelGGL(obs_assemble_kernel<NH>, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A); break;
+  switch (h->P.hist) {
+    H12_ASM_CASE(1) H12_ASM_CASE(2) H12_ASM_CASE(3) H12_ASM_CASE(4) H12_ASM_CASE(5)
+    H12_ASM_CASE(6) H12_ASM_CASE(7) H12_ASM_CASE(8) H12_ASM_CASE(9) H12_ASM_CASE(10)
+    default: return set_err(H12_E_ARG, "history_length %d out of 1..%d", h->P.hist, H12_NHIST);
+  }
+#undef H12_ASM_CASE
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -1566,14 +1698,23 @@ int h12env_config_default(h12env_config* c) {
   c->reset_yaw[0] = -3.14f; c->reset_yaw[1] = 3.14f;
   c->enable_corruption = 1;
   c->noise_ang_vel = 0.2f; c->noise_gravity = 0.05f; c->noise_joint_pos = 0.01f; c->noise_joint_vel = 1.5f;
-  const float w[H12_NREW] = {1.0f, 1.0f, -0.05f, -2e-6f, -1e-7f, -0.005f, 0.75f, -1.0f, -1.0f, -200.f, -0.25f, -0.2f};
-  for (int t = 0; t < H12_NREW; ++t) c->rew_w[t] = w[t];
+  const float w[H12_NREW_FLAT] = {1.0f, 1.0f, -0.05f, -2e-6f, -1e-7f, -0.005f, 0.75f, -1.0f, -1.0f, -200.f, -0.25f, -0.2f};
+  for (int t = 0; t < H12_NREW; ++t) c->rew_w[t] = t < H12_NREW_FLAT ? w[t] : 0.f;
   c->track_std = 0.5f; c->air_time_threshold = 0.4f; c->soft_limit_factor = 0.9f;
   c->illegal_contact_knees = 1; c->illegal_contact_torso = 1;
   c->seed = 42;
   c->task = H12_TASK_FLAT;
   c->noise_lin_vel = 0.1f; c->noise_height_scan = 0.1f;
   c->scan_offset = 0.5f; c->scan_clip = 1.f; c->scan_resolution = 0.1f; c->terrain_size = 8.f;
+  c->cmd_resample_time_max = c->cmd_resample_time;
+  c->cmd_deadzone = 0; c->velocity_deadzone = 0.f; c->ang_flip_prob = 0.f;
+  c->push_enable = 0;
+  c->push_interval[0] = 5.f; c->push_interval[1] = 8.f;
+  c->push_vel_x[0] = -1.f; c->push_vel_x[1] = 1.f; c->push_vel_y[0] = -1.f; c->push_vel_y[1] = 1.f;
+  c->history_length = H12_NHIST;
+  for (int t = 0; t < 6; ++t) c->obs_scale[t] = 1.f;
+  c->base_height_target = 1.f;
+  c->contact_force_threshold = 800.f;
   return 0;
 }
 
@@ -1633,6 +1774,15 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     delete h;
     return set_err(H12_E_ALLOC, "hipMalloc(frame): %s", hipGetErrorString(e));
   }
+  e = hipMalloc(&h->dz_cnt, 3 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(h->dz_cnt, 0, 3 * sizeof(int));
+  if (e != hipSuccess) {
+    if (h->own) (void)hipFree(state_dev);
+    (void)hipFree(h->frame);
+    delete h;
+    return set_err(H12_E_ALLOC, "hipMalloc(dz_cnt): %s", hipGetErrorString(e));
+  }
+  h->P.dz_cnt = h->dz_cnt;
   h->device = device;
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -1650,6 +1800,7 @@ void h12env_destroy(h12env* hh) {
   if (!h) return;
   if (h->own && h->W.F) (void)hipFree(h->W.F);
   if (h->frame) (void)hipFree(h->frame);
+  if (h->dz_cnt) (void)hipFree(h->dz_cnt);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   delete h;
 }
@@ -1695,6 +1846,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.lo = (uint32_t)step_index;
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   A.frame = h->frame;
+  A.dz_slot = (int)(h->dz_step++ % 3);
   timing_mark(h, 0, (hipStream_t)stream);
   LAUNCH_K(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
@@ -1762,6 +1914,25 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 
 int h12env_num_envs(const h12env* hh) { return hh ? ((const Handle*)hh)->W.n : -1; }
 
+int h12env_obs_dim(const h12env* hh) {
+  if (!hh) return set_err(H12_E_ARG, "null handle");
+  const KParams& P = ((const Handle*)hh)->P;
+  return P.task == H12_TASK_ROUGH ? H12_NOBS_ROUGH : H12_OBS_FRAME * P.hist;
+}
+
+int h12env_set_reward_weights(h12env* hh, const float* w, int n) {
+  Handle* h = (Handle*)hh;
+  if (!h || !w) return set_err(H12_E_ARG, "null argument");
+  if (n < 0 || n > H12_NREW) return set_err(H12_E_ARG, "n must be in 0..%d (got %d)", H12_NREW, n);
+  int rsl = 0;
+  for (int t = 0; t < H12_NREW; ++t) rsl |= (t < n ? w[t] : h->P.rew_w[t]) != 0.f && t >= H12_NREW_FLAT;
+  // terms 12-19 are computed by the extended kernel only, and their episode sums live in fields that
+  // kernel keeps: switching them on mid-run is a different kernel configuration (recreate the handle)
+  if (rsl && !h->P.rsl) return set_err(H12_E_STATE, "reward terms 12-19 were off at creation; recreate the env");
+  for (int t = 0; t < n; ++t) h->P.rew_w[t] = w[t];
+  return 0;
+}
+
 int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, double* flops_per_env) {
   const Handle* h = (const Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
@@ -1771,7 +1942,8 @@ int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, doub
   if (kernel == 0) {
     // state fields the kernel reads and writes, actions, reward / terminated / truncated, applied torque
     // and foot force (the ArticulationData / ContactSensor views), the noise-free frame
-    double fields = 104.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0);
+    double fields = 104.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0) +
+                    (P.rsl ? 8.0 : 0.0) + (P.push ? 1.0 : 0.0);
     bytes = fields * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 + (double)H12_NJ * 4.0 + 2.0 * 4.0 +
             (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
     flops = h->flops_per_env;
@@ -1781,9 +1953,10 @@ int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, doub
       bytes = (double)FRAME_ROWS * 4.0 + (double)H12_NSCAN * 4.0 + (double)H12_NOBS_ROUGH * 4.0;
       flops = 55.0 * 10.0 * 6.0 + (double)H12_NSCAN * 20.0;
     } else {
-      // 9 old frames + the new frame + the two reset flags read, 10 frames written
-      bytes = (double)(H12_NOBS - H12_OBS_FRAME) * 4.0 + (double)H12_OBS_FRAME * 4.0 + 2.0 + (double)H12_NOBS * 4.0;
-      flops = 30.0 * 3.0 + 8.0 * 10.0 * 6.0;  // noise affine + Philox rounds
+      // H-1 old frames + the new frame + the two reset flags read, H frames written (H = 10 Flat, 6 Rsl)
+      const double row = (double)H12_OBS_FRAME * P.hist;
+      bytes = (row - H12_OBS_FRAME) * 4.0 + (double)H12_OBS_FRAME * 4.0 + 2.0 + row * 4.0;
+      flops = 30.0 * 3.0 + 45.0 + 8.0 * 10.0 * 6.0;  // noise affine + scale + Philox rounds
     }
   } else {
     return set_err(H12_E_ARG, "kernel must be 0 or 1 (got %d)", kernel);

@@ -14,9 +14,10 @@ NHIST = 10
 OBS_FRAME = 45
 NOBS = OBS_FRAME * NHIST
 NFOOT_PTS = 4
-NREW = 12
-NLOG = 16
-ABI_VERSION = 2
+NREW = 20        # reward terms the kernel implements (REWARD_FUNCS)
+NREW_FLAT = 12   # terms 0-11: the Flat / Rough tables
+NLOG = 24        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare
+ABI_VERSION = 3
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -31,16 +32,26 @@ NOBS_ROUGH = ROUGH_FRAME + NSCAN
 F = dict(POS=(0, 3), QUAT=(3, 4), VLIN=(7, 3), WANG=(10, 3), Q=(13, 12), QD=(25, 12), ACT=(37, 12),
          ACT_PREV=(49, 12), CMD=(61, 3), HEADING=(64, 1), CMD_TIME=(65, 1), AIR=(66, 2), CONTACT=(68, 2),
          LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16), ORIGIN=(102, 3), MU=(105, 4),
-         DMASS=(109, 1))
-NF_FLOAT = 110
+         DMASS=(109, 1), EPSUM2=(110, 8), PUSH_TIME=(118, 1))
+NF_FLOAT = 119
 I = dict(EPLEN=(0, 1), PACK=(1, 1), TERRAIN=(2, 1))
 NF_INT = 3
 
+# the Flat task's reward term names, in RewardManager order (kernel ids 0-11)
 REWARD_TERMS = [
     "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "ang_vel_xy_l2", "dof_torques_l2", "dof_acc_l2",
     "action_rate_l2", "feet_air_time", "flat_orientation_l2", "dof_pos_limits", "termination_penalty",
     "feet_slide", "joint_deviation_hip",
 ]
+# kernel reward ids (H12_R_*): the isaaclab mdp function each computes, with its joint / frame variant
+REWARD_FUNCS = [
+    "track_lin_vel_xy_yaw_frame_exp", "track_ang_vel_z_world_exp", "ang_vel_xy_l2", "joint_torques_l2",
+    "joint_acc_l2", "action_rate_l2", "feet_air_time_positive_biped", "flat_orientation_l2",
+    "joint_pos_limits:ankle", "is_terminated", "feet_slide", "joint_deviation_l1:hip",
+    "track_lin_vel_xy_exp", "track_ang_vel_z_exp", "base_height_l2", "joint_vel_l2", "joint_deviation_l1:ankle",
+    "joint_pos_limits:hip", "contact_forces", "lin_vel_z_l2",
+]
+assert len(REWARD_FUNCS) == NREW
 
 f32 = C.c_float
 i32 = C.c_int32
@@ -138,6 +149,18 @@ class H12Config(C.Structure):
         ("scan_clip", f32),
         ("scan_resolution", f32),
         ("terrain_size", f32),
+        ("cmd_resample_time_max", f32),
+        ("cmd_deadzone", i32),
+        ("velocity_deadzone", f32),
+        ("ang_flip_prob", f32),
+        ("push_enable", i32),
+        ("push_interval", f32 * 2),
+        ("push_vel_x", f32 * 2),
+        ("push_vel_y", f32 * 2),
+        ("history_length", i32),
+        ("obs_scale", f32 * 6),
+        ("base_height_target", f32),
+        ("contact_force_threshold", f32),
     ]
 
 
@@ -203,6 +226,10 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_field_ptr.restype = vp
     lib.h12env_num_envs.argtypes = [vp]
     lib.h12env_num_envs.restype = C.c_int
+    lib.h12env_obs_dim.argtypes = [vp]
+    lib.h12env_obs_dim.restype = C.c_int
+    lib.h12env_set_reward_weights.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    lib.h12env_set_reward_weights.restype = C.c_int
     lib.h12env_step_cost.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.h12env_step_cost.restype = C.c_int
     lib.h12env_kernel_cost.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -237,5 +264,6 @@ EXPORTED_SYMBOLS = [
     "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
-    "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain",
+    "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
+    "h12env_set_reward_weights",
 ]

@@ -19,7 +19,8 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass, field, replace
 
-from ._abi import ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NJ, NREW, REWARD_TERMS, TASK_FLAT, TASK_ROUGH, H12Config
+from ._abi import (ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NHIST, NJ, NREW, REWARD_FUNCS, REWARD_TERMS, TASK_FLAT,
+                   TASK_ROUGH, H12Config)
 from .model import DEFAULT_JOINT_POS
 
 
@@ -143,6 +144,13 @@ class UniformVelocityCommandCfg:
 
 
 @dataclass
+class UniformVelocityCommandWithDeadzoneCfg(UniformVelocityCommandCfg):
+    """biped_tasks/utils/mdp/commands.py:99-104: half of the envs kept in |cmd_xy| < velocity_deadzone,
+    random cmd_z sign flips, no standing-env zeroing (the kernel's deadzone command mode)."""
+    velocity_deadzone: float = 0.1
+
+
+@dataclass
 class CommandsCfg:
     base_velocity: UniformVelocityCommandCfg = field(default_factory=UniformVelocityCommandCfg)
 
@@ -169,6 +177,8 @@ class PolicyObsCfg:
     height_scan: Unoise | None = None
     height_scan_clip: tuple = (-1.0, 1.0)
     height_scan_offset: float = 0.5
+    # ObsTerm(scale=...) per term (applied after noise); missing terms are unscaled
+    scales: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -178,29 +188,60 @@ class ObservationsCfg:
 
 @dataclass
 class RewTerm:
+    """RewardTermCfg: weight, params and `func` -- the kernel term it maps to (one of _abi.REWARD_FUNCS: the
+    isaaclab mdp function, qualified by its joint set / frame where the kernel hard-codes one)."""
     weight: float
     params: dict = field(default_factory=dict)
+    func: str | None = None
+
+
+_FLAT_FUNCS = dict(zip(REWARD_TERMS, REWARD_FUNCS[:len(REWARD_TERMS)]))
 
 
 def _rewards():
+    T = RewTerm
     return {
-        "track_lin_vel_xy_exp": RewTerm(1.0, {"command_name": "base_velocity", "std": 0.5}),
-        "track_ang_vel_z_exp": RewTerm(1.0, {"command_name": "base_velocity", "std": 0.5}),
-        "ang_vel_xy_l2": RewTerm(-0.05),
-        "dof_torques_l2": RewTerm(-2.0e-6),
-        "dof_acc_l2": RewTerm(-1.0e-7),
-        "action_rate_l2": RewTerm(-0.005),
-        "feet_air_time": RewTerm(0.75, {"command_name": "base_velocity", "threshold": 0.4}),
-        "flat_orientation_l2": RewTerm(-1.0),
-        "dof_pos_limits": RewTerm(-1.0),
-        "termination_penalty": RewTerm(-200.0),
-        "feet_slide": RewTerm(-0.25),
-        "joint_deviation_hip": RewTerm(-0.2),
+        "track_lin_vel_xy_exp": T(1.0, {"command_name": "base_velocity", "std": 0.5}, "track_lin_vel_xy_yaw_frame_exp"),
+        "track_ang_vel_z_exp": T(1.0, {"command_name": "base_velocity", "std": 0.5}, "track_ang_vel_z_world_exp"),
+        "ang_vel_xy_l2": T(-0.05, {}, "ang_vel_xy_l2"),
+        "dof_torques_l2": T(-2.0e-6, {}, "joint_torques_l2"),
+        "dof_acc_l2": T(-1.0e-7, {}, "joint_acc_l2"),
+        "action_rate_l2": T(-0.005, {}, "action_rate_l2"),
+        "feet_air_time": T(0.75, {"command_name": "base_velocity", "threshold": 0.4}, "feet_air_time_positive_biped"),
+        "flat_orientation_l2": T(-1.0, {}, "flat_orientation_l2"),
+        "dof_pos_limits": T(-1.0, {}, "joint_pos_limits:ankle"),
+        "termination_penalty": T(-200.0, {}, "is_terminated"),
+        "feet_slide": T(-0.25, {}, "feet_slide"),
+        "joint_deviation_hip": T(-0.2, {}, "joint_deviation_l1:hip"),
+    }
+
+
+def _rsl_rewards():
+    """rsl_env_cfg.py:279-407, in its RewardManager order."""
+    T = RewTerm
+    return {
+        "track_lin_vel_xy_exp": T(1.0, {"command_name": "base_velocity", "std": 0.5}, "track_lin_vel_xy_exp"),
+        "track_ang_vel_z_exp": T(0.5, {"command_name": "base_velocity", "std": 0.5}, "track_ang_vel_z_exp"),
+        "feet_air_time": T(0.75, {"command_name": "base_velocity", "threshold": 0.4}, "feet_air_time_positive_biped"),
+        "feet_slide": T(-0.25, {}, "feet_slide"),
+        "flat_orientation": T(-1.0, {}, "flat_orientation_l2"),
+        "base_height_l2": T(-0.2, {"target_height": 1.0}, "base_height_l2"),
+        "joint_torques_l2": T(-1.0e-5, {}, "joint_torques_l2"),
+        "joint_vel_l2": T(-1.0e-3, {}, "joint_vel_l2"),
+        "dof_acc_l2": T(-1.0e-7, {}, "joint_acc_l2"),
+        "joint_deviation_hip": T(-0.2, {}, "joint_deviation_l1:hip"),
+        "joint_deviation_ankle": T(-0.2, {}, "joint_deviation_l1:ankle"),
+        "joint_pos_limits_ankle": T(-0.2, {}, "joint_pos_limits:ankle"),
+        "joint_pos_limits_hip": T(-0.2, {}, "joint_pos_limits:hip"),
+        "action_rate_l2": T(-0.01, {}, "action_rate_l2"),
+        "contact_forces": T(-1.0e-3, {"threshold": 800.0}, "contact_forces"),
+        "termination_penalty": T(-200.0, {}, "is_terminated"),
     }
 
 
 class RewardsCfg:
-    """Attribute-access container keeping RewardManager term order (REWARD_TERMS)."""
+    """Attribute-access container keeping the cfg's RewardManager term order.  A term set to None is
+    removed (as in IsaacLab); a new RewTerm must name the kernel term it maps to (`func`)."""
 
     def __init__(self, terms=None):
         object.__setattr__(self, "_terms", terms or _rewards())
@@ -220,15 +261,34 @@ class RewardsCfg:
         object.__setattr__(self, "_terms", st["_terms"])
 
     def __setattr__(self, name, value):
-        if name not in self._terms:
-            raise AttributeError(f"unknown reward term {name!r} (the HIP kernel implements {REWARD_TERMS})")
+        if value is not None:
+            if not isinstance(value, RewTerm):
+                raise TypeError(f"reward term {name!r} must be a RewTerm or None")
+            func = value.func or (self._terms[name].func if self._terms.get(name) is not None else _FLAT_FUNCS.get(name))
+            if func not in REWARD_FUNCS:
+                raise AttributeError(f"reward term {name!r}: func {func!r} is not a kernel term {REWARD_FUNCS}")
+            value.func = func
         self._terms[name] = value
 
     def items(self):
-        return [(k, self._terms[k]) for k in REWARD_TERMS]
+        return list(self._terms.items())
+
+    def active(self):
+        """(name, kernel id) of the terms the RewardManager holds (None terms removed), in cfg order."""
+        out, seen = [], {}
+        for k, v in self._terms.items():
+            if v is None:
+                continue
+            kid = REWARD_FUNCS.index(v.func)
+            if kid in seen:
+                raise ValueError(f"reward terms {seen[kid]!r} and {k!r} map to the same kernel term {v.func!r}")
+            seen[kid] = k
+            out.append((k, kid))
+        return out
 
     def to_dict(self):
-        return {k: {"weight": v.weight, "params": dict(v.params)} for k, v in self.items()}
+        return {k: (None if v is None else {"weight": v.weight, "params": dict(v.params), "func": v.func})
+                for k, v in self.items()}
 
 
 @dataclass
@@ -241,10 +301,17 @@ class TerminationsCfg:
 
 
 @dataclass
+class PushEventCfg:
+    """push_by_setting_velocity, mode "interval" (rsl_env_cfg.py:262-273)."""
+    interval_range_s: tuple = (5.0, 8.0)
+    velocity_range: dict = field(default_factory=lambda: {"x": (-1.0, 1.0), "y": (-1.0, 1.0)})
+
+
+@dataclass
 class EventsCfg:
     reset_base_pose_range: dict = field(default_factory=lambda: {"x": (-0.5, 0.5), "y": (-0.5, 0.5), "yaw": (-3.14, 3.14)})
     reset_joints_position_range: tuple = (1.0, 1.0)
-    push_robot: None = None
+    push_robot: "PushEventCfg | None" = None
     # startup randomisation (randomize_rigid_body_material / _mass, velocity_env_cfg.py:146-166,
     # cat_env_cfg.py:231-249); None = the constant material of the Flat task / no added mass
     physics_material: "MaterialEventCfg | None" = None
@@ -266,8 +333,18 @@ class MassEventCfg:
 
 
 @dataclass
+class RewardWeightTerm:
+    """modify_reward_weight (isaaclab mdp.curriculums): once common_step_counter > num_steps, the
+    reward term's weight becomes `weight`."""
+    term_name: str
+    weight: float
+    num_steps: int
+
+
+@dataclass
 class CurriculumCfg:
     terrain_levels: bool = False  # terrain_levels_vel (velocity_env_cfg.py:271-275)
+    reward_weights: list = field(default_factory=list)  # [RewardWeightTerm] (rsl_env_cfg.py:448-501)
 
 
 @dataclass
@@ -346,9 +423,11 @@ class H12FlatEnvCfg:
         c.limit_k, c.limit_c = s.limit_k, s.limit_c
         c.contact_threshold = self.terminations.base_contact_threshold
         bv = self.commands.base_velocity
-        c.cmd_resample_time = bv.resampling_time_range[0]
-        if bv.resampling_time_range[0] != bv.resampling_time_range[1]:
-            raise ValueError("only a constant resampling time is supported")
+        c.cmd_resample_time, c.cmd_resample_time_max = bv.resampling_time_range
+        if isinstance(bv, UniformVelocityCommandWithDeadzoneCfg):
+            c.cmd_deadzone = 1
+            c.velocity_deadzone = bv.velocity_deadzone
+            c.ang_flip_prob = self.sim.dt / self.episode_length_s   # commands.py:86-87: physics_dt / episode s
         r = bv.ranges
         c.cmd_lin_x[:] = r.lin_vel_x
         c.cmd_lin_y[:] = r.lin_vel_y
@@ -363,8 +442,15 @@ class H12FlatEnvCfg:
         c.reset_yaw[:] = pr["yaw"]
         po = self.observations.policy
         c.task = self.task
-        if c.task == TASK_FLAT and po.history_length != 10:
-            raise ValueError("the flat kernel's observation history is fixed at 10 frames")
+        c.history_length = max(1, int(po.history_length or 0))
+        if c.task == TASK_FLAT and c.history_length > NHIST:
+            raise ValueError(f"observation history is at most {NHIST} frames")
+        for i, k in enumerate(("base_ang_vel", "projected_gravity", "velocity_commands", "joint_pos", "joint_vel",
+                               "actions")):
+            c.obs_scale[i] = float(po.scales.get(k, 1.0))
+        if set(po.scales) - {"base_ang_vel", "projected_gravity", "velocity_commands", "joint_pos", "joint_vel",
+                             "actions"}:
+            raise ValueError(f"observation scales for unsupported terms: {sorted(po.scales)}")
         if c.task == TASK_ROUGH:
             if po.history_length not in (0, 1, None):
                 raise ValueError("the rough observation has no history (history_length 0)")
@@ -393,15 +479,42 @@ class H12FlatEnvCfg:
         c.noise_gravity = po.projected_gravity.n_max
         c.noise_joint_pos = po.joint_pos.n_max
         c.noise_joint_vel = po.joint_vel.n_max
-        for t, (name, term) in enumerate(self.rewards.items()):
-            c.rew_w[t] = 0.0 if term is None else term.weight
-        c.track_std = self.rewards.track_lin_vel_xy_exp.params.get("std", 0.5)
-        c.air_time_threshold = self.rewards.feet_air_time.params.get("threshold", 0.4)
+        terms = dict(self.rewards.items())
+        for t in range(NREW):
+            c.rew_w[t] = 0.0
+        stds = set()
+        c.track_std, c.air_time_threshold, c.base_height_target, c.contact_force_threshold = 0.5, 0.4, 1.0, 800.0
+        for name, kid in self.rewards.active():
+            term = terms[name]
+            c.rew_w[kid] = term.weight
+            f = REWARD_FUNCS[kid]
+            if f.startswith("track_"):
+                stds.add(float(term.params.get("std", 0.5)))
+            elif f == "feet_air_time_positive_biped":
+                c.air_time_threshold = term.params.get("threshold", 0.4)
+            elif f == "base_height_l2":
+                c.base_height_target = term.params.get("target_height", 1.0)
+            elif f == "contact_forces":
+                c.contact_force_threshold = term.params.get("threshold", 1.0)
+        if len(stds) > 1:
+            raise ValueError(f"the tracking terms must share one std (got {sorted(stds)})")
+        if stds:
+            c.track_std = stds.pop()
+        pe = self.events.push_robot
+        c.push_interval[:], c.push_vel_x[:], c.push_vel_y[:] = (5.0, 8.0), (-1.0, 1.0), (-1.0, 1.0)  # C defaults
+        if pe is not None:
+            c.push_enable = 1
+            c.push_interval[:] = pe.interval_range_s
+            vr = pe.velocity_range
+            if set(vr) - {"x", "y"}:
+                raise ValueError("push velocity ranges other than x / y are not implemented")
+            c.push_vel_x[:] = vr.get("x", (0.0, 0.0))
+            c.push_vel_y[:] = vr.get("y", (0.0, 0.0))
         c.soft_limit_factor = self.robot.soft_joint_pos_limit_factor
         c.illegal_contact_knees = int(self.terminations.base_contact_knees)
         c.illegal_contact_torso = int(self.terminations.base_contact_torso)
         c.seed = (self.seed if self.seed is not None else 0) & 0xFFFFFFFFFFFFFFFF
-        assert len(REWARD_TERMS) == NREW and NJ == 12
+        assert NJ == 12
         return c
 
 
@@ -457,6 +570,53 @@ def c5_cfg(num_envs: int = 8192) -> H12RoughEnvCfg:
     c.events.physics_material = MaterialEventCfg((0.1, 1.25), (0.1, 1.25), 64)
     c.events.add_base_mass = MassEventCfg(".*torso_link", (0.0, 6.0), "add")
     return c
+
+
+@dataclass
+class H12RslEnvCfg(H12FlatEnvCfg):
+    """Isaac-Velocity-Rsl-H12_12dof-v0 (H12_12dof_EnvCfg, rsl_env_cfg.py:504-540): IdealPD actuators (no
+    delay), action scale 0.25, deadzone velocity commands resampled every U(5, 8) s, 270-float observation
+    (history 6, ang_vel x 0.25, joint_vel x 0.05), sole friction U(0.1, 1.25) in 64 buckets, pushes every
+    U(5, 8) s, the 16-term reward table and its modify_reward_weight curriculum.  The shipped deploy
+    env.yamls (scripts/deploy/policies/*) are this task's."""
+
+    def __post_init__(self):
+        MAX_CURRICULUM_ITERATIONS = 5000
+        self.sim.static_friction = self.sim.dynamic_friction = 1.0   # sim.physics_material = ground (1.0 / 1.0)
+        for g in self.robot.actuators.values():                      # H12_12DOF_IDEAL (h12.py:117-196)
+            g.min_delay = g.max_delay = 0
+        self.actions.joint_pos.scale = 0.25                          # rsl_env_cfg.py:124
+        self.commands.base_velocity = UniformVelocityCommandWithDeadzoneCfg(
+            resampling_time_range=(5.0, 8.0), rel_standing_envs=0.02, rel_heading_envs=1.0, heading_command=False,
+            heading_control_stiffness=1.0, ranges=Ranges((-1.0, 1.0), (-1.0, 1.0), (-1.0, 1.0)),
+            velocity_deadzone=0.0)                                   # rsl_env_cfg.py:83-100
+        po = self.observations.policy
+        po.history_length = 6                                        # rsl_env_cfg.py:199
+        po.scales = {"base_ang_vel": 0.25, "joint_vel": 0.05}        # rsl_env_cfg.py:142, 192
+        self.events.physics_material = MaterialEventCfg((0.1, 1.25), (0.1, 1.25), 64)   # :213-223
+        self.events.push_robot = PushEventCfg((5.0, 8.0), {"x": (-1.0, 1.0), "y": (-1.0, 1.0)})  # :262-273
+        self.rewards = RewardsCfg(_rsl_rewards())
+        n = 24 * MAX_CURRICULUM_ITERATIONS                           # rsl_env_cfg.py:448-501
+        self.curriculum.reward_weights = [
+            RewardWeightTerm(k, w, n) for k, w in (
+                ("flat_orientation", -1.0), ("joint_torques_l2", -1.0e-5), ("joint_vel_l2", -1.0e-3),
+                ("dof_acc_l2", -1.0e-7), ("joint_deviation_hip", -0.2), ("joint_deviation_ankle", -0.2),
+                ("joint_pos_limits_ankle", -0.2), ("joint_pos_limits_hip", -0.2), ("contact_forces", -1.0e-3),
+                ("feet_air_time", 0.75), ("feet_slide", -0.25), ("base_height_l2", -0.2))]
+
+
+@dataclass
+class H12RslEnvCfg_PLAY(H12RslEnvCfg):
+    """rsl_env_cfg.py:543-563: 100 envs, no pushes / material randomisation, no noise, vx 0.5."""
+
+    def __post_init__(self):
+        super().__post_init__()
+        self.scene.num_envs = 100
+        self.events.push_robot = None
+        self.events.physics_material = None
+        self.observations.policy.enable_corruption = False
+        r = self.commands.base_velocity.ranges
+        r.lin_vel_x, r.lin_vel_y, r.ang_vel_z = (0.5, 0.5), (0.0, 0.0), (0.0, 0.0)
 
 
 def mujoco_cfg(**kw) -> H12FlatEnvCfg:

@@ -23,7 +23,7 @@ import torch
 
 from . import _abi
 from ._abi import F as FIELDS
-from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, NOBS_ROUGH, REWARD_TERMS, TASK_ROUGH, H12StepOut, check, load_library
+from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS_ROUGH, NREW, H12StepOut, check, load_library
 from .cfg import H12FlatEnvCfg
 from .model import body_names, build_model, joint_names
 
@@ -46,12 +46,13 @@ class _LazyLog(dict):
     """extras["log"]: IsaacLab's Episode_Reward/* and Episode_Termination/* values, materialised on
     first access from the step's device-side accumulator (no host sync inside step())."""
 
-    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, extra: dict | None = None):
+    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, terms: list, extra: dict | None = None):
         super().__init__()
         self._acc = acc
         self._T = max_episode_length_s
+        self._terms = terms          # [(cfg name, kernel id)] in RewardManager order
         self._extra = extra or {}
-        self._keys = [f"Episode_Reward/{t}" for t in REWARD_TERMS] + [
+        self._keys = [f"Episode_Reward/{t}" for t, _ in terms] + [
             "Episode_Termination/time_out", "Episode_Termination/base_contact"] + list(self._extra)
         self._done = False
 
@@ -59,9 +60,11 @@ class _LazyLog(dict):
         if self._done:
             return
         a = self._acc
-        n = a[12].clamp(min=1.0)
-        vals = torch.cat([a[:12] / n / self._T, a[13:15]])
-        for i, k in enumerate(self._keys[:14]):
+        n = a[NREW].clamp(min=1.0)
+        ids = torch.tensor([k for _, k in self._terms], device=a.device, dtype=torch.long)
+        vals = torch.cat([a[ids] / n / self._T, a[NREW + 1:NREW + 3]])
+        nt = len(self._terms) + 2
+        for i, k in enumerate(self._keys[:nt]):
             dict.__setitem__(self, k, vals[i])
         for k, f in self._extra.items():
             dict.__setitem__(self, k, f())
@@ -106,6 +109,28 @@ class _ObservationManager:
 
     def compute(self):
         return {"policy": self._env._obs[self._env._k]}
+
+
+class _RewardManager:
+    """RewardManager surface used by curriculum terms (modify_reward_weight): term names in order and
+    get/set_term_cfg; a weight change is pushed to the kernel (h12env_set_reward_weights)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    @property
+    def active_terms(self):
+        return [k for k, _ in self._env.cfg.rewards.active()]
+
+    def get_term_cfg(self, name):
+        t = dict(self._env.cfg.rewards.items()).get(name)
+        if t is None:
+            raise ValueError(f"reward term {name!r} not found")
+        return t
+
+    def set_term_cfg(self, name, term_cfg):
+        setattr(self._env.cfg.rewards, name, term_cfg)
+        self._env._push_reward_weights()
 
 
 class _ActionManager:
@@ -198,7 +223,7 @@ class H12VelocityEnv:
         self._fstate = self._state.view(torch.float32)[: NF_FLOAT * self.num_envs].view(NF_FLOAT, self.num_envs)
         self._istate = self._state.view(torch.int32)[NF_FLOAT * self.num_envs:].view(NF_INT, self.num_envs)
         n = self.num_envs
-        self.obs_dim = NOBS_ROUGH if self._ccfg.task == TASK_ROUGH else NOBS
+        self.obs_dim = int(self._lib.h12env_obs_dim(h))
         self._obs = [torch.zeros(n, self.obs_dim, device=self.device), torch.zeros(n, self.obs_dim, device=self.device)]
         self._k = 0
         self.reward_buf = torch.zeros(n, device=self.device)
@@ -219,6 +244,9 @@ class H12VelocityEnv:
         self.scene = SimpleNamespace(env_origins=origins, num_envs=n, terrain=self.terrain)
         self.observation_manager = _ObservationManager(self)
         self.action_manager = _ActionManager(self)
+        self.reward_manager = _RewardManager(self)
+        self._reward_terms = self.cfg.rewards.active()
+        self._rw_pending = list(getattr(self.cfg.curriculum, "reward_weights", []) or [])
         self._data = _ArticulationData(self)
         self.scene.articulations = {"robot": SimpleNamespace(data=self._data, joint_names=self._data.joint_names,
                                                              body_names=self._data.body_names,
@@ -310,6 +338,24 @@ class H12VelocityEnv:
                                                        C.c_void_p(self._t_origins.data_ptr()), rows, cols),
               "h12env_set_terrain")
 
+    def _push_reward_weights(self):
+        self._ccfg = self.cfg.to_c()
+        self._reward_terms = self.cfg.rewards.active()
+        w = (C.c_float * NREW)(*self._ccfg.rew_w)
+        check(self._lib, self._lib.h12env_set_reward_weights(self._h, w, NREW), "h12env_set_reward_weights")
+
+    def _reward_curriculum(self):
+        """modify_reward_weight terms: CurriculumManager.compute runs in _reset_idx after the rewards of a
+        step, so a term whose num_steps the previous step passed reweights from this step on."""
+        due = [t for t in self._rw_pending if self.common_step_counter - 1 > t.num_steps]
+        if not due:
+            return
+        for t in due:
+            term = self.reward_manager.get_term_cfg(t.term_name)
+            term.weight = t.weight
+            self._rw_pending.remove(t)
+        self._push_reward_weights()
+
     def terrain_levels(self) -> torch.Tensor:
         return (self._istate[_abi.I["TERRAIN"][0]] & 0xFFFF).float()
 
@@ -347,6 +393,8 @@ class H12VelocityEnv:
         if a.shape != (self.num_envs, NJ):
             raise ValueError(f"actions must be ({self.num_envs}, {NJ}), got {tuple(a.shape)}")
         self.common_step_counter += 1
+        if self._rw_pending:
+            self._reward_curriculum()
         prev = self._obs[self._k]
         self._k ^= 1
         obs = self._obs[self._k]
@@ -367,7 +415,8 @@ class H12VelocityEnv:
         if rc:
             check(self._lib, rc, "h12env_step")
         extra = {"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()} if self.terrain is not None else None
-        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, extra), "time_outs": self.reset_time_outs}
+        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, self._reward_terms, extra),
+                       "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
         return {"policy": obs_out}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
 

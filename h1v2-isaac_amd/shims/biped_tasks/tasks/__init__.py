@@ -43,3 +43,25 @@ gym.register(
         "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
     },
 )
+
+# h12_12dof/__init__.py:85-103: the Rsl task (IdealPD, deadzone commands, pushes, history 6; the task the
+# shipped deploy env.yamls were exported from), trained with the Flat PPO runner cfg
+gym.register(
+    id="Isaac-Velocity-Rsl-H12_12dof-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "h12env.cfg:H12RslEnvCfg",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
+    },
+)
+
+gym.register(
+    id="Isaac-Velocity-Rsl-H12_12dof-Play-v0",
+    entry_point="isaaclab.envs:ManagerBasedRLEnv",
+    disable_env_checker=True,
+    kwargs={
+        "env_cfg_entry_point": "h12env.cfg:H12RslEnvCfg_PLAY",
+        "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
+    },
+)

@@ -40,14 +40,15 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 2
+#define H12ENV_ABI_VERSION 3
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
-#define H12_NHIST 10       /* observation history length (flat_env_cfg.py:26) */
+#define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
 #define H12_NOBS (H12_OBS_FRAME * H12_NHIST) /* 450 */
 #define H12_NFOOT_PTS 4    /* sole contact spheres per foot (URDF rods, h12_12dof.urdf:168-191) */
-#define H12_NREW 12        /* active reward terms of the Flat task */
-#define H12_NLOG 16        /* log accumulator: 12 episode sums, count, 2 termination counts, spare */
+#define H12_NREW 20        /* reward terms the kernel implements (union of the Flat / Rough / Rsl tables) */
+#define H12_NREW_FLAT 12   /* terms 0-11: the Flat / Rough tables */
+#define H12_NLOG 24        /* log accumulator: 20 episode sums, count, time-out / base-contact counts, spare */
 /* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:128-188): no history, base_lin_vel
  * first, height scan last (velocity_env_cfg.py:118-137) */
 #define H12_ROUGH_FRAME 48 /* lin_vel 3, ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -68,10 +69,13 @@ extern "C" {
 #define H12_MODE_MUJOCO 1   /* PD every substep, no delay, MJCF actuatorfrcrange clamp (sim2sim) */
 
 /* tasks (observation layout) */
-#define H12_TASK_FLAT 0     /* 450-float term-major 10-frame history (flat_env_cfg.py:25-27) */
+#define H12_TASK_FLAT 0     /* 45 x history_length floats, term-major history (flat_env_cfg.py:25-27: 450) */
 #define H12_TASK_ROUGH 1    /* 235 floats: 48-float frame + 187-ray height scan, no history */
+/* (the Rsl task, rsl_env_cfg.py, is H12_TASK_FLAT with history_length 6 and per-term obs_scale) */
 
-/* reward term order (RewardManager order of the merged Flat cfg; weights in h12env_config.rew_w) */
+/* reward terms the kernel implements; h12env_config.rew_w[term] weights them (0 = off).  Terms 0-11 are
+ * the Flat table in its RewardManager order; 12-19 complete the Rsl table (rsl_env_cfg.py:279-407).
+ * The host maps each cfg term (name, mdp function, joint set) onto one of these ids. */
 enum {
   H12_R_TRACK_LIN_VEL_XY = 0, /* track_lin_vel_xy_yaw_frame_exp, std 0.5   rough_env_cfg.py:87-91 */
   H12_R_TRACK_ANG_VEL_Z,      /* track_ang_vel_z_world_exp, std 0.5       rough_env_cfg.py:92-96 */
@@ -84,7 +88,15 @@ enum {
   H12_R_DOF_POS_LIMITS,       /* joint_pos_limits (ankles)                rough_env_cfg.py:115-119 */
   H12_R_TERMINATION,          /* is_terminated                            rough_env_cfg.py:85 */
   H12_R_FEET_SLIDE,           /* feet_slide                               rough_env_cfg.py:106-113 */
-  H12_R_JOINT_DEV_HIP         /* joint_deviation_l1 (hip yaw/roll)        rough_env_cfg.py:121-125 */
+  H12_R_JOINT_DEV_HIP,        /* joint_deviation_l1 (hip yaw/roll)        rough_env_cfg.py:121-125 */
+  H12_R_TRACK_LIN_VEL_XY_BASE,/* track_lin_vel_xy_exp (base frame)        rsl_env_cfg.py:283-287 */
+  H12_R_TRACK_ANG_VEL_Z_BASE, /* track_ang_vel_z_exp (base frame)         rsl_env_cfg.py:288-292 */
+  H12_R_BASE_HEIGHT_L2,       /* base_height_l2, (z - target)^2           rsl_env_cfg.py:322-328 */
+  H12_R_JOINT_VEL_L2,         /* joint_vel_l2 (all joints)                rsl_env_cfg.py:335-338 */
+  H12_R_JOINT_DEV_ANKLE,      /* joint_deviation_l1 (ankle pitch/roll)    rsl_env_cfg.py:358-372 */
+  H12_R_DOF_POS_LIMITS_HIP,   /* joint_pos_limits (hip yaw/roll)          rsl_env_cfg.py:380-386 */
+  H12_R_CONTACT_FORCES,       /* contact_forces: sum_f max(max_h|F|-thr,0) rsl_env_cfg.py:395-405 */
+  H12_R_LIN_VEL_Z_L2          /* lin_vel_z_l2 (v_b,z^2)                   velocity_env_cfg.py:236 */
 };
 
 /* Model constants (filled from h12env/assets/h12_12dof_model.json, generated from the MJCF). */
@@ -162,6 +174,18 @@ typedef struct h12env_config {
   float scan_clip;             /* 1.0 */
   float scan_resolution;       /* 0.1 m grid spacing */
   float terrain_size;          /* 8.0 m sub-terrain edge (terrains.py:12) */
+  /* Rsl task (ABI 3; rsl_env_cfg.py) */
+  float cmd_resample_time_max; /* resampling_time_range = (cmd_resample_time, this); Rsl (5, 8) s */
+  int32_t cmd_deadzone;        /* UniformVelocityCommandWithDeadzone._update_command (utils/mdp/commands.py:41-96) */
+  float velocity_deadzone;     /* |cmd_xy| < this counts as in the deadzone (Rsl 0.0) */
+  float ang_flip_prob;         /* per-step probability of cmd_z *= -1 (physics_dt / episode_length_s) */
+  int32_t push_enable;         /* push_by_setting_velocity interval event (rsl_env_cfg.py:262-273) */
+  float push_interval[2];      /* interval_range_s (5, 8) */
+  float push_vel_x[2], push_vel_y[2]; /* velocity_range x / y (-1, 1) m/s added to the root velocity */
+  int32_t history_length;      /* observation history (flat layout): 10 Flat, 6 Rsl; 1..H12_NHIST */
+  float obs_scale[6];          /* per-term scale after noise: ang_vel, gravity, command, q-q0, qd, action */
+  float base_height_target;    /* base_height_l2 target (1.0) */
+  float contact_force_threshold; /* contact_forces threshold (800 N) */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */
@@ -186,7 +210,9 @@ enum {
   H12_F_ORIGIN = 102,   /* 3  env origin (terrain origin of the env's level / type; 0 on the plane) */
   H12_F_MU = 105,       /* 4  static, dynamic friction of the left / right sole (per_env_friction) */
   H12_F_DMASS = 109,    /* 1  mass added at the torso COM (per_env_mass) */
-  H12_NF_FLOAT = 110
+  H12_F_EPSUM2 = 110,   /* 8  episode sums of reward terms 12-19 */
+  H12_F_PUSH_TIME = 118,/* 1  push_robot interval time left */
+  H12_NF_FLOAT = 119
 };
 enum {
   H12_I_EPLEN = 0,      /* episode_length_buf (int32) */
@@ -198,7 +224,7 @@ enum {
 
 /* Optional per-step outputs; any pointer may be NULL. */
 typedef struct h12env_step_out {
-  float* obs;              /* N x 450 (flat) or N x 235 (rough) (required) */
+  float* obs;              /* N x h12env_obs_dim: 45 x history (flat layout) or 235 (rough) (required) */
   float* rew;              /* N       (required) */
   uint8_t* terminated;     /* N       (required) */
   uint8_t* truncated;      /* N       (required) */
@@ -217,7 +243,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
                   int device, void* state_dev, h12env** out);
 void h12env_destroy(h12env* h);
 /* Reset the envs flagged in mask (N bytes, NULL = all) and write their first observation
- * (history filled with the first frame) into obs (N x 450); other rows are left untouched. */
+ * (history filled with the first frame) into obs (N x h12env_obs_dim); other rows are left untouched. */
 int h12env_reset(h12env* h, const uint8_t* mask, float* obs, void* stream);
 /* One env step (decimation x physics).  obs_prev: previous obs (history source), may equal
  * out->obs.  step_index: common_step_counter after increment (>= 1). */
@@ -240,6 +266,11 @@ int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* str
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);
+/* Observation row length: 45 x history_length (flat layout; 450 Flat, 270 Rsl) or 235 (rough). */
+int h12env_obs_dim(const h12env* h);
+/* Replace the reward weights (n <= H12_NREW floats, indexed by H12_R_*) for the following steps:
+ * CurriculumManager's modify_reward_weight (rsl_env_cfg.py:448-501) without recreating the handle. */
+int h12env_set_reward_weights(h12env* h, const float* w, int n);
 /* Algorithmic accounting of one env step for the roofline report (both kernels of h12env_step). */
 int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_env);
 /* Per-kernel accounting: kernel 0 = the env kernel of h12env_step (physics + MDP), 1 = the observation

@@ -35,7 +35,7 @@ void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c
   out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
 }
 /* streams (counter word c2 = stream << 16 | block) */
-enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3 };
+enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3, ST_PUSH = 4 };
 static double u01(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
 static double uab(uint32_t x, double a, double b) { return a + (b - a) * (double)(float)u01(x); }
 
@@ -77,7 +77,14 @@ double orc_ground(const h12env_config* c, double x, double y, double* gx, double
   return h00 + fu * a + fv * b;
 }
 
-int orc_obs_dim(const h12env_config* c) { return c->task == H12_TASK_ROUGH ? H12_NOBS_ROUGH : H12_NOBS; }
+int orc_obs_dim(const h12env_config* c) {
+  return c->task == H12_TASK_ROUGH ? H12_NOBS_ROUGH : H12_OBS_FRAME * c->history_length;
+}
+
+/* deadzone command count carried between steps (UniformVelocityCommandWithDeadzone; see cmd_update) */
+static int g_dz_count = 0;
+void orc_set_dz_count(int v) { g_dz_count = v; }
+int orc_dz_count(void) { return g_dz_count; }
 
 /* ------------------------------------------------------------------ small linear algebra */
 typedef double m3[3][3];
@@ -630,6 +637,7 @@ int orc_mujoco_rollout(const h12env_model* m, const h12env_config* c, orc_phys* 
 typedef struct orc_env {
   orc_phys p;
   double act[NJ], act_prev[NJ], cmd[3], heading, cmd_time, air[2], con[2], last_air[2], last_con[2], epsum[H12_NREW];
+  double push_t;
   int eplen, lag[3], since_reset, is_heading, is_standing;
   double origin[3];
   int32_t tcell; /* terrain level | type << 16 */
@@ -659,7 +667,9 @@ static void env_load(const float* F, const int32_t* I, int n, int i, orc_env* e)
   LD(e->act, H12_F_ACT, NJ); LD(e->act_prev, H12_F_ACT_PREV, NJ); LD(e->cmd, H12_F_CMD, 3);
   LD(&e->heading, H12_F_HEADING, 1); LD(&e->cmd_time, H12_F_CMD_TIME, 1); LD(e->air, H12_F_AIR, 2);
   LD(e->con, H12_F_CONTACT, 2); LD(e->last_air, H12_F_LAST_AIR, 2); LD(e->last_con, H12_F_LAST_CONTACT, 2);
-  LD(e->epsum, H12_F_EPSUM, H12_NREW);
+  LD(e->epsum, H12_F_EPSUM, H12_NREW_FLAT);
+  LD(e->epsum + H12_NREW_FLAT, H12_F_EPSUM2, H12_NREW - H12_NREW_FLAT);
+  LD(&e->push_t, H12_F_PUSH_TIME, 1);
   LD(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
 #undef LD
   e->eplen = I[(size_t)H12_I_EPLEN * n + i];
@@ -677,7 +687,9 @@ static void env_store(float* F, int32_t* I, int n, int i, const orc_env* e) {
   ST(e->act, H12_F_ACT, NJ); ST(e->act_prev, H12_F_ACT_PREV, NJ); ST(e->cmd, H12_F_CMD, 3);
   ST(&e->heading, H12_F_HEADING, 1); ST(&e->cmd_time, H12_F_CMD_TIME, 1); ST(e->air, H12_F_AIR, 2);
   ST(e->con, H12_F_CONTACT, 2); ST(e->last_air, H12_F_LAST_AIR, 2); ST(e->last_con, H12_F_LAST_CONTACT, 2);
-  ST(e->epsum, H12_F_EPSUM, H12_NREW);
+  ST(e->epsum, H12_F_EPSUM, H12_NREW_FLAT);
+  ST(e->epsum + H12_NREW_FLAT, H12_F_EPSUM2, H12_NREW - H12_NREW_FLAT);
+  ST(&e->push_t, H12_F_PUSH_TIME, 1);
   ST(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
 #undef ST
   I[(size_t)H12_I_EPLEN * n + i] = e->eplen;
@@ -701,27 +713,61 @@ static double heading_w(const orc_phys* p) { /* atan2 of the body x axis in worl
   return atan2(R[1][0], R[0][0]);
 }
 
-/* UniformVelocityCommand._resample_command (upstream; in-repo twin utils/mdp/commands.py:19-59) */
-static void cmd_resample(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi) {
+/* CommandTerm._resample: UniformVelocityCommand._resample_command (upstream; in-repo twin
+ * utils/mdp/commands.py:19-59) and time_left ~ U(resampling_time_range).  blk: first Philox block. */
+static void cmd_resample(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi, int blk) {
   uint32_t r0[4], r1[4];
-  rng_block(c->seed, g, lo, hi, ST_CMD, 0, r0);
-  rng_block(c->seed, g, lo, hi, ST_CMD, 1, r1);
+  rng_block(c->seed, g, lo, hi, ST_CMD, blk, r0);
+  rng_block(c->seed, g, lo, hi, ST_CMD, blk + 1, r1);
   e->cmd[0] = uab(r0[0], c->cmd_lin_x[0], c->cmd_lin_x[1]);
   e->cmd[1] = uab(r0[1], c->cmd_lin_y[0], c->cmd_lin_y[1]);
   e->cmd[2] = uab(r0[2], c->cmd_ang_z[0], c->cmd_ang_z[1]);
   e->heading = uab(r0[3], c->cmd_heading[0], c->cmd_heading[1]);
   e->is_heading = (float)u01(r1[0]) <= c->rel_heading_envs;
   e->is_standing = (float)u01(r1[1]) <= c->rel_standing_envs;
-  e->cmd_time = c->cmd_resample_time;
+  e->cmd_time = uab(r1[2], c->cmd_resample_time, c->cmd_resample_time_max);
 }
-/* UniformVelocityCommand._update_command */
-static void cmd_update(const h12env_config* c, orc_env* e) {
+/* UniformVelocityCommand._update_command; with cmd_deadzone the Rsl/CaT subclass
+ * (utils/mdp/commands.py:41-96): the reference picks exactly (target - count) of the active envs
+ * (or (count - target) of the deadzone ones) by randperm; here each env draws the per-env marginal
+ * of that choice, Bernoulli((target - count) / (n - count)) resp. Bernoulli((count - target) / count),
+ * with the count of the previous step (dz_prev; exact for the shipped velocity_deadzone = 0, where the
+ * count is always 0).  Then cmd_z *= -1 with probability ang_flip_prob.  No standing-env zeroing. */
+static void cmd_update(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi, int dz_prev, int n) {
   if (e->is_heading) {
     double err = wrap_to_pi(e->heading - heading_w(&e->p));
     double w = c->heading_stiffness * err;
     e->cmd[2] = w < c->cmd_ang_z[0] ? c->cmd_ang_z[0] : (w > c->cmd_ang_z[1] ? c->cmd_ang_z[1] : w);
   }
+  if (c->cmd_deadzone) {
+    uint32_t r[4];
+    rng_block(c->seed, g, lo, hi, ST_CMD, 2, r);
+    int target = n / 2;
+    double v = (double)c->velocity_deadzone;
+    int in_dz = (float)e->cmd[0] * (float)e->cmd[0] + (float)e->cmd[1] * (float)e->cmd[1] < (float)(v * v);
+    uint64_t u24 = r[0] >> 8;
+    if (dz_prev < target) {
+      if (!in_dz && u24 * (uint64_t)(n - dz_prev) < ((uint64_t)(target - dz_prev) << 24)) e->cmd[0] = e->cmd[1] = 0;
+    } else if (dz_prev > target) {
+      if (in_dz && u24 * (uint64_t)dz_prev < ((uint64_t)(dz_prev - target) << 24)) cmd_resample(c, e, g, lo, hi, 3);
+    }
+    if (u01(r[1]) < (double)c->ang_flip_prob) e->cmd[2] = -e->cmd[2];
+    return;
+  }
   if (e->is_standing) e->cmd[0] = e->cmd[1] = e->cmd[2] = 0;
+}
+
+/* push_by_setting_velocity interval event (EventManager.apply(mode="interval"), rsl_env_cfg.py:262-273) */
+static void push_event(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi, double step_dt) {
+  if (!c->push_enable) return;
+  e->push_t = (float)(e->push_t - step_dt);
+  if (e->push_t < 1e-6) {
+    uint32_t r[4];
+    rng_block(c->seed, g, lo, hi, ST_PUSH, 0, r);
+    e->push_t = uab(r[2], c->push_interval[0], c->push_interval[1]);
+    e->p.vlin[0] += uab(r[0], c->push_vel_x[0], c->push_vel_x[1]);
+    e->p.vlin[1] += uab(r[1], c->push_vel_y[0], c->push_vel_y[1]);
+  }
 }
 
 /* _reset_idx: scene reset (delay lags, sensor), reset events, manager resets (cat_env.py:195-248) */
@@ -783,7 +829,12 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   memset(e->last_con, 0, sizeof e->last_con);
   memset(e->epsum, 0, sizeof e->epsum);
   e->eplen = 0;
-  cmd_resample(c, e, g, lo, hi);
+  if (c->push_enable) { /* EventManager.reset: new interval for the reset envs */
+    uint32_t r3[4];
+    rng_block(c->seed, g, lo, hi, ST_RESET, 3, r3);
+    e->push_t = uab(r3[0], c->push_interval[0], c->push_interval[1]);
+  }
+  cmd_resample(c, e, g, lo, hi, 0);
 }
 
 /* observation frame (ObservationManager.compute_group, observation_manager.py:318-351) */
@@ -814,20 +865,26 @@ static void obs_frame(const h12env_model* m, const h12env_config* c, const orc_e
       fr[idx[t]] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)noise[t]);
     }
   }
+  /* ObsTerm scale, after noise (observation_manager.py:327-336) */
+  for (int k2 = 0; k2 < H12_OBS_FRAME; ++k2) {
+    int t = k2 < 9 ? k2 / 3 : 3 + (k2 - 9) / NJ;
+    fr[k2] *= (double)c->obs_scale[t];
+  }
 }
 static const int TERM_DIM[6] = {3, 3, 3, NJ, NJ, NJ};
-static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* out, int fill) {
+/* CircularBuffer append + buffer() flattening of a term-major row, nh frames per term (oldest first) */
+static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* out, int fill, int nh) {
   int off = 0, fo = 0;
   for (int t = 0; t < 6; ++t) {
     int d = TERM_DIM[t];
-    for (int h = 0; h < H12_NHIST; ++h)
+    for (int h = 0; h < nh; ++h)
       for (int a = 0; a < d; ++a) {
         double v;
-        if (fill || h == H12_NHIST - 1) v = fr[fo + a];
+        if (fill || h == nh - 1) v = fr[fo + a];
         else v = prev[off + (h + 1) * d + a];
         out[off + h * d + a] = (float)v;
       }
-    off += d * H12_NHIST;
+    off += d * nh;
     fo += d;
   }
 }
@@ -898,7 +955,7 @@ int orc_delay_source(int lag, int since_reset, int substep, int decimation) {
 }
 
 void orc_history_write(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill) {
-  obs_write(frame, prev_row, out_row, fill);
+  obs_write(frame, prev_row, out_row, fill, H12_NHIST);
 }
 
 /* ObservationManager.compute() outside step(): one new frame per env, history shifted (or filled
@@ -915,8 +972,9 @@ int orc_env_observe(const h12env_model* m, const h12env_config* c, int n, int64_
       continue;
     }
     double fr[H12_OBS_FRAME];
+    const size_t row = (size_t)orc_obs_dim(c);
     obs_frame(m, c, &e, env_offset + i, lo, hi, fr);
-    obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, fill_mask ? fill_mask[i] : 0);
+    obs_write(fr, obs_prev + (size_t)i * row, obs + (size_t)i * row, fill_mask ? fill_mask[i] : 0, c->history_length);
   }
   return 0;
 }
@@ -936,7 +994,7 @@ int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t 
     } else {
       double fr[H12_OBS_FRAME];
       obs_frame(m, c, &e, g, lo, hi, fr);
-      obs_write(fr, 0, obs + (size_t)i * H12_NOBS, 1);
+      obs_write(fr, 0, obs + (size_t)i * orc_obs_dim(c), 1, c->history_length);
     }
     env_store(F, I, n, i, &e);
     env_store_extra(c, F, I, n, i, &e);
@@ -953,6 +1011,8 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
   const uint32_t lo = (uint32_t)step_index, hi = (uint32_t)((uint64_t)step_index >> 32);
   const int dec = c->decimation;
   const double dt = c->physics_dt, step_dt = c->physics_dt * dec;
+  const int dz_prev = g_dz_count;
+  int dz_next = 0;
   int err = 0;
 #ifdef _OPENMP
   if (n_threads < 1) n_threads = 1;
@@ -1095,6 +1155,32 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       s_dev += fabs(e.p.q[j0] - m->q_default[j0]) + fabs(e.p.q[j2] - m->q_default[j2]);
     }
     terms[H12_R_JOINT_DEV_HIP] = s_dev;
+    /* Rsl table (rsl_env_cfg.py:279-407) */
+    {
+      double vb[3];
+      m3tv(R, vcom, vb); /* root_lin_vel_b */
+      terms[H12_R_TRACK_LIN_VEL_XY_BASE] = exp(-(sq(e.cmd[0] - vb[0]) + sq(e.cmd[1] - vb[1])) / std2);
+      terms[H12_R_TRACK_ANG_VEL_Z_BASE] = exp(-sq(e.cmd[2] - wb[2]) / std2);
+      terms[H12_R_BASE_HEIGHT_L2] = sq(e.p.pos[2] - c->base_height_target);
+      double s_v = 0, s_da = 0, s_lh = 0, s_cf = 0;
+      for (int j = 0; j < NJ; ++j) s_v += sq(e.p.qd[j]);
+      for (int f = 0; f < 2; ++f) {
+        for (int k = 4; k < 6; ++k) s_da += fabs(e.p.q[6 * f + k] - m->q_default[6 * f + k]);
+        for (int k = 0; k < 3; k += 2) { /* hip yaw, hip roll soft limits */
+          int j = 6 * f + k;
+          double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+          double lo_s = mid - half, hi_s = mid + half, q = e.p.q[j];
+          s_lh += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
+        }
+        double viol = fmax_foot[f] - c->contact_force_threshold;
+        s_cf += viol > 0 ? viol : 0.0;
+      }
+      terms[H12_R_JOINT_VEL_L2] = s_v;
+      terms[H12_R_JOINT_DEV_ANKLE] = s_da;
+      terms[H12_R_DOF_POS_LIMITS_HIP] = s_lh;
+      terms[H12_R_CONTACT_FORCES] = s_cf;
+      terms[H12_R_LIN_VEL_Z_L2] = sq(vb[2]);
+    }
     double r = 0;
     for (int t = 0; t < H12_NREW; ++t) {
       double v = terms[t] * c->rew_w[t] * step_dt;
@@ -1114,9 +1200,9 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
 #endif
         {
           for (int t = 0; t < H12_NREW; ++t) log_acc[t] += (float)e.epsum[t];
-          log_acc[12] += 1.0f;
-          log_acc[13] += (float)tout;
-          log_acc[14] += (float)term;
+          log_acc[H12_NREW] += 1.0f;
+          log_acc[H12_NREW + 1] += (float)tout;
+          log_acc[H12_NREW + 2] += (float)term;
         }
       }
       env_reset_one(m, c, &e, g, lo, hi);
@@ -1124,19 +1210,30 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       e.since_reset = e.since_reset < 2 ? e.since_reset + 1 : 2;
     }
     /* CommandTerm.compute(dt) */
-    e.cmd_time -= step_dt;
-    if (e.cmd_time <= 0) cmd_resample(c, &e, g, lo, hi);
-    cmd_update(c, &e);
+    e.cmd_time = (float)(e.cmd_time - step_dt);
+    if (e.cmd_time <= 0) cmd_resample(c, &e, g, lo, hi, 0);
+    cmd_update(c, &e, g, lo, hi, dz_prev, n);
+    if (c->cmd_deadzone && (float)e.cmd[0] * (float)e.cmd[0] + (float)e.cmd[1] * (float)e.cmd[1] <
+                               (float)((double)c->velocity_deadzone * c->velocity_deadzone)) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+      dz_next++;
+    }
+    /* interval events */
+    push_event(c, &e, g, lo, hi, step_dt);
     if (c->task == H12_TASK_ROUGH) {
       obs_row_rough(m, c, &e, g, lo, hi, obs + (size_t)i * H12_NOBS_ROUGH);
     } else {
       double fr[H12_OBS_FRAME];
+      const size_t row = (size_t)orc_obs_dim(c);
       obs_frame(m, c, &e, g, lo, hi, fr);
-      obs_write(fr, obs_prev + (size_t)i * H12_NOBS, obs + (size_t)i * H12_NOBS, reset);
+      obs_write(fr, obs_prev + (size_t)i * row, obs + (size_t)i * row, reset, c->history_length);
     }
     env_store(F, I, n, i, &e);
     env_store_extra(c, F, I, n, i, &e);
   }
+  if (c->cmd_deadzone) g_dz_count = dz_next;
   return err;
 }
 

@@ -15,7 +15,10 @@
  *   - the MDP terms of Isaac-Velocity-Flat-H12_12dof-v0 (rewards, terminations, resets,
  *     commands, observations + 10-frame history) as restated in SURVEY.md §8(a);
  *   - the rough task's additions (heightfield contact, height scan, base_lin_vel, terrain
- *     curriculum, per-env friction / added torso mass) as restated in DESIGN.md (row f2).
+ *     curriculum, per-env friction / added torso mass) as restated in DESIGN.md (row f2);
+ *   - the Rsl task's additions (rsl_env_cfg.py: reward terms 12-19, deadzone commands with
+ *     sign flips, push_by_setting_velocity interval event, observation history 6 + term scales,
+ *     resampling-time range) as restated in DESIGN.md (row f4).
  *
  * Parity status: the algorithm of record (PhysX / MuJoCo / IsaacLab managers) is not present
  * in this container, so physics parity against it is UNPINNED; the oracle itself is pinned
@@ -97,8 +100,12 @@ void orc_set_terrain(const float* heights, int nx, int ny, double hscale, double
                      const float* origins, int rows, int cols);
 /* Ground height and slope at (x, y) (plane z = 0 when c->terrain = 0). */
 double orc_ground(const h12env_config* c, double x, double y, double* gx, double* gy);
-/* Observation row length of the configured task: 450 (flat) or 235 (rough). */
+/* Observation row length of the configured task: 45 x history_length (flat layout) or 235 (rough). */
 int orc_obs_dim(const h12env_config* c);
+/* Deadzone command count carried from one orc_env_step to the next (the kernel's rotating counter);
+ * process-global like the terrain. */
+void orc_set_dz_count(int v);
+int orc_dz_count(void);
 
 /* RNG shared by both sides (Philox4x32-10). */
 void orc_philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]);

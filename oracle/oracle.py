@@ -16,7 +16,7 @@ HERE = Path(__file__).resolve().parent
 ROOT = HERE.parent
 sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 
-from h12env._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, NOBS_ROUGH, TASK_ROUGH, H12Config, H12Model  # noqa: E402
+from h12env._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS, H12Config, H12Model  # noqa: E402
 
 LIB = HERE / "liboracle.so"
 
@@ -89,6 +89,12 @@ def lib():
         L.orc_set_terrain.restype = None
         L.orc_ground.argtypes = [Cf, C.c_double, C.c_double, dp, dp]
         L.orc_ground.restype = C.c_double
+        L.orc_obs_dim.argtypes = [Cf]
+        L.orc_obs_dim.restype = C.c_int
+        L.orc_set_dz_count.argtypes = [C.c_int]
+        L.orc_set_dz_count.restype = None
+        L.orc_dz_count.argtypes = []
+        L.orc_dz_count.restype = C.c_int
         _lib = L
     return _lib
 
@@ -179,6 +185,15 @@ def set_terrain(heights, hscale, x0, y0, origins=None):
     lib().orc_set_terrain(_p(h), h.shape[0], h.shape[1], float(hscale), float(x0), float(y0), _p(o), rows, cols)
 
 
+def set_dz_count(v: int):
+    """Deadzone command count the next step reads (the kernel's counter starts at 0)."""
+    lib().orc_set_dz_count(int(v))
+
+
+def dz_count() -> int:
+    return int(lib().orc_dz_count())
+
+
 def ground(cfg, x, y):
     gx, gy = np.zeros(1), np.zeros(1)
     h = lib().orc_ground(C.byref(cfg), float(x), float(y), _d(gx), _d(gy))
@@ -192,7 +207,7 @@ class OracleEnv:
         self.model, self.cfg, self.n, self.env_offset = model, cfg, n, env_offset
         self.F = np.zeros((NF_FLOAT, n), dtype=np.float32)
         self.I = np.zeros((NF_INT, n), dtype=np.int32)
-        self.obs = np.zeros((n, NOBS_ROUGH if cfg.task == TASK_ROUGH else NOBS), dtype=np.float32)
+        self.obs = np.zeros((n, lib().orc_obs_dim(C.byref(cfg))), dtype=np.float32)
         self.reset_counter = 0
         self.observe_counter = 0
 

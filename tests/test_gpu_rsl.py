@@ -1,0 +1,137 @@
+"""GPU parity of the Rsl task (row f4, Isaac-Velocity-Rsl-H12_12dof-v0) through the C-ABI against the oracle:
+the 270-float observation (history 6, term scales) from the H=6 instantiation of obs_assemble_kernel, the
+extended reward table, deadzone commands (the rotating device counter vs the oracle's carried count), the
+push interval event, IdealPD (no delay) and the modify_reward_weight curriculum.  Tolerances as in
+test_gpu_parity.py: rtol 1e-5 on reset observations / state; >= 99 % of envs at 2e-3 after contact-rich
+steps (fp32 vs fp64 contact/slip decisions); command decisions and integer state bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from h12env._abi import F as FIELDS
+from h12env._abi import REWARD_FUNCS
+from h12env.cfg import H12RslEnvCfg, RewardWeightTerm
+from h12env.env import H12VelocityEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def make(n, cfg=None):
+    cfg = cfg or H12RslEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    ref = O.OracleEnv(env._model, env._ccfg, n)
+    ref.F[:] = env._fstate.cpu().numpy()
+    ref.I[:] = env._istate.cpu().numpy()
+    O.set_dz_count(0)
+    return env, ref
+
+
+def close_rows(a, b, tol=2e-3):
+    return (np.abs(a - b) <= tol * np.maximum(1, np.abs(b))).all(axis=1)
+
+
+def field(Fm, k):
+    o, c = FIELDS[k]
+    return Fm[o:o + c]
+
+
+def test_rsl_reset_and_steps_match_oracle(gpu):
+    n = 512
+    env, ref = make(n)
+    obs, _ = env.reset()
+    r = ref.reset()
+    assert obs["policy"].shape == (n, 270) and env.observation_manager.group_obs_dim["policy"] == (270,)
+    np.testing.assert_allclose(obs["policy"].cpu().numpy(), r, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(env._fstate.cpu().numpy(), ref.F, rtol=1e-6, atol=1e-6)
+    assert (env._istate.cpu().numpy() == ref.I).all()
+    rng = np.random.default_rng(31)
+    for t in range(1, 6):
+        a = rng.normal(size=(n, 12)).astype(np.float32)
+        obs, rew, term, trunc, ext = env.step(torch.from_numpy(a).cuda())
+        r_obs, r_rew, r_term, r_trunc, _ = ref.step(a, t)
+        ok = close_rows(obs["policy"].cpu().numpy(), r_obs)
+        assert ok.mean() >= 0.99, (t, ok.mean())
+        assert (term.cpu().numpy() == r_term).mean() >= 0.99
+        assert (trunc.cpu().numpy() == r_trunc).all()
+        okr = np.abs(rew.cpu().numpy() - r_rew) <= 1e-3 * np.maximum(1, np.abs(r_rew))
+        assert okr.mean() >= 0.99, (t, okr.mean())
+        # deadzone decisions (xy zeroed or kept) and sign flips are the same draws on both sides
+        g = env._fstate.cpu().numpy()
+        zg = (field(g, "CMD")[0] == 0) & (field(g, "CMD")[1] == 0)
+        zr = (field(ref.F, "CMD")[0] == 0) & (field(ref.F, "CMD")[1] == 0)
+        assert (zg == zr).mean() >= 0.99
+        # velocity_deadzone 0: half of all envs are zeroed every step and stay zero until resampled
+        assert abs(zg.mean() - (1 - 0.5 ** t)) < 0.1, (t, zg.mean())
+    keys = list(ext["log"].keys())
+    assert "Episode_Reward/joint_deviation_ankle" in keys and "Episode_Reward/contact_forces" in keys
+    assert len([k for k in keys if k.startswith("Episode_Reward/")]) == 16
+    env.close()
+
+
+def test_deadzone_counter_and_flips_match_oracle(gpu):
+    n = 1024
+    cfg = H12RslEnvCfg()
+    cfg.commands.base_velocity.velocity_deadzone = 0.6
+    env, ref = make(n, cfg)
+    env.reset()
+    ref.reset()
+    for t in range(1, 5):
+        a = np.zeros((n, 12), np.float32)
+        env.step(torch.from_numpy(a).cuda())
+        ref.step(a, t)
+        g = env._fstate.cpu().numpy()
+        np.testing.assert_array_equal(field(g, "CMD")[0:2] == 0, field(ref.F, "CMD")[0:2] == 0)
+        np.testing.assert_allclose(field(g, "CMD"), field(ref.F, "CMD"), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(field(g, "CMD_TIME"), field(ref.F, "CMD_TIME"), atol=1e-5)
+    # about half of the envs sit in the deadzone once the controller has acted
+    cm = field(env._fstate.cpu().numpy(), "CMD")
+    assert 0.35 < ((cm[0] ** 2 + cm[1] ** 2) < 0.36).mean() < 0.65
+    env.close()
+
+
+def test_push_event_matches_oracle(gpu):
+    n = 256
+    env, ref = make(n)
+    env.reset()
+    ref.reset()
+    Fm = env._fstate.cpu().numpy()
+    pt = field(Fm, "PUSH_TIME")
+    assert (pt >= 5.0).all() and (pt <= 8.0).all()
+    o = FIELDS["PUSH_TIME"][0]
+    Fm[o, : n // 2] = 0.01           # half of the envs are pushed in the next step
+    env._fstate.copy_(torch.from_numpy(Fm))
+    ref.F[:] = Fm
+    a = np.zeros((n, 12), np.float32)
+    env.step(torch.from_numpy(a).cuda())
+    ref.step(a, 1)
+    g = env._fstate.cpu().numpy()
+    np.testing.assert_allclose(field(g, "PUSH_TIME"), field(ref.F, "PUSH_TIME"), atol=1e-5)
+    ok = close_rows(field(g, "VLIN").T, field(ref.F, "VLIN").T)
+    assert ok.mean() >= 0.99
+    pushed = field(g, "PUSH_TIME")[: n // 2]
+    assert (pushed >= 5.0 - 1e-5).all()
+    env.close()
+
+
+def test_reward_weight_curriculum_reaches_the_kernel(gpu):
+    n = 128
+    cfg = H12RslEnvCfg()
+    cfg.curriculum.reward_weights = [RewardWeightTerm("base_height_l2", -50.0, 1)]
+    env, ref = make(n, cfg)
+    env.reset()
+    ref.reset()
+    kid = REWARD_FUNCS.index("base_height_l2")
+    rng = np.random.default_rng(3)
+    for t in range(1, 4):
+        if t == 3:   # the curriculum term passed num_steps in step 2's reset pass
+            ref.cfg.rew_w[kid] = -50.0
+        a = (0.2 * rng.normal(size=(n, 12))).astype(np.float32)
+        _, rew, *_ = env.step(torch.from_numpy(a).cuda())
+        _, r_rew, *_ = ref.step(a, t)
+        okr = np.abs(rew.cpu().numpy() - r_rew) <= 1e-3 * np.maximum(1, np.abs(r_rew))
+        assert okr.mean() >= 0.99, (t, okr.mean())
+    assert env.cfg.rewards.base_height_l2.weight == -50.0
+    env.close()

@@ -60,3 +60,15 @@ def test_train_rough_task_one_iteration(gpu, tmp_path, monkeypatch):
     run = next((tmp_path / "logs" / "rsl_rl" / "h12_12dof_rough").iterdir())
     x = json.loads((run / "metrics.jsonl").read_text().splitlines()[-1])
     assert "Curriculum/terrain_levels" in x
+
+
+def test_train_rsl_task_one_iteration(gpu, tmp_path, monkeypatch):
+    import train
+
+    monkeypatch.chdir(tmp_path)
+    rc = train.main(["--task", "Isaac-Velocity-Rsl-H12_12dof-v0", "--headless", "--num_envs", "256",
+                     "--max_iterations", "1"])
+    assert rc == 0
+    run = next((tmp_path / "logs" / "rsl_rl" / "h12_12dof_flat").iterdir())
+    x = json.loads((run / "metrics.jsonl").read_text().splitlines()[-1])
+    assert "Episode_Reward/joint_vel_l2" in x and "Episode_Reward/base_height_l2" in x

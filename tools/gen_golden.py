@@ -128,6 +128,7 @@ def gen_deploy_env_yaml():
         out[p.parent.name] = {"keys": list(d.keys()), "observations": d["observations"],
                               "history_length": d["history_length"], "action_scale": d["action_scale"],
                               "control_dt": d["control_dt"], "command_ranges": d["command_ranges"],
+                              "velocity_deadzone": d["velocity_deadzone"], "history_step": d["history_step"],
                               "leg_joints": legs}
     (OUT / "deploy_env_yaml.json").write_text(json.dumps(out, indent=1))
 
