@@ -45,10 +45,10 @@ def parse():
                         "of the train.py runner, rollout all-gathered over RCCL when N > 1)")
     p.add_argument("--iterations", type=int, default=5, help="train mode: timed PPO iterations")
     p.add_argument("--precision", choices=("fp32", "bf16"), default="fp32", help="train mode: learning-phase GEMM precision")
-    p.add_argument("--task", choices=("flat", "rough", "c5", "rsl"), default="flat",
+    p.add_argument("--task", choices=("flat", "rough", "c5", "rsl", "cat"), default="flat",
                    help="flat: the metric's task; rough: Isaac-Velocity-Rough-H12_12dof-v0; c5: BASELINE config C5 "
                         "(rough + per-env friction / torso mass, 8192 envs unless --envs); rsl: "
-                        "Isaac-Velocity-Rsl-H12_12dof-v0")
+                        "Isaac-Velocity-Rsl-H12_12dof-v0; cat: Isaac-Velocity-CaT-Flat-H12_12dof-v0")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
@@ -182,7 +182,7 @@ def main():
         return
 
     from h12env import H12FlatEnvCfg
-    from h12env.cfg import H12RoughEnvCfg, H12RslEnvCfg, c5_cfg
+    from h12env.cfg import H12CaTEnvCfg, H12RoughEnvCfg, H12RslEnvCfg, c5_cfg
     from h12env.env import H12VelocityEnv
 
     n = args.envs
@@ -192,6 +192,8 @@ def main():
         cfg = H12RoughEnvCfg()
     elif args.task == "rsl":
         cfg = H12RslEnvCfg()
+    elif args.task == "cat":
+        cfg = H12CaTEnvCfg()
     else:
         cfg = c5_cfg()
     cfg.scene.num_envs = n
@@ -249,9 +251,10 @@ def main():
         achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
         traffic, obs_traffic, pmc_src = load_pmc(args.pmc_file)
         metric, workload = METRIC, "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X"
-        if args.task == "rsl":
-            metric = f"env-steps/sec at {n} envs, Velocity-Rsl-H12_12dof"
-            workload = f"Isaac-Velocity-Rsl-H12_12dof-v0 random-action rollout, {n} envs per MI355X"
+        if args.task in ("rsl", "cat"):
+            tid = {"rsl": "Rsl-H12_12dof", "cat": "CaT-Flat-H12_12dof"}[args.task]
+            metric = f"env-steps/sec at {n} envs, Velocity-{tid}"
+            workload = f"Isaac-Velocity-{tid}-v0 random-action rollout, {n} envs per MI355X"
         elif args.task != "flat":
             metric = f"env-steps/sec at {n} envs, Velocity-Rough-H12_12dof" + (" + friction/mass randomisation (C5)"
                                                                                if args.task == "c5" else "")

@@ -116,7 +116,32 @@ struct KParams {
   int hist;               // observation history length (flat layout)
   float oscale[6];        // per-term observation scale
   float h_target, cf_thr;
+  // CaT task (T/utils/cat/*): constraints -> termination probabilities
+  int cat;
+  uint32_t cmask;
+  float cmaxp[H12_NCSTR], ctau, cminp;
+  float cvlim[NL], celim[NL];  // joint velocity / effort limits (leg-symmetric)
+  float c_ff, c_nm_dz, c_nm_v, c_or, c_h, c_hstd, c_clr, c_clr_dz;
+  float* cscr;            // [CAT_ROWS][n] raw constraints of the step (+ no_move flag, pre-reset episode length)
+  int* ckey;              // [H12_NCSTR_COLS] column maxima of the step (order-preserving int keys)
+  float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
+  int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
+  int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised
 };
+
+// CaT constraint columns (ConstraintsCfg order, cat_env_cfg.py:336-427) and the scratch rows after them
+constexpr int C_COL0[H12_NCSTR + 1] = {0, 1, 13, 25, 37, 39, 51, 52, 53, 54, 56};
+constexpr int CAT_ROW_NOMOVE = H12_NCSTR_COLS;      // 1 if all |cmd| < no_move deadzone
+constexpr int CAT_ROW_EPLEN = H12_NCSTR_COLS + 1;   // episode length before the reset of this step
+constexpr int CAT_ROWS = H12_NCSTR_COLS + 2;
+static_assert(C_COL0[H12_NCSTR] == H12_NCSTR_COLS, "constraint columns");
+// float -> int key with the same order (atomicMax on floats of either sign)
+H12_DEV int fkey(float f) {
+  int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+H12_DEV float fkey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
+constexpr float CAT_NEG = -3.0e38f;  // "no value" in the column maxima (finite: device code is finite-math)
 static_assert(sizeof(KParams) < 1024, "kernarg budget");
 
 struct Workspace {
@@ -776,6 +801,70 @@ H12_DEV void cmd_update(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uin
   if (s.is_standing) s.cmd[0] = s.cmd[1] = s.cmd[2] = 0.f;
 }
 
+// ---- CaT constraints (T/utils/cat/constraints.py) on the pre-reset state of the step, raw values into the
+// scratch [col][n] (each lane its leg's joint columns and its foot's columns, lane 0 of the pair the base
+// ones), the no_move activity flag and the pre-reset episode length for cat_prob_kernel.  foot_clearance
+// keeps its swing state (max foot height since the last touchdown) in H12_F_SWING_H.
+template <int LINK>
+H12_DEV void link_pos(const Leg& lg, float (&R)[3][3], float* p) {
+  float sn, cs;
+  fsincos(lg.q[LINK], &sn, &cs);
+  float Rr[3];
+  mv(R, h12m::R[LINK], Rr);
+  p[0] += Rr[0]; p[1] += Rr[1]; p[2] += Rr[2];
+  rmul_axis<AX[LINK]>(R, cs, sn);
+}
+
+// constraints.no_move applies while every command component is inside the deadzone
+H12_DEV bool cat_still(const KParams& P, const EnvSt& s) {
+  return fabsf(s.cmd[0]) < P.c_nm_dz && fabsf(s.cmd[1]) < P.c_nm_dz && fabsf(s.cmd[2]) < P.c_nm_dz;
+}
+
+H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int leg, const EnvSt& s, const float* tau,
+                             float fmax_foot, int term, const float R[3][3], int eplen_pre) {
+  const int n = W.n;
+  float* S = P.cscr;
+  const float sg = leg ? -1.f : 1.f;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int j = NL * leg + k;
+    const float q = s.lg.q[k], qd = fabsf(s.lg.qd[k]);
+    S[(size_t)(C_COL0[H12_C_JOINT_POS_LIMITS] + j) * n + e] = fmaxf(soft_lo(P, k) - q, q - soft_hi(P, k));
+    S[(size_t)(C_COL0[H12_C_JOINT_VEL_LIMITS] + j) * n + e] = qd - P.cvlim[k];
+    S[(size_t)(C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j) * n + e] = fabsf(tau[k]) - P.celim[k];
+    S[(size_t)(C_COL0[H12_C_NO_MOVE] + j) * n + e] = qd - P.c_nm_v;
+  }
+  S[(size_t)(C_COL0[H12_C_FOOT_CONTACT_FORCE] + leg) * n + e] = fmax_foot - P.c_ff;
+  // foot_clearance: touchdown = ContactSensor.compute_first_contact(step_dt); command active = any |cmd| > dz
+  {
+    const bool touchdown = s.con > 0.f && s.con < P.step_dt + 1e-8f;
+    const bool active = fabsf(s.cmd[0]) > P.c_clr_dz || fabsf(s.cmd[1]) > P.c_clr_dz || fabsf(s.cmd[2]) > P.c_clr_dz;
+    float Rf[3][3];
+    const float mm[3] = {1.f, sg, 1.f};
+    for (int i = 0; i < 3; ++i)
+      for (int jj = 0; jj < 3; ++jj) Rf[i][jj] = mm[i] * mm[jj] * R[i][jj];
+    float p[3] = {0.f, 0.f, 0.f};
+    link_pos<0>(s.lg, Rf, p); link_pos<1>(s.lg, Rf, p); link_pos<2>(s.lg, Rf, p);
+    link_pos<3>(s.lg, Rf, p); link_pos<4>(s.lg, Rf, p); link_pos<5>(s.lg, Rf, p);
+    const float foot_z = s.b.pos[2] + p[2];  // body_link_pos_w z of the ankle-roll link
+    float& sw = W.F[(size_t)(H12_F_SWING_H + leg) * n + e];
+    const float sh = sw;
+    S[(size_t)(C_COL0[H12_C_FOOT_CLEARANCE] + leg) * n + e] = (touchdown && active) ? (P.c_clr - sh) : 0.f;
+    sw = touchdown ? 0.f : fmaxf(sh, foot_z);
+  }
+  const int nfeet = (fmax_foot > 1.0f ? 1 : 0) + (pair_swap(fmax_foot) > 1.0f ? 1 : 0);
+  if (leg == 0) {
+    S[(size_t)C_COL0[H12_C_CONTACT] * n + e] = term ? 1.f : 0.f;
+    const float gx = R[2][0], gy = R[2][1];  // projected gravity xy (sign irrelevant under the norm)
+    S[(size_t)C_COL0[H12_C_BASE_ORIENTATION] * n + e] = fsqrt(gx * gx + gy * gy) - P.c_or;
+    const float z = s.b.pos[2];
+    S[(size_t)C_COL0[H12_C_BASE_HEIGHT] * n + e] = (z < P.c_h - P.c_hstd || z > P.c_h + P.c_hstd) ? 1.f : 0.f;
+    S[(size_t)C_COL0[H12_C_FOOT_CONTACT] * n + e] = (nfeet < 1 || nfeet > 2) ? 1.f : 0.f;
+    S[(size_t)CAT_ROW_NOMOVE * n + e] = cat_still(P, s) ? 1.f : 0.f;
+    S[(size_t)CAT_ROW_EPLEN * n + e] = (float)eplen_pre;
+  }
+}
+
 // push_by_setting_velocity as an interval event (EventManager.apply(mode="interval"), rsl_env_cfg.py:262-273):
 // time_left -= step_dt; at < 1e-6 a new interval is drawn and U(range) is added to the root x / y velocity
 template <int K>
@@ -1343,6 +1432,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       r += v;
       s.epsum[t] += v;
     }
+    if (Feat<K>::ext && P.cat) cat_constraints(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
     PH(3);
     const bool reset = term || tout;
     if (leg == 0) {
@@ -1381,6 +1471,154 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     PH(6);
     store_env<K>(P, W, e, leg, s);
     PH(7);
+  }
+}
+
+// CaT, after step_kernel: per-column maxima over the envs (CaT.add: constraint.max(dim=0)).  Grid
+// (env chunks of CAT_CHUNK, columns): one block max per (chunk, column) through LDS, one atomic per block.
+// no_move columns only take the still envs -- the maximum over the reference's remapped rows.
+constexpr int CAT_CBLOCK = 256, CAT_CHUNK = 1024;
+__global__ void __launch_bounds__(CAT_CBLOCK) cat_colmax_kernel(KParams P, int n) {
+  __shared__ float s_red[CAT_CBLOCK / 64];
+  const int col = blockIdx.y;
+  const int i0 = blockIdx.x * CAT_CHUNK;
+  const float* S = P.cscr;
+  const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
+  float m = CAT_NEG;
+#pragma unroll
+  for (int u = 0; u < CAT_CHUNK / CAT_CBLOCK; ++u) {
+    const int i = i0 + u * CAT_CBLOCK + threadIdx.x;
+    if (i < n) {
+      const float v = S[(size_t)col * n + i];
+      const bool take = !nm || S[(size_t)CAT_ROW_NOMOVE * n + i] != 0.f;
+      if (take) m = fmaxf(m, v);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = s_red[0];
+    for (int w = 1; w < CAT_CBLOCK / 64; ++w) b = fmaxf(b, s_red[w]);
+    atomicMax(&P.ckey[col], fkey(b));
+  }
+}
+
+// CaT: the running maxima (CaT.add, constraint_manager.py:42-78) and the compacted list of still envs in
+// ascending order (constraints.no_move hands env i the row of the (i mod m)-th still env,
+// constraints.py:202-238).  One block; per 1024-env chunk a ballot prefix in each wave and one LDS pass over
+// the wave totals.  Resets the column maxima for the next step.
+constexpr int CAT_RBLOCK = 1024;
+__global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n) {
+  __shared__ int s_wsum[CAT_RBLOCK / 64];
+  __shared__ int s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_base = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += CAT_RBLOCK) {
+    const int i = c0 + tid;
+    const bool f = i < n && P.cscr[(size_t)CAT_ROW_NOMOVE * n + i] != 0.f;
+    const unsigned long long b = __ballot(f);
+    const int below = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wsum[wave] = __popcll(b);
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < wave; ++w) off += s_wsum[w];
+    if (f) P.clist[off + below] = i;
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < CAT_RBLOCK / 64; ++w) t += s_wsum[w];
+      s_base += t;
+    }
+    __syncthreads();
+  }
+  const int m = s_base;
+  if (tid < H12_NCSTR_COLS) {
+    float cm = fkey_inv(P.ckey[tid]);
+    const bool nm = tid >= C_COL0[H12_C_NO_MOVE] && tid < C_COL0[H12_C_NO_MOVE + 1];
+    if (nm && m == 0) cm = 0.f;  // constraints.no_move returns zeros when no env is still
+    cm = fmaxf(cm, 1e-6f);       // constraint.max(dim=0).clamp(min=1e-6)
+    const float old = P.crun[tid];
+    const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
+    P.crun[tid] = run;
+    P.crun[H12_NCSTR_COLS + tid] = 1.f / run;
+    P.ckey[tid] = fkey(CAT_NEG);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    P.cmeta[0] = m;
+    P.cmeta[1] = 1;
+  }
+}
+
+// CaT, last: per env, p = min_p + clamp(c / running_max, 0, 1) (max_p - min_p) on violated columns, the max over
+// all columns scales the reward (CaTEnv.step, cat_env.py:148-153) and is returned as dones (1 where the env
+// was reset); ConstraintManager's episode statistics, logged and cleared for the envs reset this step.
+struct CatArgs {
+  float* rew;
+  const uint8_t* term;
+  const uint8_t* trunc;
+  float* cstr_prob;
+  float* log_acc;
+};
+constexpr int CAT_PBLOCK = 64;
+__global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspace W, CatArgs A) {
+  const int n = W.n;
+  const int i = blockIdx.x * CAT_PBLOCK + threadIdx.x;
+  if (i >= n) return;
+  const float* S = P.cscr;
+  // every load is issued up front (one memory round trip for the env's own rows and statistics, one more
+  // for the no_move rows of the remapped env), then branch-free arithmetic
+  float cv[H12_NCSTR_COLS], vs[H12_NCSTR], vp[H12_NCSTR];
+  constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NM1 = C_COL0[H12_C_NO_MOVE + 1];
+#pragma unroll
+  for (int col = 0; col < H12_NCSTR_COLS; ++col)
+    if (col < NM0 || col >= NM1) cv[col] = S[(size_t)col * n + i];
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) {
+    vs[t] = W.F[(size_t)(H12_F_CSTR_SUM + t) * n + i];
+    vp[t] = W.F[(size_t)(H12_F_CSTR_P + t) * n + i];
+  }
+  const float len = S[(size_t)CAT_ROW_EPLEN * n + i];
+  const int m = P.cmeta[0];
+  const int src = m > 0 ? P.clist[i % m] : -1;
+  const int srow = src >= 0 ? src : i;
+#pragma unroll
+  for (int col = NM0; col < NM1; ++col) cv[col] = src >= 0 ? S[(size_t)col * n + srow] : 0.f;
+  float pmax = 0.f;
+  float pt[H12_NCSTR];
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) {
+    pt[t] = 0.f;
+    const bool on = (P.cmask >> t) & 1u;
+#pragma unroll
+    for (int col = C_COL0[t]; col < C_COL0[t + 1]; ++col) {
+      const float c = cv[col];
+      // c / running_max as c * (1 / running_max): within 1 ulp of the division
+      const float p = P.cminp + fminf(fmaxf(c * P.crun[H12_NCSTR_COLS + col], 0.f), 1.f) * (P.cmaxp[t] - P.cminp);
+      pt[t] = fmaxf(pt[t], (on && c > 0.f) ? p : 0.f);
+    }
+    pmax = fmaxf(pmax, pt[t]);
+  }
+  A.rew[i] *= 1.f - pmax;
+  const bool reset = A.term[i] || A.trunc[i];
+  if (A.cstr_prob) A.cstr_prob[i] = reset ? 1.f : pmax;
+  const float inv_len = 1.f / len;
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) {
+    if (!((P.cmask >> t) & 1u)) continue;
+    float a = vs[t] + (pt[t] > 0.f ? 1.f : 0.f), b = vp[t] + pt[t];
+    if (reset) {
+      if (A.log_acc) {
+        atomicAdd(&A.log_acc[H12_NREW + 4 + t], a * inv_len);
+        atomicAdd(&A.log_acc[H12_NREW + 4 + H12_NCSTR + t], b * inv_len);
+      }
+      a = b = 0.f;
+    }
+    W.F[(size_t)(H12_F_CSTR_SUM + t) * n + i] = a;
+    W.F[(size_t)(H12_F_CSTR_P + t) * n + i] = b;
   }
 }
 
@@ -1452,6 +1690,7 @@ struct Handle {
   float* frame;  // [45][n] observation frame scratch between the env kernels and obs_assemble_kernel
   int* dz_cnt = nullptr;  // 3 rotating deadzone counters (UniformVelocityCommandWithDeadzone)
   uint64_t dz_step = 0;
+  void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
   std::vector<hipEvent_t> ev;  // 3 per timed step: before env kernel, between, after assembly
   size_t n_timed = 0;
@@ -1597,6 +1836,27 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
       if (c->obs_scale[t] != 1.f) return set_err(H12_E_ARG, "observation scales need the flat layout");
   P.h_target = c->base_height_target;
   P.cf_thr = c->contact_force_threshold;
+  // CaT
+  P.cat = c->cat_enable;
+  P.cmask = c->cstr_mask;
+  for (int t = 0; t < H12_NCSTR; ++t) P.cmaxp[t] = c->cstr_max_p[t];
+  P.ctau = c->cat_tau;
+  P.cminp = c->cat_min_p;
+  for (int k = 0; k < NL; ++k) {
+    if (c->cstr_joint_vel_limit[k] != c->cstr_joint_vel_limit[NL + k] ||
+        c->cstr_joint_effort_limit[k] != c->cstr_joint_effort_limit[NL + k])
+      return set_err(H12_E_ARG, "constraint joint limits must be leg-symmetric");
+    P.cvlim[k] = c->cstr_joint_vel_limit[k];
+    P.celim[k] = c->cstr_joint_effort_limit[k];
+  }
+  P.c_ff = c->cstr_foot_force_limit;
+  P.c_nm_dz = c->cstr_nomove_deadzone;
+  P.c_nm_v = c->cstr_nomove_vel;
+  P.c_or = c->cstr_orient_limit;
+  P.c_h = c->cstr_height;
+  P.c_hstd = c->cstr_height_std;
+  P.c_clr = c->cstr_clearance_min;
+  P.c_clr_dz = c->cstr_clearance_deadzone;
   return 0;
 }
 
@@ -1605,7 +1865,8 @@ int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_
 // feature level of the env kernels (Feat<K>)
 int feature_level(const KParams& P) {
   if (P.terrain) return 2;
-  return (P.task != H12_TASK_FLAT || P.env_mu || P.env_mass || P.curriculum || P.rsl || P.dz || P.push) ? 1 : 0;
+  return (P.task != H12_TASK_FLAT || P.env_mu || P.env_mass || P.curriculum || P.rsl || P.dz || P.push || P.cat) ? 1
+                                                                                                             : 0;
 }
 #define LAUNCH_K(KERNEL, ...)                                                   \
   do {                                                                          \
@@ -1715,6 +1976,24 @@ int h12env_config_default(h12env_config* c) {
   for (int t = 0; t < 6; ++t) c->obs_scale[t] = 1.f;
   c->base_height_target = 1.f;
   c->contact_force_threshold = 800.f;
+  c->cat_enable = 0;
+  c->cstr_mask = (1u << H12_NCSTR) - 1u;
+  for (int t = 0; t < H12_NCSTR; ++t) c->cstr_max_p[t] = t == H12_C_CONTACT ? 1.f : 0.25f;
+  c->cat_tau = 0.95f;
+  c->cat_min_p = 0.f;
+  const float vlim[NL] = {23.f, 23.f, 23.f, 14.f, 9.f, 9.f};  // h12_12dof.urdf joint velocity limits
+  for (int j = 0; j < H12_NJ; ++j) {
+    c->cstr_joint_vel_limit[j] = vlim[j % NL];
+    c->cstr_joint_effort_limit[j] = 1e9f;
+  }
+  c->cstr_foot_force_limit = 750.f;
+  c->cstr_nomove_deadzone = 0.2f;
+  c->cstr_nomove_vel = 6.f;
+  c->cstr_orient_limit = 0.1f;
+  c->cstr_height = 1.f;
+  c->cstr_height_std = 0.05f;
+  c->cstr_clearance_min = 0.1f;
+  c->cstr_clearance_deadzone = 0.2f;
   return 0;
 }
 
@@ -1783,6 +2062,38 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     return set_err(H12_E_ALLOC, "hipMalloc(dz_cnt): %s", hipGetErrorString(e));
   }
   h->P.dz_cnt = h->dz_cnt;
+  if (h->P.cat) {
+    const size_t nn = (size_t)n_envs;
+    const size_t bytes_cat = sizeof(float) * CAT_ROWS * nn + sizeof(int) * H12_NCSTR_COLS +
+                             sizeof(float) * 2 * H12_NCSTR_COLS + sizeof(int) * nn + sizeof(int) * 4;
+    e = hipMalloc(&h->cat_mem, bytes_cat);
+    if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
+    if (e != hipSuccess) {
+      if (h->own) (void)hipFree(state_dev);
+      (void)hipFree(h->frame);
+      (void)hipFree(h->dz_cnt);
+      delete h;
+      return set_err(H12_E_ALLOC, "hipMalloc(CaT buffers): %s", hipGetErrorString(e));
+    }
+    char* q = (char*)h->cat_mem;
+    h->P.cscr = (float*)q; q += sizeof(float) * CAT_ROWS * nn;
+    h->P.ckey = (int*)q; q += sizeof(int) * H12_NCSTR_COLS;
+    h->P.crun = (float*)q; q += sizeof(float) * 2 * H12_NCSTR_COLS;
+    h->P.clist = (int*)q; q += sizeof(int) * nn;
+    h->P.cmeta = (int*)q;
+    int keys[H12_NCSTR_COLS];
+    for (int i = 0; i < H12_NCSTR_COLS; ++i) {
+      float ninf = CAT_NEG;
+      int b;
+      memcpy(&b, &ninf, 4);
+      keys[i] = b >= 0 ? b : b ^ 0x7FFFFFFF;
+    }
+    e = hipMemcpy(h->P.ckey, keys, sizeof keys, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      h12env_destroy((h12env*)h);
+      return set_err(H12_E_HIP, "hipMemcpy(CaT keys): %s", hipGetErrorString(e));
+    }
+  }
   h->device = device;
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -1801,6 +2112,7 @@ void h12env_destroy(h12env* hh) {
   if (h->own && h->W.F) (void)hipFree(h->W.F);
   if (h->frame) (void)hipFree(h->frame);
   if (h->dz_cnt) (void)hipFree(h->dz_cnt);
+  if (h->cat_mem) (void)hipFree(h->cat_mem);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   delete h;
 }
@@ -1850,6 +2162,17 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   timing_mark(h, 0, (hipStream_t)stream);
   LAUNCH_K(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
+  if (h->P.cat) {
+    const dim3 cg((h->W.n + CAT_CHUNK - 1) / CAT_CHUNK, H12_NCSTR_COLS);
+    hipLaunchKernelGGL(cat_colmax_kernel, cg, dim3(CAT_CBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
+    HIP_TRY(hipGetLastError());
+    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, out->log_acc};
+    hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0,
+                       (hipStream_t)stream, h->P, h->W, C);
+    HIP_TRY(hipGetLastError());
+  }
   timing_mark(h, 1, (hipStream_t)stream);
   // fill = terminated | truncated: the envs reset inside the step restart their history
   int rc = launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
@@ -1920,6 +2243,14 @@ int h12env_obs_dim(const h12env* hh) {
   return P.task == H12_TASK_ROUGH ? H12_NOBS_ROUGH : H12_OBS_FRAME * P.hist;
 }
 
+int h12env_set_constraint_max_p(h12env* hh, const float* max_p, int n) {
+  Handle* h = (Handle*)hh;
+  if (!h || !max_p) return set_err(H12_E_ARG, "null argument");
+  if (n < 0 || n > H12_NCSTR) return set_err(H12_E_ARG, "n must be in 0..%d (got %d)", H12_NCSTR, n);
+  for (int t = 0; t < n; ++t) h->P.cmaxp[t] = max_p[t];
+  return 0;
+}
+
 int h12env_set_reward_weights(h12env* hh, const float* w, int n) {
   Handle* h = (Handle*)hh;
   if (!h || !w) return set_err(H12_E_ARG, "null argument");
@@ -1943,9 +2274,11 @@ int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, doub
     // state fields the kernel reads and writes, actions, reward / terminated / truncated, applied torque
     // and foot force (the ArticulationData / ContactSensor views), the noise-free frame
     double fields = 104.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0) +
-                    (P.rsl ? 8.0 : 0.0) + (P.push ? 1.0 : 0.0);
+                    (P.rsl ? 8.0 : 0.0) + (P.push ? 1.0 : 0.0) + (P.cat ? 22.0 : 0.0);
+    // CaT: the constraint scratch written and read back, the no_move list entry, reward and dones rewritten
+    const double cat_bytes = P.cat ? (double)CAT_ROWS * 4.0 * 2.0 + 4.0 + 4.0 * 2.0 + 4.0 : 0.0;
     bytes = fields * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 + (double)H12_NJ * 4.0 + 2.0 * 4.0 +
-            (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
+            (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0 + cat_bytes;
     flops = h->flops_per_env;
   } else if (kernel == 1) {
     if (rough) {

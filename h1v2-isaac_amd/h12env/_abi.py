@@ -16,8 +16,11 @@ NOBS = OBS_FRAME * NHIST
 NFOOT_PTS = 4
 NREW = 20        # reward terms the kernel implements (REWARD_FUNCS)
 NREW_FLAT = 12   # terms 0-11: the Flat / Rough tables
-NLOG = 24        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare
-ABI_VERSION = 3
+NCSTR = 10       # CaT constraint terms (CONSTRAINT_TERMS)
+NCSTR_COLS = 56
+NLOG = 44        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare,
+                 # then per constraint term the summed violation rates (10) and mean probabilities (10)
+ABI_VERSION = 4
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -32,8 +35,9 @@ NOBS_ROUGH = ROUGH_FRAME + NSCAN
 F = dict(POS=(0, 3), QUAT=(3, 4), VLIN=(7, 3), WANG=(10, 3), Q=(13, 12), QD=(25, 12), ACT=(37, 12),
          ACT_PREV=(49, 12), CMD=(61, 3), HEADING=(64, 1), CMD_TIME=(65, 1), AIR=(66, 2), CONTACT=(68, 2),
          LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16), ORIGIN=(102, 3), MU=(105, 4),
-         DMASS=(109, 1), EPSUM2=(110, 8), PUSH_TIME=(118, 1))
-NF_FLOAT = 119
+         DMASS=(109, 1), EPSUM2=(110, 8), PUSH_TIME=(118, 1), CSTR_SUM=(119, 10), CSTR_P=(129, 10),
+         SWING_H=(139, 2))
+NF_FLOAT = 141
 I = dict(EPLEN=(0, 1), PACK=(1, 1), TERRAIN=(2, 1))
 NF_INT = 3
 
@@ -52,6 +56,11 @@ REWARD_FUNCS = [
     "joint_pos_limits:hip", "contact_forces", "lin_vel_z_l2",
 ]
 assert len(REWARD_FUNCS) == NREW
+# CaT constraint terms (H12_C_*), ConstraintsCfg order of cat_env_cfg.py:336-427
+CONSTRAINT_TERMS = ["contact", "joint_position_limits", "joint_velocity_limits", "joint_torque_limits",
+                    "foot_contact_force", "no_move", "base_orientation", "base_height", "foot_contact",
+                    "foot_clearance"]
+assert len(CONSTRAINT_TERMS) == NCSTR
 
 f32 = C.c_float
 i32 = C.c_int32
@@ -161,6 +170,21 @@ class H12Config(C.Structure):
         ("obs_scale", f32 * 6),
         ("base_height_target", f32),
         ("contact_force_threshold", f32),
+        ("cat_enable", i32),
+        ("cstr_mask", C.c_uint32),
+        ("cstr_max_p", f32 * NCSTR),
+        ("cat_tau", f32),
+        ("cat_min_p", f32),
+        ("cstr_joint_vel_limit", f32 * NJ),
+        ("cstr_joint_effort_limit", f32 * NJ),
+        ("cstr_foot_force_limit", f32),
+        ("cstr_nomove_deadzone", f32),
+        ("cstr_nomove_vel", f32),
+        ("cstr_orient_limit", f32),
+        ("cstr_height", f32),
+        ("cstr_height_std", f32),
+        ("cstr_clearance_min", f32),
+        ("cstr_clearance_deadzone", f32),
     ]
 
 
@@ -173,6 +197,7 @@ class H12StepOut(C.Structure):
         ("log_acc", C.c_void_p),
         ("applied_torque", C.c_void_p),
         ("foot_force", C.c_void_p),
+        ("cstr_prob", C.c_void_p),
     ]
 
 
@@ -230,6 +255,8 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_obs_dim.restype = C.c_int
     lib.h12env_set_reward_weights.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
     lib.h12env_set_reward_weights.restype = C.c_int
+    lib.h12env_set_constraint_max_p.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    lib.h12env_set_constraint_max_p.restype = C.c_int
     lib.h12env_step_cost.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.h12env_step_cost.restype = C.c_int
     lib.h12env_kernel_cost.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -265,5 +292,5 @@ EXPORTED_SYMBOLS = [
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
-    "h12env_set_reward_weights",
+    "h12env_set_reward_weights", "h12env_set_constraint_max_p",
 ]

@@ -19,8 +19,8 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass, field, replace
 
-from ._abi import (ABI_VERSION, MODE_ISAACLAB, MODE_MUJOCO, NHIST, NJ, NREW, REWARD_FUNCS, REWARD_TERMS, TASK_FLAT,
-                   TASK_ROUGH, H12Config)
+from ._abi import (ABI_VERSION, CONSTRAINT_TERMS, MODE_ISAACLAB, MODE_MUJOCO, NCSTR, NHIST, NJ, NREW, REWARD_FUNCS,
+                   REWARD_TERMS, TASK_FLAT, TASK_ROUGH, H12Config)
 from .model import DEFAULT_JOINT_POS
 
 
@@ -103,6 +103,11 @@ class RobotCfg:
     init_pos: tuple = (0.0, 0.0, 1.05)
     joint_pos: tuple = tuple(DEFAULT_JOINT_POS)
     soft_joint_pos_limit_factor: float = 0.9
+    # ArticulationData.joint_vel_limits / joint_effort_limits as the sim holds them: the URDF velocity limits
+    # (h12_12dof.urdf:53-198, USD import keeps them) and, for explicit actuator models, IsaacLab's 1e9 effort
+    # limit in the solver; read by the CaT joint_velocity_limits / joint_torque_limits constraints
+    joint_vel_limits: tuple = (23.0, 23.0, 23.0, 14.0, 9.0, 9.0) * 2
+    joint_effort_limits_sim: tuple = (1.0e9,) * 12
     actuators: dict = field(default_factory=lambda: {
         "legs": ActuatorGroupCfg([".*_hip_yaw_joint", ".*_hip_roll_joint", ".*_hip_pitch_joint"], 220.0, 200.0, 2.5),
         "knees": ActuatorGroupCfg([".*_knee_joint"], 360.0, 300.0, 4.0),
@@ -192,7 +197,11 @@ class RewTerm:
     isaaclab mdp function, qualified by its joint set / frame where the kernel hard-codes one)."""
     weight: float
     params: dict = field(default_factory=dict)
-    func: str | None = None
+    func: "str | tuple | None" = None   # one kernel term, or several summed (one joint set split over ids)
+
+
+def _funcs(v) -> tuple:
+    return tuple(v) if isinstance(v, (tuple, list)) else (v,)
 
 
 _FLAT_FUNCS = dict(zip(REWARD_TERMS, REWARD_FUNCS[:len(REWARD_TERMS)]))
@@ -265,7 +274,7 @@ class RewardsCfg:
             if not isinstance(value, RewTerm):
                 raise TypeError(f"reward term {name!r} must be a RewTerm or None")
             func = value.func or (self._terms[name].func if self._terms.get(name) is not None else _FLAT_FUNCS.get(name))
-            if func not in REWARD_FUNCS:
+            if func is None or any(f not in REWARD_FUNCS for f in _funcs(func)):
                 raise AttributeError(f"reward term {name!r}: func {func!r} is not a kernel term {REWARD_FUNCS}")
             value.func = func
         self._terms[name] = value
@@ -274,16 +283,18 @@ class RewardsCfg:
         return list(self._terms.items())
 
     def active(self):
-        """(name, kernel id) of the terms the RewardManager holds (None terms removed), in cfg order."""
+        """(name, kernel ids) of the terms the RewardManager holds (None terms removed), in cfg order."""
         out, seen = [], {}
         for k, v in self._terms.items():
             if v is None:
                 continue
-            kid = REWARD_FUNCS.index(v.func)
-            if kid in seen:
-                raise ValueError(f"reward terms {seen[kid]!r} and {k!r} map to the same kernel term {v.func!r}")
-            seen[kid] = k
-            out.append((k, kid))
+            ids = tuple(REWARD_FUNCS.index(f) for f in _funcs(v.func))
+            for kid in ids:
+                if kid in seen:
+                    raise ValueError(f"reward terms {seen[kid]!r} and {k!r} map to the same kernel term "
+                                     f"{REWARD_FUNCS[kid]!r}")
+                seen[kid] = k
+            out.append((k, ids))
         return out
 
     def to_dict(self):
@@ -333,6 +344,91 @@ class MassEventCfg:
 
 
 @dataclass
+class ConstraintTerm:
+    """ConstraintTermCfg (T/utils/cat/manager_constraint_cfg.py): `func` names the kernel constraint
+    (one of _abi.CONSTRAINT_TERMS), max_p its maximum termination probability, params its limits."""
+    func: str
+    max_p: float
+    params: dict = field(default_factory=dict)
+
+
+def _cat_constraints():
+    """cat_env_cfg.py:336-427 (ConstraintsCfg order)."""
+    T = ConstraintTerm
+    return {
+        "contact": T("contact", 1.0),
+        "joint_position_limits": T("joint_position_limits", 0.25),
+        "joint_velocity_limits": T("joint_velocity_limits", 0.25),
+        "joint_torque_limits": T("joint_torque_limits", 0.25),
+        "foot_contact_force": T("foot_contact_force", 0.25, {"limit": 750.0}),
+        "no_move": T("no_move", 0.25, {"velocity_deadzone": 0.2, "joint_vel_limit": 6.0}),
+        "base_orientation": T("base_orientation", 0.25, {"limit": 0.1}),
+        "base_height": T("base_height", 0.25, {"height": 1.0, "std": 0.05}),
+        "foot_contact": T("foot_contact", 0.25),
+        "foot_clearance": T("foot_clearance", 0.25, {"min_height": 0.1, "velocity_deadzone": 0.2}),
+    }
+
+
+class ConstraintsCfg:
+    """Attribute-access container of the ConstraintManager's terms (cfg order); a term set to None is removed."""
+
+    def __init__(self, terms=None):
+        object.__setattr__(self, "_terms", terms if terms is not None else _cat_constraints())
+
+    def __getattr__(self, name):
+        if name.startswith("__") or name == "_terms":
+            raise AttributeError(name)
+        try:
+            return self._terms[name]
+        except KeyError as e:
+            raise AttributeError(name) from e
+
+    def __getstate__(self):
+        return {"_terms": self._terms}
+
+    def __setstate__(self, st):
+        object.__setattr__(self, "_terms", st["_terms"])
+
+    def __setattr__(self, name, value):
+        if value is not None and (not isinstance(value, ConstraintTerm) or value.func not in CONSTRAINT_TERMS):
+            raise AttributeError(f"constraint {name!r} must be a ConstraintTerm on one of {CONSTRAINT_TERMS}")
+        self._terms[name] = value
+
+    def items(self):
+        return list(self._terms.items())
+
+    def active(self):
+        """(name, kernel constraint id) in cfg order."""
+        out, seen = [], set()
+        for k, v in self._terms.items():
+            if v is None:
+                continue
+            cid = CONSTRAINT_TERMS.index(v.func)
+            if cid in seen:
+                raise ValueError(f"two constraints map to the kernel term {v.func!r}")
+            seen.add(cid)
+            out.append((k, cid))
+        return out
+
+    def to_dict(self):
+        return {k: (None if v is None else {"func": v.func, "max_p": v.max_p, "params": dict(v.params)})
+                for k, v in self.items()}
+
+
+@dataclass
+class ConstraintPTerm:
+    """modify_constraint_p (T/utils/cat/curriculums.py:16-42): max_p = 1 / (20 + progress (1 / init_max_p - 20)),
+    progress = min(common_step_counter / num_steps, 1)."""
+    term_name: str
+    num_steps: int
+    init_max_p: float
+
+    def max_p(self, step: int) -> float:
+        progress = min(step / self.num_steps, 1.0)
+        return 1.0 / (20 + progress * (1 / self.init_max_p - 20))
+
+
+@dataclass
 class RewardWeightTerm:
     """modify_reward_weight (isaaclab mdp.curriculums): once common_step_counter > num_steps, the
     reward term's weight becomes `weight`."""
@@ -345,6 +441,7 @@ class RewardWeightTerm:
 class CurriculumCfg:
     terrain_levels: bool = False  # terrain_levels_vel (velocity_env_cfg.py:271-275)
     reward_weights: list = field(default_factory=list)  # [RewardWeightTerm] (rsl_env_cfg.py:448-501)
+    constraint_p: list = field(default_factory=list)    # [ConstraintPTerm] (cat_env_cfg.py:466-520)
 
 
 @dataclass
@@ -365,6 +462,7 @@ class H12FlatEnvCfg:
     terminations: TerminationsCfg = field(default_factory=TerminationsCfg)
     events: EventsCfg = field(default_factory=EventsCfg)
     curriculum: CurriculumCfg = field(default_factory=CurriculumCfg)
+    constraints: "ConstraintsCfg | None" = None   # the CaT task's ConstraintManager terms
     fix_base: bool = False
 
     @property
@@ -484,18 +582,19 @@ class H12FlatEnvCfg:
             c.rew_w[t] = 0.0
         stds = set()
         c.track_std, c.air_time_threshold, c.base_height_target, c.contact_force_threshold = 0.5, 0.4, 1.0, 800.0
-        for name, kid in self.rewards.active():
+        for name, kids in self.rewards.active():
             term = terms[name]
-            c.rew_w[kid] = term.weight
-            f = REWARD_FUNCS[kid]
-            if f.startswith("track_"):
-                stds.add(float(term.params.get("std", 0.5)))
-            elif f == "feet_air_time_positive_biped":
-                c.air_time_threshold = term.params.get("threshold", 0.4)
-            elif f == "base_height_l2":
-                c.base_height_target = term.params.get("target_height", 1.0)
-            elif f == "contact_forces":
-                c.contact_force_threshold = term.params.get("threshold", 1.0)
+            for kid in kids:
+                c.rew_w[kid] = term.weight
+                f = REWARD_FUNCS[kid]
+                if f.startswith("track_"):
+                    stds.add(float(term.params.get("std", 0.5)))
+                elif f == "feet_air_time_positive_biped":
+                    c.air_time_threshold = term.params.get("threshold", 0.4)
+                elif f == "base_height_l2":
+                    c.base_height_target = term.params.get("target_height", 1.0)
+                elif f == "contact_forces":
+                    c.contact_force_threshold = term.params.get("threshold", 1.0)
         if len(stds) > 1:
             raise ValueError(f"the tracking terms must share one std (got {sorted(stds)})")
         if stds:
@@ -514,8 +613,43 @@ class H12FlatEnvCfg:
         c.illegal_contact_knees = int(self.terminations.base_contact_knees)
         c.illegal_contact_torso = int(self.terminations.base_contact_torso)
         c.seed = (self.seed if self.seed is not None else 0) & 0xFFFFFFFFFFFFFFFF
+        self._constraints_to_c(c)
         assert NJ == 12
         return c
+
+    def _constraints_to_c(self, c):
+        # C defaults (h12env_config_default) when the task has no ConstraintManager
+        c.cat_enable, c.cstr_mask, c.cat_tau, c.cat_min_p = 0, (1 << NCSTR) - 1, 0.95, 0.0
+        for t in range(NCSTR):
+            c.cstr_max_p[t] = 1.0 if t == 0 else 0.25
+        c.cstr_joint_vel_limit[:] = self.robot.joint_vel_limits
+        c.cstr_joint_effort_limit[:] = self.robot.joint_effort_limits_sim
+        c.cstr_foot_force_limit, c.cstr_nomove_deadzone, c.cstr_nomove_vel = 750.0, 0.2, 6.0
+        c.cstr_orient_limit, c.cstr_height, c.cstr_height_std = 0.1, 1.0, 0.05
+        c.cstr_clearance_min, c.cstr_clearance_deadzone = 0.1, 0.2
+        if self.constraints is None:
+            return
+        c.cat_enable = 1
+        c.cstr_mask = 0
+        terms = dict(self.constraints.items())
+        for name, cid in self.constraints.active():
+            t = terms[name]
+            c.cstr_mask |= 1 << cid
+            c.cstr_max_p[cid] = t.max_p
+            p = t.params
+            f = CONSTRAINT_TERMS[cid]
+            if f == "foot_contact_force":
+                c.cstr_foot_force_limit = p.get("limit", 750.0)
+            elif f == "no_move":
+                c.cstr_nomove_deadzone = p.get("velocity_deadzone", 0.2)
+                c.cstr_nomove_vel = p.get("joint_vel_limit", 6.0)
+            elif f == "base_orientation":
+                c.cstr_orient_limit = p.get("limit", 0.1)
+            elif f == "base_height":
+                c.cstr_height, c.cstr_height_std = p.get("height", 1.0), p.get("std", 0.05)
+            elif f == "foot_clearance":
+                c.cstr_clearance_min = p.get("min_height", 0.1)
+                c.cstr_clearance_deadzone = p.get("velocity_deadzone", 0.2)
 
 
 @dataclass
@@ -617,6 +751,57 @@ class H12RslEnvCfg_PLAY(H12RslEnvCfg):
         self.observations.policy.enable_corruption = False
         r = self.commands.base_velocity.ranges
         r.lin_vel_x, r.lin_vel_y, r.ang_vel_z = (0.5, 0.5), (0.0, 0.0), (0.0, 0.0)
+
+
+@dataclass
+class H12CaTEnvCfg(H12FlatEnvCfg):
+    """Isaac-Velocity-CaT-Flat-H12_12dof-v0 (H12_12dof_EnvCfg, cat_env_cfg.py:528-565): Constraints as
+    Terminations on the delayed-PD robot -- deadzone commands (0.2), 270-float observation (history 6,
+    scales), friction + torso-mass randomisation, pushes, a 7-term reward and the 10 constraints whose
+    termination probability scales the reward and is returned as dones (CaTEnv.step, cat_env.py:95-193)."""
+
+    def __post_init__(self):
+        MAX_CURRICULUM_ITERATIONS = 5000
+        self.sim.static_friction = self.sim.dynamic_friction = 1.0
+        self.actions.joint_pos.scale = 0.25                                   # cat_env_cfg.py:141
+        self.commands.base_velocity = UniformVelocityCommandWithDeadzoneCfg(
+            resampling_time_range=(5.0, 8.0), rel_standing_envs=0.02, rel_heading_envs=1.0, heading_command=False,
+            heading_control_stiffness=1.0, ranges=Ranges((-1.0, 1.0), (-1.0, 1.0), (-1.0, 1.0)),
+            velocity_deadzone=0.2)                                            # :99-116
+        po = self.observations.policy
+        po.history_length = 6                                                 # :216
+        po.scales = {"base_ang_vel": 0.25, "joint_vel": 0.05}                 # :159, 188
+        self.events.physics_material = MaterialEventCfg((0.1, 1.25), (0.1, 1.25), 64)   # :231-240
+        self.events.add_base_mass = MassEventCfg(".*torso_link", (0.0, 6.0), "add")     # :242-251
+        self.events.push_robot = PushEventCfg((5.0, 8.0), {"x": (-1.0, 1.0), "y": (-1.0, 1.0)})  # :288-293
+        T = RewTerm
+        self.rewards = RewardsCfg({                                           # :300-331
+            "track_lin_vel_xy_exp": T(1.0, {"command_name": "base_velocity", "std": math.sqrt(0.25)},
+                                      "track_lin_vel_xy_exp"),
+            "track_ang_vel_z_exp": T(0.5, {"command_name": "base_velocity", "std": math.sqrt(0.25)},
+                                     "track_ang_vel_z_exp"),
+            "dof_torques_l2": T(-1.0e-5, {}, "joint_torques_l2"),
+            "joint_acc_l2": T(-2.5e-7, {}, "joint_acc_l2"),
+            "joint_vel_l2": T(-1.0e-3, {}, "joint_vel_l2"),
+            "action_rate_l2": T(-0.01, {}, "action_rate_l2"),
+            "joint_deviation_l1": T(-0.1, {}, ("joint_deviation_l1:hip", "joint_deviation_l1:ankle")),
+        })
+        self.constraints = ConstraintsCfg()
+        n = 24 * MAX_CURRICULUM_ITERATIONS                                    # :466-520
+        self.curriculum.constraint_p = [ConstraintPTerm(k, n, 0.25) for k in (
+            "joint_position_limits", "joint_velocity_limits", "joint_torque_limits", "foot_contact_force", "no_move",
+            "base_orientation", "base_height", "foot_contact", "foot_clearance")]
+
+
+@dataclass
+class H12CaTEnvCfg_PLAY(H12CaTEnvCfg):
+    """cat_env_cfg.py:568-583: 100 envs, zero commands."""
+
+    def __post_init__(self):
+        super().__post_init__()
+        self.scene.num_envs = 100
+        r = self.commands.base_velocity.ranges
+        r.lin_vel_x, r.lin_vel_y, r.ang_vel_z = (0.0, 0.0), (0.0, 0.0), (0.0, 0.0)
 
 
 def mujoco_cfg(**kw) -> H12FlatEnvCfg:

@@ -23,7 +23,7 @@ import torch
 
 from . import _abi
 from ._abi import F as FIELDS
-from ._abi import NF_FLOAT, NF_INT, NJ, NLOG, NOBS_ROUGH, NREW, H12StepOut, check, load_library
+from ._abi import NCSTR, NF_FLOAT, NF_INT, NJ, NLOG, NOBS_ROUGH, NREW, H12StepOut, check, load_library
 from .cfg import H12FlatEnvCfg
 from .model import body_names, build_model, joint_names
 
@@ -46,14 +46,20 @@ class _LazyLog(dict):
     """extras["log"]: IsaacLab's Episode_Reward/* and Episode_Termination/* values, materialised on
     first access from the step's device-side accumulator (no host sync inside step())."""
 
-    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, terms: list, extra: dict | None = None):
+    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, terms: list, term_map: torch.Tensor,
+                 cstr: list | None = None, extra: dict | None = None):
         super().__init__()
         self._acc = acc
         self._T = max_episode_length_s
-        self._terms = terms          # [(cfg name, kernel id)] in RewardManager order
+        self._terms = terms          # [(cfg name, kernel ids)] in RewardManager order
+        self._map = term_map         # (terms, NREW) 0/1: a cfg term sums its kernel ids
+        self._cstr = cstr or []      # [(constraint name, kernel constraint id)]
         self._extra = extra or {}
         self._keys = [f"Episode_Reward/{t}" for t, _ in terms] + [
-            "Episode_Termination/time_out", "Episode_Termination/base_contact"] + list(self._extra)
+            "Episode_Termination/time_out", "Episode_Termination/base_contact"]
+        self._keys += [f"Episode_Constraint_violation/{c}" for c, _ in self._cstr]
+        self._keys += [f"Episode_Constraint_probability/{c}" for c, _ in self._cstr]
+        self._keys += list(self._extra)
         self._done = False
 
     def _fill(self):
@@ -61,9 +67,12 @@ class _LazyLog(dict):
             return
         a = self._acc
         n = a[NREW].clamp(min=1.0)
-        ids = torch.tensor([k for _, k in self._terms], device=a.device, dtype=torch.long)
-        vals = torch.cat([a[ids] / n / self._T, a[NREW + 1:NREW + 3]])
-        nt = len(self._terms) + 2
+        parts = [self._map @ a[:NREW] / n / self._T, a[NREW + 1:NREW + 3]]
+        if self._cstr:
+            cid = torch.tensor([k for _, k in self._cstr], device=a.device, dtype=torch.long)
+            parts += [a[NREW + 4 + cid] / n * 100.0, a[NREW + 4 + NCSTR + cid] / n]
+        vals = torch.cat(parts)
+        nt = len(self._terms) + 2 + 2 * len(self._cstr)
         for i, k in enumerate(self._keys[:nt]):
             dict.__setitem__(self, k, vals[i])
         for k, f in self._extra.items():
@@ -131,6 +140,30 @@ class _RewardManager:
     def set_term_cfg(self, name, term_cfg):
         setattr(self._env.cfg.rewards, name, term_cfg)
         self._env._push_reward_weights()
+
+
+class _ConstraintManager:
+    """ConstraintManager surface (T/utils/cat/constraint_manager.py:126-269) over the kernel's constraint terms:
+    active terms in order, get/set_term_cfg (max_p reaches the kernel via h12env_set_constraint_max_p)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    @property
+    def active_terms(self):
+        return [k for k, _ in self._env.cfg.constraints.active()]
+
+    def get_term_cfg(self, name):
+        t = dict(self._env.cfg.constraints.items()).get(name)
+        if t is None:
+            raise ValueError(f"Constraint term '{name}' not found.")
+        return t
+
+    def set_term_cfg(self, name, term_cfg):
+        if name not in self.active_terms:
+            raise ValueError(f"Constraint term '{name}' not found.")
+        setattr(self._env.cfg.constraints, name, term_cfg)
+        self._env._push_constraint_p()
 
 
 class _ActionManager:
@@ -245,8 +278,15 @@ class H12VelocityEnv:
         self.observation_manager = _ObservationManager(self)
         self.action_manager = _ActionManager(self)
         self.reward_manager = _RewardManager(self)
-        self._reward_terms = self.cfg.rewards.active()
+        self._set_reward_terms()
         self._rw_pending = list(getattr(self.cfg.curriculum, "reward_weights", []) or [])
+        # CaT (Isaac-Velocity-CaT-Flat-H12_12dof-v0): constraint probabilities -> dones
+        self._cat = self.cfg.constraints is not None
+        self._cstr_terms = self.cfg.constraints.active() if self._cat else []
+        self._cp_terms = list(getattr(self.cfg.curriculum, "constraint_p", []) or []) if self._cat else []
+        if self._cat:
+            self.constraint_manager = _ConstraintManager(self)
+            self._dones = torch.zeros(n, device=self.device)
         self._data = _ArticulationData(self)
         self.scene.articulations = {"robot": SimpleNamespace(data=self._data, joint_names=self._data.joint_names,
                                                              body_names=self._data.body_names,
@@ -338,9 +378,28 @@ class H12VelocityEnv:
                                                        C.c_void_p(self._t_origins.data_ptr()), rows, cols),
               "h12env_set_terrain")
 
+    def _set_reward_terms(self):
+        self._reward_terms = self.cfg.rewards.active()
+        m = torch.zeros(len(self._reward_terms), NREW, device=self.device)
+        for i, (_, ids) in enumerate(self._reward_terms):
+            m[i, list(ids)] = 1.0
+        self._reward_map = m
+
+    def _push_constraint_p(self):
+        c = self.cfg.to_c()
+        p = (C.c_float * NCSTR)(*c.cstr_max_p)
+        check(self._lib, self._lib.h12env_set_constraint_max_p(self._h, p, NCSTR), "h12env_set_constraint_max_p")
+
+    def _constraint_curriculum(self):
+        """modify_constraint_p runs in _reset_idx after the constraints of a step: step t uses the max_p
+        computed with common_step_counter t - 1 (the first step: the initial reset's counter 0)."""
+        for t in self._cp_terms:
+            self.constraint_manager.get_term_cfg(t.term_name).max_p = t.max_p(self.common_step_counter - 1)
+        self._push_constraint_p()
+
     def _push_reward_weights(self):
         self._ccfg = self.cfg.to_c()
-        self._reward_terms = self.cfg.rewards.active()
+        self._set_reward_terms()
         w = (C.c_float * NREW)(*self._ccfg.rew_w)
         check(self._lib, self._lib.h12env_set_reward_weights(self._h, w, NREW), "h12env_set_reward_weights")
 
@@ -395,6 +454,8 @@ class H12VelocityEnv:
         self.common_step_counter += 1
         if self._rw_pending:
             self._reward_curriculum()
+        if self._cp_terms:
+            self._constraint_curriculum()
         prev = self._obs[self._k]
         self._k ^= 1
         obs = self._obs[self._k]
@@ -410,14 +471,18 @@ class H12VelocityEnv:
         o.log_acc = acc.data_ptr()
         o.applied_torque = self._applied_torque.data_ptr()
         o.foot_force = None
+        o.cstr_prob = self._dones.data_ptr() if self._cat else None
         rc = self._lib.h12env_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(prev.data_ptr()), C.byref(o),
                                    self.common_step_counter, self._stream())
         if rc:
             check(self._lib, rc, "h12env_step")
         extra = {"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()} if self.terrain is not None else None
-        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, self._reward_terms, extra),
+        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, self._reward_terms, self._reward_map,
+                                       self._cstr_terms, extra),
                        "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
+        if self._cat:  # CaTEnv.step: dones = constraint termination probability, 1 where reset (cat_env.py:153-193)
+            return {"policy": obs_out}, self.reward_buf, self._dones, self.reset_time_outs, self.extras
         return {"policy": obs_out}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
 
     def step_physics(self, q_ref: torch.Tensor, n_substeps: int):

@@ -65,3 +65,19 @@ gym.register(
         "rsl_rl_cfg_entry_point": f"{agents.__name__}:H12_12dof_FlatPPORunnerCfg",
     },
 )
+
+# h12_12dof/__init__.py:64-83: Constraints-as-Terminations (the env class returns the constraint termination
+# probability as dones; trained by the reference with CleanRL's PPO, which this build does not ship)
+gym.register(
+    id="Isaac-Velocity-CaT-Flat-H12_12dof-v0",
+    entry_point="h12env.cat:CaTEnv",
+    disable_env_checker=True,
+    kwargs={"env_cfg_entry_point": "h12env.cfg:H12CaTEnvCfg"},
+)
+
+gym.register(
+    id="Isaac-Velocity-CaT-Flat-H12_12dof-Play-v0",
+    entry_point="h12env.cat:CaTEnv",
+    disable_env_checker=True,
+    kwargs={"env_cfg_entry_point": "h12env.cfg:H12CaTEnvCfg_PLAY"},
+)

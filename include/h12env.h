@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 3
+#define H12ENV_ABI_VERSION 4
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -48,7 +48,11 @@ extern "C" {
 #define H12_NFOOT_PTS 4    /* sole contact spheres per foot (URDF rods, h12_12dof.urdf:168-191) */
 #define H12_NREW 20        /* reward terms the kernel implements (union of the Flat / Rough / Rsl tables) */
 #define H12_NREW_FLAT 12   /* terms 0-11: the Flat / Rough tables */
-#define H12_NLOG 24        /* log accumulator: 20 episode sums, count, time-out / base-contact counts, spare */
+#define H12_NCSTR 10       /* CaT constraint terms (cat_env_cfg.py:336-427, ConstraintsCfg order) */
+#define H12_NCSTR_COLS 56  /* their columns: 1 + 12 + 12 + 12 + 2 + 12 + 1 + 1 + 1 + 2 */
+#define H12_NLOG 44        /* log accumulator: 20 episode reward sums, reset count, time-out / base-contact counts,
+                              spare, then per constraint term the sums over reset envs of the episode's
+                              violation rate (10) and mean probability (10) */
 /* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:128-188): no history, base_lin_vel
  * first, height scan last (velocity_env_cfg.py:118-137) */
 #define H12_ROUGH_FRAME 48 /* lin_vel 3, ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -97,6 +101,20 @@ enum {
   H12_R_DOF_POS_LIMITS_HIP,   /* joint_pos_limits (hip yaw/roll)          rsl_env_cfg.py:380-386 */
   H12_R_CONTACT_FORCES,       /* contact_forces: sum_f max(max_h|F|-thr,0) rsl_env_cfg.py:395-405 */
   H12_R_LIN_VEL_Z_L2          /* lin_vel_z_l2 (v_b,z^2)                   velocity_env_cfg.py:236 */
+};
+
+/* CaT constraint terms (Constraints-as-Terminations, T/utils/cat/constraints.py; cfg cat_env_cfg.py:336-427) */
+enum {
+  H12_C_CONTACT = 0,          /* contact: any illegal body in contact (max_p 1.0)            1 column */
+  H12_C_JOINT_POS_LIMITS,     /* max(soft_lo - q, q - soft_hi)                              12 columns */
+  H12_C_JOINT_VEL_LIMITS,     /* |qd| - joint_vel_limits                                    12 columns */
+  H12_C_JOINT_TORQUE_LIMITS,  /* |applied_torque| - joint_effort_limits                     12 columns */
+  H12_C_FOOT_CONTACT_FORCE,   /* max_h |F_foot| - 750                                        2 columns */
+  H12_C_NO_MOVE,              /* |qd| - 6 while all |cmd| < deadzone (rows remapped, see DESIGN) 12 columns */
+  H12_C_BASE_ORIENTATION,     /* |g_b,xy| - 0.1                                              1 column */
+  H12_C_BASE_HEIGHT,          /* z outside height +- std                                     1 column */
+  H12_C_FOOT_CONTACT,         /* number of feet in contact not in {1, 2}                     1 column */
+  H12_C_FOOT_CLEARANCE        /* (min_height - swing max height) at touchdown, command active 2 columns */
 };
 
 /* Model constants (filled from h12env/assets/h12_12dof_model.json, generated from the MJCF). */
@@ -186,6 +204,21 @@ typedef struct h12env_config {
   float obs_scale[6];          /* per-term scale after noise: ang_vel, gravity, command, q-q0, qd, action */
   float base_height_target;    /* base_height_l2 target (1.0) */
   float contact_force_threshold; /* contact_forces threshold (800 N) */
+  /* CaT task (ABI 4; T/utils/cat, cat_env_cfg.py): constraint probabilities scale the reward and are
+   * returned as dones (h12env_step_out.cstr_prob) */
+  int32_t cat_enable;
+  uint32_t cstr_mask;          /* bit t: constraint term t (H12_C_*) active */
+  float cstr_max_p[H12_NCSTR]; /* per-term maximum termination probability (curriculum: h12env_set_constraint_max_p) */
+  float cat_tau, cat_min_p;    /* running-max Polyak factor 0.95, minimum probability 0 (constraint_manager.py:26) */
+  float cstr_joint_vel_limit[H12_NJ];    /* ArticulationData.joint_vel_limits (URDF velocity 23 / 14 / 9 rad/s) */
+  float cstr_joint_effort_limit[H12_NJ]; /* ArticulationData.joint_effort_limits (explicit actuators: 1e9) */
+  float cstr_foot_force_limit;  /* 750 N */
+  float cstr_nomove_deadzone;   /* 0.2 */
+  float cstr_nomove_vel;        /* 6.0 rad/s */
+  float cstr_orient_limit;      /* 0.1 */
+  float cstr_height, cstr_height_std; /* 1.0, 0.05 */
+  float cstr_clearance_min;     /* 0.1 m */
+  float cstr_clearance_deadzone;/* 0.2 */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */
@@ -212,7 +245,10 @@ enum {
   H12_F_DMASS = 109,    /* 1  mass added at the torso COM (per_env_mass) */
   H12_F_EPSUM2 = 110,   /* 8  episode sums of reward terms 12-19 */
   H12_F_PUSH_TIME = 118,/* 1  push_robot interval time left */
-  H12_NF_FLOAT = 119
+  H12_F_CSTR_SUM = 119, /* 10 CaT: episode count of steps with the term violated (max prob > 0) */
+  H12_F_CSTR_P = 129,   /* 10 CaT: episode sum of the term's max probability */
+  H12_F_SWING_H = 139,  /* 2  CaT foot_clearance: max foot height of the current swing (left, right) */
+  H12_NF_FLOAT = 141
 };
 enum {
   H12_I_EPLEN = 0,      /* episode_length_buf (int32) */
@@ -231,6 +267,8 @@ typedef struct h12env_step_out {
   float* log_acc;          /* H12_NLOG floats, accumulated with atomics (caller zeroes) */
   float* applied_torque;   /* N x 12, last physics step (ArticulationData.applied_torque) */
   float* foot_force;       /* N x 2,  |net contact force| of the feet, last physics step */
+  float* cstr_prob;        /* N, CaT task: the dones CaTEnv.step returns (constraint termination probability,
+                              1 for envs reset this step); the reward is already scaled by 1 - p */
 } h12env_step_out;
 
 typedef struct h12env h12env;
@@ -271,6 +309,9 @@ int h12env_obs_dim(const h12env* h);
 /* Replace the reward weights (n <= H12_NREW floats, indexed by H12_R_*) for the following steps:
  * CurriculumManager's modify_reward_weight (rsl_env_cfg.py:448-501) without recreating the handle. */
 int h12env_set_reward_weights(h12env* h, const float* w, int n);
+/* Replace the constraint terms' max_p (n <= H12_NCSTR) for the following steps: the CaT curriculum
+ * modify_constraint_p (T/utils/cat/curriculums.py:16-42). */
+int h12env_set_constraint_max_p(h12env* h, const float* max_p, int n);
 /* Algorithmic accounting of one env step for the roofline report (both kernels of h12env_step). */
 int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_env);
 /* Per-kernel accounting: kernel 0 = the env kernel of h12env_step (physics + MDP), 1 = the observation

@@ -7,6 +7,7 @@
 #include "h12_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -1004,16 +1005,136 @@ int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t 
 
 static double sq(double x) { return x * x; }
 
+/* ---------------------------------------------------------------- CaT (T/utils/cat, cat_env_cfg.py) */
+enum { CAT_ROW_NOMOVE = H12_NCSTR_COLS, CAT_ROW_EPLEN = H12_NCSTR_COLS + 1, CAT_ROWS = H12_NCSTR_COLS + 2 };
+static const int C_COL0[H12_NCSTR + 1] = {0, 1, 13, 25, 37, 39, 51, 52, 53, 54, 56};
+/* CaT.running_maxes, carried from one orc_env_step to the next (process-global, like the kernel's buffer) */
+static double g_crun[H12_NCSTR_COLS];
+static int g_crun_init = 0;
+static double* g_cs_last = NULL;  /* the last step's raw constraints [CAT_ROWS][n] (tests) */
+static int g_cs_n = 0;
+void orc_cat_reset(void) { g_crun_init = 0; }
+int orc_cat_last_constraints(double* out, int n) {
+  if (!g_cs_last || n != g_cs_n) return -1;
+  memcpy(out, g_cs_last, sizeof(double) * (size_t)CAT_ROWS * (size_t)n);
+  return 0;
+}
+void orc_cat_running_max(double out[H12_NCSTR_COLS]) { memcpy(out, g_crun, sizeof g_crun); }
+
+/* constraints.py:18-308 for one env on its pre-reset state; cs is [CAT_ROWS][n] */
+static void cat_constraints(const h12env_model* m, const h12env_config* c, const orc_env* e, const double tau[NJ],
+                            const double fmax_foot[2], int term, const double gb[3], int n, int i, float* F,
+                            double step_dt, double* cs) {
+#define CS(col) cs[(size_t)(col) * n + i]
+  for (int j = 0; j < NJ; ++j) {
+    double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+    double q = e->p.q[j], qd = fabs(e->p.qd[j]);
+    double lo_v = (mid - half) - q, hi_v = q - (mid + half);
+    CS(C_COL0[H12_C_JOINT_POS_LIMITS] + j) = lo_v > hi_v ? lo_v : hi_v;
+    CS(C_COL0[H12_C_JOINT_VEL_LIMITS] + j) = qd - c->cstr_joint_vel_limit[j];
+    CS(C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j) = fabs(tau[j]) - c->cstr_joint_effort_limit[j];
+    CS(C_COL0[H12_C_NO_MOVE] + j) = qd - c->cstr_nomove_vel;
+  }
+  kin_t k;
+  kinematics(m, &e->p, &k);
+  int active = fabs(e->cmd[0]) > c->cstr_clearance_deadzone || fabs(e->cmd[1]) > c->cstr_clearance_deadzone ||
+               fabs(e->cmd[2]) > c->cstr_clearance_deadzone;
+  int nfeet = 0;
+  for (int f = 0; f < 2; ++f) {
+    CS(C_COL0[H12_C_FOOT_CONTACT_FORCE] + f) = fmax_foot[f] - c->cstr_foot_force_limit;
+    nfeet += fmax_foot[f] > 1.0;
+    /* foot_clearance: touchdown = compute_first_contact(step_dt); swing max height of the ankle-roll link */
+    int touchdown = e->con[f] > 0 && e->con[f] < step_dt + 1e-8;
+    float* sw = &F[(size_t)(H12_F_SWING_H + f) * n + i];
+    double sh = *sw, foot_z = k.p[6 * f + 6][2];
+    CS(C_COL0[H12_C_FOOT_CLEARANCE] + f) = (touchdown && active) ? c->cstr_clearance_min - sh : 0.0;
+    *sw = (float)(touchdown ? 0.0 : (foot_z > sh ? foot_z : sh));
+  }
+  CS(C_COL0[H12_C_CONTACT]) = term ? 1.0 : 0.0;
+  CS(C_COL0[H12_C_BASE_ORIENTATION]) = sqrt(sq(gb[0]) + sq(gb[1])) - c->cstr_orient_limit;
+  double z = e->p.pos[2];
+  CS(C_COL0[H12_C_BASE_HEIGHT]) = (z < c->cstr_height - c->cstr_height_std || z > c->cstr_height + c->cstr_height_std) ? 1.0 : 0.0;
+  CS(C_COL0[H12_C_FOOT_CONTACT]) = (nfeet < 1 || nfeet > 2) ? 1.0 : 0.0;
+  double dz = c->cstr_nomove_deadzone;
+  CS(CAT_ROW_NOMOVE) = (fabs(e->cmd[0]) < dz && fabs(e->cmd[1]) < dz && fabs(e->cmd[2]) < dz) ? 1.0 : 0.0;
+  CS(CAT_ROW_EPLEN) = e->eplen;
+#undef CS
+}
+
+/* ConstraintManager.compute + CaTEnv.step's use of it (constraint_manager.py:42-78, 222-237; cat_env.py:148-153,
+ * 164-166) over the whole batch: column maxima (no_move: env i takes the row of the (i mod m)-th still env),
+ * running maxima, probabilities, reward scaling, dones, episode statistics. */
+static void cat_pass(const h12env_config* c, int n, float* F, const double* cs, float* rew, const uint8_t* terminated,
+                     const uint8_t* truncated, float* cstr_prob, float* log_acc) {
+  int* list = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  int mcount = 0;
+  for (int i = 0; i < n; ++i)
+    if (cs[(size_t)CAT_ROW_NOMOVE * n + i] != 0) list[mcount++] = i;
+  for (int col = 0; col < H12_NCSTR_COLS; ++col) {
+    int nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
+    double cm = -1e300;
+    if (nm) {
+      if (mcount == 0) cm = 0.0;
+      for (int a = 0; a < mcount; ++a) { double v = cs[(size_t)col * n + list[a]]; if (v > cm) cm = v; }
+    } else {
+      for (int i = 0; i < n; ++i) { double v = cs[(size_t)col * n + i]; if (v > cm) cm = v; }
+    }
+    if (cm < 1e-6) cm = 1e-6;
+    g_crun[col] = g_crun_init ? c->cat_tau * g_crun[col] + (1.0 - (double)c->cat_tau) * cm : cm;
+  }
+  g_crun_init = 1;
+  for (int i = 0; i < n; ++i) {
+    int src = mcount > 0 ? list[i % mcount] : -1;
+    double pt[H12_NCSTR], pmax = 0;
+    for (int t = 0; t < H12_NCSTR; ++t) {
+      pt[t] = 0;
+      if (!((c->cstr_mask >> t) & 1u)) continue;
+      for (int col = C_COL0[t]; col < C_COL0[t + 1]; ++col) {
+        double v = t == H12_C_NO_MOVE ? (src >= 0 ? cs[(size_t)col * n + src] : 0.0) : cs[(size_t)col * n + i];
+        double p = 0;
+        if (v > 0) {
+          double r = v / g_crun[col];
+          r = r < 0 ? 0 : (r > 1 ? 1 : r);
+          p = c->cat_min_p + r * (c->cstr_max_p[t] - c->cat_min_p);
+        }
+        if (p > pt[t]) pt[t] = p;
+      }
+      if (pt[t] > pmax) pmax = pt[t];
+    }
+    rew[i] = (float)(rew[i] * (1.0 - pmax));
+    int reset = terminated[i] || truncated[i];
+    if (cstr_prob) cstr_prob[i] = reset ? 1.0f : (float)pmax;
+    double len = cs[(size_t)CAT_ROW_EPLEN * n + i];
+    for (int t = 0; t < H12_NCSTR; ++t) {
+      if (!((c->cstr_mask >> t) & 1u)) continue;
+      float* fs = &F[(size_t)(H12_F_CSTR_SUM + t) * n + i];
+      float* fp = &F[(size_t)(H12_F_CSTR_P + t) * n + i];
+      double vs = *fs + (pt[t] > 0 ? 1.0 : 0.0), vp = *fp + pt[t];
+      if (reset) {
+        if (log_acc) {
+          log_acc[H12_NREW + 4 + t] += (float)(vs / len);
+          log_acc[H12_NREW + 4 + H12_NCSTR + t] += (float)(vp / len);
+        }
+        vs = vp = 0;
+      }
+      *fs = (float)vs;
+      *fp = (float)vp;
+    }
+  }
+  free(list);
+}
+
 int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
                  const float* actions, const float* obs_prev, float* obs, float* rew, uint8_t* terminated,
-                 uint8_t* truncated, float* log_acc, float* applied_torque, float* foot_force, int64_t step_index,
-                 int n_threads) {
+                 uint8_t* truncated, float* log_acc, float* applied_torque, float* foot_force, float* cstr_prob,
+                 int64_t step_index, int n_threads) {
   const uint32_t lo = (uint32_t)step_index, hi = (uint32_t)((uint64_t)step_index >> 32);
   const int dec = c->decimation;
   const double dt = c->physics_dt, step_dt = c->physics_dt * dec;
   const int dz_prev = g_dz_count;
   int dz_next = 0;
   int err = 0;
+  double* cs = c->cat_enable ? (double*)calloc((size_t)CAT_ROWS * (size_t)n, sizeof(double)) : NULL;
 #ifdef _OPENMP
   if (n_threads < 1) n_threads = 1;
 #pragma omp parallel for num_threads(n_threads) schedule(static)
@@ -1188,6 +1309,7 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       e.epsum[t] += v;
     }
     rew[i] = (float)r;
+    if (cs) cat_constraints(m, c, &e, tau_applied, fmax_foot, term, gb, n, i, F, step_dt, cs);
     terminated[i] = (uint8_t)term;
     truncated[i] = (uint8_t)tout;
     if (applied_torque) for (int j = 0; j < NJ; ++j) applied_torque[(size_t)i * NJ + j] = (float)tau_applied[j];
@@ -1234,6 +1356,12 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
     env_store_extra(c, F, I, n, i, &e);
   }
   if (c->cmd_deadzone) g_dz_count = dz_next;
+  if (cs) {
+    cat_pass(c, n, F, cs, rew, terminated, truncated, cstr_prob, log_acc);
+    free(g_cs_last);
+    g_cs_last = cs;
+    g_cs_n = n;
+  }
   return err;
 }
 

@@ -81,7 +81,13 @@ int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t 
 int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* fstate,
                  int32_t* istate, const float* actions, const float* obs_prev, float* obs, float* rew,
                  uint8_t* terminated, uint8_t* truncated, float* log_acc, float* applied_torque,
-                 float* foot_force, int64_t step_index, int n_threads);
+                 float* foot_force, float* cstr_prob, int64_t step_index, int n_threads);
+/* CaT running maxima carried between steps (process-global): forget them / read them. */
+void orc_cat_reset(void);
+void orc_cat_running_max(double out[H12_NCSTR_COLS]);
+/* The last orc_env_step's raw constraint values, [H12_NCSTR_COLS + 2][n] (+ no_move flag, pre-reset
+ * episode length); -1 if n differs. */
+int orc_cat_last_constraints(double* out, int n);
 /* Physics-only batched step (h12env_step_physics): n_substeps with held q_ref per env. */
 int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, float* fstate, int32_t* istate,
                          const float* q_ref, int n_substeps);

@@ -75,8 +75,14 @@ def lib():
         L.orc_physics_step.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.POINTER(Report)]
         L.orc_mujoco_rollout.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.c_int, dp]
         L.orc_env_reset.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, C.c_uint64]
-        L.orc_env_step.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int64,
-                                   C.c_int]
+        L.orc_env_step.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                   C.c_int64, C.c_int]
+        L.orc_cat_reset.argtypes = []
+        L.orc_cat_reset.restype = None
+        L.orc_cat_running_max.argtypes = [dp]
+        L.orc_cat_running_max.restype = None
+        L.orc_cat_last_constraints.argtypes = [dp, C.c_int]
+        L.orc_cat_last_constraints.restype = C.c_int
         L.orc_env_step_physics.argtypes = [M, Cf, C.c_int, vp, vp, vp, C.c_int]
         L.orc_env_observe.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, vp, C.c_uint64]
         L.orc_delay_source.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
@@ -190,6 +196,25 @@ def set_dz_count(v: int):
     lib().orc_set_dz_count(int(v))
 
 
+def cat_reset():
+    """Forget the CaT running maxima (a fresh ConstraintManager)."""
+    lib().orc_cat_reset()
+
+
+def cat_running_max() -> np.ndarray:
+    out = np.zeros(56)
+    lib().orc_cat_running_max(_d(out))
+    return out
+
+
+def cat_last_constraints(n: int) -> np.ndarray:
+    """(58, n): the last step's raw constraints (56 columns), no_move flag, pre-reset episode length."""
+    out = np.zeros((58, n))
+    if lib().orc_cat_last_constraints(_d(out), n):
+        raise RuntimeError("no CaT step of that size")
+    return out
+
+
 def dz_count() -> int:
     return int(lib().orc_dz_count())
 
@@ -227,13 +252,15 @@ class OracleEnv:
         log = np.zeros(NLOG, dtype=np.float32)
         tq = np.empty((self.n, NJ), dtype=np.float32)
         ff = np.empty((self.n, 2), dtype=np.float32)
+        cp = np.zeros(self.n, dtype=np.float32)
         rc = lib().orc_env_step(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, _p(self.F), _p(self.I),
                                 _p(a), _p(self.obs), _p(obs), _p(rew), _p(term), _p(trunc), _p(log), _p(tq), _p(ff),
-                                step_index, n_threads)
+                                _p(cp), step_index, n_threads)
         if rc:
             raise RuntimeError("oracle env step failed")
         self.obs = obs
-        return obs.copy(), rew, term.astype(bool), trunc.astype(bool), dict(log=log, applied_torque=tq, foot_force=ff)
+        return obs.copy(), rew, term.astype(bool), trunc.astype(bool), dict(log=log, applied_torque=tq, foot_force=ff,
+                                                                            cstr_prob=cp)
 
     def observe(self, fill_mask=None):
         m = None if fill_mask is None else np.ascontiguousarray(fill_mask, dtype=np.uint8)
