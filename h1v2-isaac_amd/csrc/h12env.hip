@@ -1248,6 +1248,8 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   if (active) {
     EnvSt s;
     load_phys<K>(P, W, e, leg, s);
+    // the MDP part of the state is loaded here too: its memory round trip overlaps the physics loop
+    load_mdp<K>(P, W, e, leg, s);
     PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
@@ -1301,7 +1303,6 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       }
     }
     PH(1);
-    load_mdp<K>(P, W, e, leg, s);
     // ContactSensor._update_buffers_impl replayed per physics step (threshold 1 N, elapsed = dt)
     for (int st = 0; st < dec; ++st) {
       bool is_c = (cflags >> st) & 1u;

@@ -88,7 +88,9 @@ def write_env_yaml(cfg, path: str) -> str:
 class _ExportedPolicy(nn.Module):
     def __init__(self, actor: nn.Module, normalizer: nn.Module | None):
         super().__init__()
-        self.actor = copy.deepcopy(actor).cpu().eval()
+        from .ppo import plain_linear
+
+        self.actor = plain_linear(actor).cpu().eval()
         self.normalizer = copy.deepcopy(normalizer).cpu().eval() if normalizer is not None else nn.Identity()
 
     def forward(self, x):

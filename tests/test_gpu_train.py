@@ -72,3 +72,51 @@ def test_train_rsl_task_one_iteration(gpu, tmp_path, monkeypatch):
     run = next((tmp_path / "logs" / "rsl_rl" / "h12_12dof_flat").iterdir())
     x = json.loads((run / "metrics.jsonl").read_text().splitlines()[-1])
     assert "Episode_Reward/joint_vel_l2" in x and "Episode_Reward/base_height_l2" in x
+
+
+def test_split_k_linear_gradients_match_linear(gpu):
+    """The learner's split-K weight gradient equals nn.Linear's (fp32; summation order differs)."""
+    from h12env.ppo import SplitKLinear
+
+    torch.manual_seed(0)
+    lin = SplitKLinear(270, 512).cuda()
+    ref = torch.nn.Linear(270, 512).cuda()
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(24576, 270, device="cuda", requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    gy = torch.randn(24576, 512, device="cuda")
+    lin(x).backward(gy)
+    ref(xr).backward(gy)
+    for a, b in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad), (x.grad, xr.grad)):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-3 * b.abs().max().item() * 1e-2), (a - b).abs().max()
+
+
+def test_graph_captured_update_equals_eager(gpu, monkeypatch):
+    """PPO.update replayed from the captured HIP graph gives the eager update's parameters (same kernels; the
+    capture's warm-up is undone bit-exactly), over two updates with the KL-adaptive learning rate."""
+    import copy
+
+    from h12env.ppo import PPO, ActorCritic
+
+    def run(graph: bool):
+        monkeypatch.setenv("H12_PPO_GRAPH", "1" if graph else "0")
+        torch.manual_seed(7)
+        pol = ActorCritic(270, 270, 12, [128, 64], [128, 64])
+        alg = PPO(copy.deepcopy(pol), num_learning_epochs=2, num_mini_batches=4, learning_rate=1e-3,
+                  schedule="adaptive", desired_kl=0.01, device="cuda:0")
+        alg.init_storage(1024, 8, [270], None, [12])
+        out = []
+        for u in range(2):
+            g = torch.Generator(device="cuda:0").manual_seed(100 + u)
+            for k, v in alg.storage.t.items():
+                v.copy_(torch.randn(v.shape, generator=g, device="cuda:0") * (0.1 if k == "sigma" else 1.0))
+            alg.storage.t["sigma"].abs_().add_(0.5)
+            out.append(alg.update())
+        return alg, out
+
+    a, la = run(True)
+    b, lb = run(False)
+    assert a._graph is not None and b._graph is None
+    for p, q in zip(a.policy.parameters(), b.policy.parameters()):
+        assert torch.equal(p, q), (p - q).abs().max()
+    assert la == lb and a.learning_rate == b.learning_rate
