@@ -115,3 +115,40 @@ def test_partial_reset_ragged(gpu):
     np.testing.assert_array_equal(after[~mask], before[~mask])
     np.testing.assert_allclose(after[mask], r[mask], rtol=1e-5, atol=1e-6)
     env.close()
+
+
+@pytest.mark.parametrize("task", ["rsl", "cat"])
+@pytest.mark.parametrize("n", [1, 37, 100])
+def test_ragged_env_counts_rsl_cat(gpu, task, n):
+    """The Play configs run 100 envs: partial lane blocks, partial 4-row assembly blocks of the 270-float
+    rows (270 * 4 bytes is not a multiple of 16 per row), CaT's chunked column maxima and compaction."""
+    from h12env.cfg import H12CaTEnvCfg, H12RslEnvCfg
+
+    cfg = H12RslEnvCfg() if task == "rsl" else H12CaTEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    ref = O.OracleEnv(env._model, env._ccfg, n)
+    ref.F[:] = env._fstate.cpu().numpy()
+    ref.I[:] = env._istate.cpu().numpy()
+    O.set_dz_count(0)
+    O.cat_reset()
+    obs, _ = env.reset()
+    np.testing.assert_allclose(obs["policy"].cpu().numpy(), ref.reset(), rtol=1e-5, atol=2e-5)
+    rng = np.random.default_rng(13)
+    for t in range(1, 4):
+        if task == "cat":
+            for name, cid in cfg.constraints.active():
+                if name != "contact":
+                    ref.cfg.cstr_max_p[cid] = 1.0 / (20 + min((t - 1) / 120000, 1.0) * (4 - 20))
+        a = (0.3 * rng.normal(size=(n, 12))).astype(np.float32)
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(a).cuda())
+        r_obs, r_rew, r_term, r_trunc, info = ref.step(a, t)
+        go = obs["policy"].cpu().numpy()
+        ok = (np.abs(go - r_obs) <= 2e-3 * np.maximum(1, np.abs(r_obs))).all(axis=1)
+        assert ok.mean() >= 0.97, (t, ok.mean())
+        okr = np.abs(rew.cpu().numpy() - r_rew) <= 2e-3 * np.maximum(1, np.abs(r_rew))
+        assert okr.mean() >= 0.97, (t, okr.mean())
+        if task == "cat":
+            assert np.isfinite(term.cpu().numpy()).all()
+    env.close()
