@@ -304,12 +304,54 @@ class PPO:
 
     # ---- collection
     def act(self, obs, critic_obs):
+        if self._act_graph_ok(obs, critic_obs):
+            return self._act_graphed(obs, critic_obs)
         self._obs, self._critic_obs = obs, critic_obs
         self._actions = self.policy.act(obs).detach()
         self._values = self.policy.evaluate(critic_obs).detach()
         self._log_prob = self.policy.get_actions_log_prob(self._actions).detach()
         self._mu = self.policy.action_mean.detach()
         self._sigma = self.policy.action_std.detach()
+        return self._actions
+
+    # ---- collection as a HIP graph: actor + critic forward, Gaussian sample, log-probability in one launch
+    def _act_graph_ok(self, obs, critic_obs) -> bool:
+        return (obs.is_cuda and not torch.is_grad_enabled() and os.environ.get("H12_PPO_GRAPH", "1") != "0"
+                and not getattr(self.policy, "is_recurrent", False))
+
+    def _act_body(self):
+        mean = self.policy.actor(self._ga_obs)
+        std = self.policy._std(mean)
+        # mean + std * N(0, 1): the same Normal(mean, std) sample as distribution.sample(), from randn (capturable)
+        actions = mean + std * torch.randn_like(mean)
+        values = self.policy.critic(self._ga_cobs)
+        log_prob = Normal(mean, std).log_prob(actions).sum(dim=-1)
+        self._ga_out = (actions, values, log_prob, mean, std)
+
+    def _act_graphed(self, obs, critic_obs):
+        key = (tuple(obs.shape), tuple(critic_obs.shape), critic_obs is obs, obs.dtype)
+        if getattr(self, "_ga", None) is None or self._ga_key != key:
+            # normal (not inference) tensors throughout: the graph's RNG state is updated outside inference mode
+            with torch.inference_mode(False), torch.no_grad():
+                self._ga_obs = torch.zeros(obs.shape, dtype=obs.dtype, device=obs.device)
+                self._ga_cobs = (self._ga_obs if critic_obs is obs else
+                                 torch.zeros(critic_obs.shape, dtype=critic_obs.dtype, device=obs.device))
+                s = torch.cuda.Stream(device=obs.device)
+                s.wait_stream(torch.cuda.current_stream(obs.device))
+                with torch.cuda.stream(s):
+                    for _ in range(2):
+                        self._act_body()
+                torch.cuda.current_stream(obs.device).wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._act_body()
+            self._ga, self._ga_key = g, key
+        self._ga_obs.copy_(obs)
+        if critic_obs is not obs:
+            self._ga_cobs.copy_(critic_obs)
+        self._ga.replay()
+        self._obs, self._critic_obs = obs, critic_obs
+        self._actions, self._values, self._log_prob, self._mu, self._sigma = self._ga_out
         return self._actions
 
     def process_env_step(self, rewards, dones, infos):
