@@ -49,6 +49,9 @@ def parse():
                    help="flat: the metric's task; rough: Isaac-Velocity-Rough-H12_12dof-v0; c5: BASELINE config C5 "
                         "(rough + per-env friction / torso mass, 8192 envs unless --envs); rsl: "
                         "Isaac-Velocity-Rsl-H12_12dof-v0; cat: Isaac-Velocity-CaT-Flat-H12_12dof-v0")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse several "
+                        "ranks on one GPU: rank r uses GPU r mod device_count)")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     return p.parse_args()
@@ -169,10 +172,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev)
 
     if args.mode == "train":
         train_mode(args, world, rank, dev, torch, dist)
