@@ -98,7 +98,26 @@ def cpu_baseline(seconds: float):
         env.step(acts[steps % 8], steps + 2, n_threads=threads)
         steps += 1
     dt = time.perf_counter() - t0
+    # BASELINE config C1: the sim2sim MuJoCo loop, one env on one core -- 1000 policy steps of 20 substeps
+    # (dt 1 ms, PD every substep, MJCF clamps; oracle MuJoCo mode, free base with ground contact)
+    from h12env.cfg import mujoco_cfg
+
+    mc = mujoco_cfg().to_c()
+    model = build_model()
+    s = np.zeros(37)
+    s[2], s[3] = 1.05, 1.0
+    s[13:25] = np.asarray(model.q_default)
+    q0 = np.asarray(model.q_default)
+    t1 = time.perf_counter()
+    for k in range(1000):
+        q_ref = q0 + 0.25 * rng.normal(size=12) * 0.2
+        s, _ = O.mujoco_rollout(model, mc, s, q_ref, 20, contact=True, algo=1)
+    dt1 = time.perf_counter() - t1
+    mujoco = {"value": 1000 / dt1, "unit": "env-steps/s", "cores": 1,
+              "sample": "C1: oracle MuJoCo mode (sim2sim semantics), 1 env x 1000 policy steps x 20 substeps, "
+                        f"random q_ref, ground contact ({dt1:.2f} s)"}
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "single_env_sim2sim": mujoco,
             "sample": f"oracle/h12_oracle.c (fp64, OpenMP) on {n} envs x {steps} env steps "
                       f"({dt:.1f} s) of the same random-action Flat-H12 workload, {threads} host threads"}
 
