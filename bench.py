@@ -54,6 +54,8 @@ def parse():
                         "ranks on one GPU: rank r uses GPU r mod device_count)")
     p.add_argument("--decimation", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
+    p.add_argument("--explicit-penalty", action="store_true",
+                   help="experiment: round-1 explicit penalty contact (use with --inner-steps 2)")
     return p.parse_args()
 
 
@@ -227,6 +229,8 @@ def main():
         cfg.decimation = args.decimation
     if args.inner_steps:
         cfg.sim.inner_steps = args.inner_steps
+    if args.explicit_penalty:
+        cfg.sim.implicit_penalty = False
     env = H12VelocityEnv(cfg, env_offset=rank * n)
     env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -305,6 +309,7 @@ def main():
                 "decimation": cfg.decimation,
                 "physics_dt": cfg.sim.dt,
                 "inner_steps": cfg.sim.inner_steps,
+                "implicit_penalty": bool(cfg.sim.implicit_penalty),
                 "parallelism": f"env-shard x{world}",
             },
             "roofline": {

@@ -85,12 +85,20 @@ int set_err(int code, const char* fmt, ...) {
 // ------------------------------------------------------------------ runtime parameters (kernarg)
 struct KParams {
   float kp[NL], kd[NL], elim[NL], dimpl[NL];  // per leg link (leg-symmetric)
+  float vmax[NL];         // PhysX max joint velocity (h12env_config.max_joint_vel; 0 -> no limit = 3e38)
+  float cv;               // its damper (h12env_config.max_joint_vel_damping)
   int dgroup[NL];
   float g;
   int mode, fix_base, decimation, inner, max_len, min_delay, max_delay, use_fl;
   int corrupt, ill_knees, ill_torso;
   float dt, h, step_dt, action_scale, soft_f;
   float ck, cc, fk, fc, mus, mud, lk, lc, cthr;
+  // implicit contact (h12env_config.implicit_penalty): cc / fc already include the
+  // extra damping h k; impl != 0 adds the point inertia h cc (normal) / h fc (tangential, sticking or
+  // below the drag cap) of every active contact to its body in the dynamics solve
+  int impl;
+  float fc_v;             // viscous tangential coefficient of the knee / torso contacts
+  float dl;               // implicit joint-limit inertia h (lc + h lk) (lc already includes h lk)
   float cmd_T, cmd_x0, cmd_x1, cmd_y0, cmd_y1, cmd_w0, cmd_w1, cmd_h0, cmd_h1;
   float rel_stand, rel_head, head_k;
   float rx0, rx1, ry0, ry1, ryaw0, ryaw1, root_z;
@@ -193,18 +201,62 @@ struct Leg {                // this lane's leg in the lane frame (mirrored for t
   float mus, mud;           // sole Coulomb coefficients (per env and foot, or the config's)
   float dmass;              // mass added at the torso COM (lane 0 applies it)
 };
-struct Forces {             // net contact force of this lane's bodies (lane world frame), summed
+struct Forces {             // net contact force on this lane's bodies (body coords; only norms are used), summed
   float foot[3], knee[3], torso[3];
 };
+
+// Added point inertia of an implicit contact at body point p: mass tensor M = beta I + gamma u u^T (body
+// coords, u = the ground normal in body coords) -> C += M, B += [p]x M, A += -[p]x M [p]x
+// (= beta (|p|^2 I - p p^T) + gamma w w^T with w = p x u).
+H12_DEV void ai_add_contact(AInertia& I, const float* p, const float* u, float beta, float gamma) {
+  float w[3];
+  cross(p, u, w);
+  const float gu[3] = {gamma * u[0], gamma * u[1], gamma * u[2]};
+  const float gw[3] = {gamma * w[0], gamma * w[1], gamma * w[2]};
+  I.C[0] += beta + gu[0] * u[0]; I.C[1] += beta + gu[1] * u[1]; I.C[2] += beta + gu[2] * u[2];
+  I.C[3] += gu[0] * u[1]; I.C[4] += gu[0] * u[2]; I.C[5] += gu[1] * u[2];
+  I.B[0][1] -= beta * p[2]; I.B[0][2] += beta * p[1];
+  I.B[1][0] += beta * p[2]; I.B[1][2] -= beta * p[0];
+  I.B[2][0] -= beta * p[1]; I.B[2][1] += beta * p[0];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) I.B[i][j] += gw[i] * u[j];
+  const float p2 = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
+  I.A[0] += beta * (p2 - p[0] * p[0]) + gw[0] * w[0];
+  I.A[1] += beta * (p2 - p[1] * p[1]) + gw[1] * w[1];
+  I.A[2] += beta * (p2 - p[2] * p[2]) + gw[2] * w[2];
+  I.A[3] += gw[0] * w[1] - beta * p[0] * p[1];
+  I.A[4] += gw[0] * w[2] - beta * p[0] * p[2];
+  I.A[5] += gw[1] * w[2] - beta * p[1] * p[2];
+}
+
+// implicit-contact linearisation of one active contact (zero when P.impl == 0 or out of contact)
+struct ImplC {
+  float beta, gamma, u[3];
+};
+// implicit part of a contact's force, -M a'_p (body coords): a = the body's spatial acceleration in the
+// gravity-shifted frame of the solve, p the contact point, M = beta I + gamma u u^T (oracle implicit_report)
+H12_DEV void impl_force(const float* a, const float* p, const float* u, float beta, float gamma, float* f) {
+  float ap[3];
+  cross(a, p, ap);
+  ap[0] += a[3]; ap[1] += a[4]; ap[2] += a[5];
+  const float gn = gamma * (u[0] * ap[0] + u[1] * ap[1] + u[2] * ap[2]);
+  f[0] -= beta * ap[0] + gn * u[0];
+  f[1] -= beta * ap[1] + gn * u[1];
+  f[2] -= beta * ap[2] + gn * u[2];
+}
 
 // one penalty contact (sphere centre pl in body coords, body world pose Rb/pb, body spatial velocity
 // vb in body coords); adds the body-frame spatial force into f[6]; anchored stiction for sole spheres
 // sg: the lane's mirror sign (the heightfield is looked up at the real y = sg * y); mus / mud: Coulomb
-// coefficients of this contact (per-env sole friction or the config's)
+// coefficients of this contact (per-env sole friction or the config's).  With P.impl, ic receives the
+// added point inertia of the contact (oracle contact_point) and f the force that cancels its weight
+// under the gravity-as-base-acceleration formulation.
 template <bool ANCHOR, bool TERRAIN>
 H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
                             const float* pl, float rad, float* f, float* fw, float* anc, bool was_in, float sg,
-                            float mus, float mud) {
+                            float mus, float mud, ImplC& ic) {
+  ic.beta = 0.f;
+  ic.gamma = 0.f;
   float xw[3];
   mv(Rb, pl, xw);
   xw[0] += pb[0]; xw[1] += pb[1]; xw[2] += pb[2];
@@ -228,12 +280,14 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   float fn = P.ck * depth - P.cc * vn;
   if (!(fn > 0.f)) return false;
   float ft0, ft1;
+  bool stick;
   if constexpr (ANCHOR) {
     float ax = was_in ? anc[0] : xw[0], ay = was_in ? anc[1] : xw[1];
     ft0 = -P.fk * (xw[0] - ax) - P.fc * vw[0];
     ft1 = -P.fk * (xw[1] - ay) - P.fc * vw[1];
     float ftn2 = ft0 * ft0 + ft1 * ft1, cap = mus * fn;
-    if (ftn2 > cap * cap) {
+    stick = !(ftn2 > cap * cap);
+    if (!stick) {
       float sc = mud * fn * __builtin_amdgcn_rsqf(ftn2);
       ft0 *= sc;
       ft1 *= sc;
@@ -244,18 +298,30 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
     anc[0] = ax;
     anc[1] = ay;
   } else {
-    ft0 = -P.fc * vw[0];
-    ft1 = -P.fc * vw[1];
+    ft0 = -P.fc_v * vw[0];
+    ft1 = -P.fc_v * vw[1];
     float ftn2 = ft0 * ft0 + ft1 * ft1, cap = mud * fn;
-    if (ftn2 > cap * cap) { float sc = cap * __builtin_amdgcn_rsqf(ftn2); ft0 *= sc; ft1 *= sc; }
+    stick = !(ftn2 > cap * cap);
+    if (!stick) { float sc = cap * __builtin_amdgcn_rsqf(ftn2); ft0 *= sc; ft1 *= sc; }
   }
   float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
   if constexpr (TERRAIN) { Fw[0] += fn * nrm[0]; Fw[1] += fn * nrm[1]; Fw[2] = fn * nrm[2]; }
+  if (P.impl) {
+    const float h = P.h;
+    const float alpha = h * P.cc;
+    const float beta = stick ? h * (ANCHOR ? P.fc : P.fc_v) : 0.f;
+    ic.beta = beta;
+    ic.gamma = alpha - beta;
+    mtv(Rb, nrm, ic.u);
+    // g Mw e_z = g (beta e_z + gamma n n_z)
+    const float gb = P.g * beta, gg = P.g * ic.gamma * nrm[2];
+    Fw[0] += gg * nrm[0]; Fw[1] += gg * nrm[1]; Fw[2] += gb + gg * nrm[2];
+  }
   mtv(Rb, Fw, fl);
   cross(pl, fl, nl);
   f[0] += nl[0]; f[1] += nl[1]; f[2] += nl[2];
   f[3] += fl[0]; f[4] += fl[1]; f[5] += fl[2];
-  fw[0] += Fw[0]; fw[1] += Fw[1]; fw[2] += Fw[2];
+  fw[0] += fl[0]; fw[1] += fl[1]; fw[2] += fl[2];  // reported in body coords (only its norm is used)
   return true;
 }
 
@@ -376,12 +442,12 @@ H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, floa
 // for LINK == 0 the leg's contribution to the base, at the base origin).
 template <int LINK>
 H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
-                        const float* fext_knee, const float* tau, AInertia& IA, float* pAcc, float (&U)[NL][6],
-                        float (&Dinv)[NL], float (&u)[NL], float h) {
+                        const float* fext_knee, const ImplC& ick, float knee_pz, const float* tau, const float* dl,
+                        AInertia& IA, float* pAcc, float (&U)[NL][6], float (&Dinv)[NL], float (&u)[NL], float h) {
   constexpr int A = AX[LINK];
   float Ua[3] = {sget(IA.A, 0, A), sget(IA.A, 1, A), sget(IA.A, 2, A)};
   float Ul[3] = {IA.B[A][0], IA.B[A][1], IA.B[A][2]};
-  float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK];
+  float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK] + dl[LINK];
   float di = frcp(D);
   float uu = tau[LINK] - pAcc[A];
   U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
@@ -425,8 +491,13 @@ H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2
     float pb[6];
     bias<LINK - 1>(v[LINK - 1], pb);
     for (int i = 0; i < 6; ++i) pAcc[i] += pb[i];
-    if constexpr (LINK - 1 == 3)
+    if constexpr (LINK - 1 == 3) {
       for (int i = 0; i < 6; ++i) pAcc[i] -= fext_knee[i];
+      if (P.impl && ick.gamma + ick.beta > 0.f) {
+        const float pk[3] = {0.f, 0.f, knee_pz};
+        ai_add_contact(IA, pk, ick.u, ick.beta, ick.gamma);
+      }
+    }
   }
 }
 
@@ -473,6 +544,8 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float p[3] = {b.pos[0], sg * b.pos[1], b.pos[2]};
   float cs[NL][2], v[NL][6];
   float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ImplC ick;     // knee contact linearisation (added to link 3 in pass 2)
+  float knee_pz;  // z of the knee contact point (KNEE0 or KNEE1; x = y = 0)
   link_pass1<0>(lg, cs, vl0, v, R, p);
   link_pass1<1>(lg, cs, v[0], v, R, p);
   link_pass1<2>(lg, cs, v[1], v, R, p);
@@ -482,13 +555,17 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     float w0[3], w1[3];
     mv(R, h12m::KNEE0, w0);
     mv(R, h12m::KNEE1, w1);
-    const float* pl = (w0[2] <= w1[2]) ? h12m::KNEE0 : h12m::KNEE1;
+    const bool lo0 = w0[2] <= w1[2];
+    const float* pl = lo0 ? h12m::KNEE0 : h12m::KNEE1;
+    knee_pz = lo0 ? h12m::KNEE0[2] : h12m::KNEE1[2];
     float dummy[2];
-    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, P.mus, P.mud);
+    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, P.mus, P.mud, ick);
   }
   link_pass1<4>(lg, cs, v[3], v, R, p);
   link_pass1<5>(lg, cs, v[4], v, R, p);
   // ---- foot: 4 anchored sole spheres on the ankle-roll link; starts pass 2 of link 5
+  int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
+  float fu[H12_NFOOT_PTS][3];         // implicit: ground normal at each sole sphere, foot coords
   AInertia IA;
   ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
   float pAcc[6];
@@ -499,33 +576,51 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
 #pragma unroll
     for (int q = 0; q < H12_NFOOT_PTS; ++q) {
       bool was = (lg.cmask >> q) & 1;
+      ImplC ic;
       if (contact_sphere<true, Feat<K>::terrain>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was, sg, lg.mus,
-                               lg.mud))
+                               lg.mud, ic)) {
         nmask |= 1 << q;
+        if (P.impl) {
+          ai_add_contact(IA, h12m::FOOT[q], ic.u, ic.beta, ic.gamma);
+          smask |= (ic.beta > 0.f ? 1 : 0) << q;
+          fu[q][0] = ic.u[0]; fu[q][1] = ic.u[1]; fu[q][2] = ic.u[2];
+        }
+      }
     }
     lg.cmask = nmask;
     for (int i = 0; i < 6; ++i) pAcc[i] -= fext[i];
   }
   // ---- joint torques for this inner step: actuator + limit penalty (+ MuJoCo passive)
-  float tau[NL];
+  float tau[NL], dl[NL];  // dl: implicit joint-limit inertia h (lc + h lk) of an active limit (oracle joint_limit_torque)
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float q = lg.q[k], qd = lg.qd[k];
     float t = tau_pd[k];
-    if (q > h12m::QHI[k]) t += fminf(0.f, -P.lk * (q - h12m::QHI[k]) - P.lc * qd);
-    else if (q < h12m::QLO[k]) t += fmaxf(0.f, -P.lk * (q - h12m::QLO[k]) - P.lc * qd);
+    float tl = 0.f;
+    if (q > h12m::QHI[k]) tl = fminf(0.f, -P.lk * (q - h12m::QHI[k]) - P.lc * qd);
+    else if (q < h12m::QLO[k]) tl = fmaxf(0.f, -P.lk * (q - h12m::QLO[k]) - P.lc * qd);
+    t += tl;
+    dl[k] = tl != 0.f ? P.dl : 0.f;
+    // PhysX max joint velocity: implicit stiff damper on the excess (oracle joint_limit_torque)
+    const float ex = fabsf(qd) - P.vmax[k];
+    if (ex > 0.f) {  // C1 ramp-in over H12_VLIM_RAMP (h12env.h)
+      const float r = fminf(ex * (1.f / H12_VLIM_RAMP), 1.f);
+      const float mag = ex < H12_VLIM_RAMP ? 0.5f * P.cv * ex * r : P.cv * (ex - 0.5f * H12_VLIM_RAMP);
+      t -= copysignf(mag, qd);
+      dl[k] += h * P.cv * r;
+    }
     t -= P.dimpl[k] * qd;
     if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
     tau[k] = t;
   }
   // ---- pass 2 (leaf -> root)
   float U[NL][6], Dinv[NL], u[NL];
-  link_pass2<5>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<4>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<3>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<2>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<1>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
-  link_pass2<0>(P, lg, cs, v, fext_knee, tau, IA, pAcc, U, Dinv, u, h);
+  link_pass2<5>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  link_pass2<4>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  link_pass2<3>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  link_pass2<2>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  link_pass2<1>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  link_pass2<0>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
   // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
@@ -534,6 +629,9 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   for (int i = 0; i < 6; ++i) pAcc[i] *= s6(i, sg);
   // ---- lane 0 adds the base body: rigid inertia, bias force, torso-box contact
   float ag[6] = {0.f, 0.f, 0.f, -P.g * R0[2][0], -P.g * R0[2][1], -P.g * R0[2][2]};
+  ImplC ict;  // torso contact linearisation (lane 0)
+  float corner[3];
+  ict.beta = ict.gamma = 0.f;
   if (leg == 0) {
     AInertia Rg;
     ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
@@ -547,11 +645,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     cross(v0, hb + 3, x3);
     pAcc[0] += x1[0] + x2[0]; pAcc[1] += x1[1] + x2[1]; pAcc[2] += x1[2] + x2[2];
     pAcc[3] += x3[0]; pAcc[4] += x3[1]; pAcc[5] += x3[2];
-    float corner[3];
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dummy[2];
-    contact_sphere<false, Feat<K>::terrain>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, P.mus, P.mud);
+    if (contact_sphere<false, Feat<K>::terrain>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, P.mus, P.mud,
+                                                ict) &&
+        P.impl)
+      ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
   }
   // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
@@ -573,6 +673,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     float rhs[6] = {-pB[0], -pB[1], -pB[2], -pB[3], -pB[4], -pB[5]};
     solve6(IB, rhs, a0);
   }
+  if (P.impl && leg == 0 && ict.gamma + ict.beta > 0.f) impl_force(a0, corner, ict.u, ict.beta, ict.gamma, fr.torso);
   // ---- pass 3 (root -> leaf) in the lane frame
   float a[6];
   for (int i = 0; i < 6; ++i) a[i] = s6(i, sg) * a0[i];
@@ -581,8 +682,21 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   link_pass3<1>(lg, cs, v, U, Dinv, u, a, qdd);
   link_pass3<2>(lg, cs, v, U, Dinv, u, a, qdd);
   link_pass3<3>(lg, cs, v, U, Dinv, u, a, qdd);
+  if (P.impl && ick.gamma + ick.beta > 0.f) {  // implicit part of the knee contact force
+    const float pk[3] = {0.f, 0.f, knee_pz};
+    impl_force(a, pk, ick.u, ick.beta, ick.gamma, fr.knee);
+  }
   link_pass3<4>(lg, cs, v, U, Dinv, u, a, qdd);
   link_pass3<5>(lg, cs, v, U, Dinv, u, a, qdd);
+  if (P.impl && lg.cmask) {  // implicit part of the sole forces (a = foot acceleration, shifted frame)
+    const float hb = P.h * P.fc, ha = P.h * P.cc;
+#pragma unroll
+    for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+      const float beta = ((smask >> q) & 1) ? hb : 0.f;
+      const float gamma = ((lg.cmask >> q) & 1) ? ha - beta : 0.f;
+      if ((lg.cmask >> q) & 1) impl_force(a, h12m::FOOT[q], fu[q], beta, gamma, fr.foot);
+    }
+  }
   // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates
   if (!P.fix_base) {
     float nd[6];
@@ -1751,8 +1865,9 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   for (int k = 0; k < NL; ++k) {
     if (c->delay_group[k] != c->delay_group[NL + k] || c->delay_group[k] < 0 || c->delay_group[k] > 2)
       return set_err(H12_E_ARG, "delay groups must be leg-symmetric and in 0..2");
-    if (c->kp[k] != c->kp[NL + k] || c->kd[k] != c->kd[NL + k] || c->effort_limit[k] != c->effort_limit[NL + k])
-      return set_err(H12_E_ARG, "gains must be leg-symmetric");
+    if (c->kp[k] != c->kp[NL + k] || c->kd[k] != c->kd[NL + k] || c->effort_limit[k] != c->effort_limit[NL + k] ||
+        c->max_joint_vel[k] != c->max_joint_vel[NL + k] || c->max_joint_vel[k] < 0)
+      return set_err(H12_E_ARG, "gains / velocity limits must be leg-symmetric (and >= 0)");
   }
   if (!(c->friction_k > 0)) return set_err(H12_E_ARG, "friction_k must be > 0");
   const bool mj = c->mode == H12_MODE_MUJOCO;
@@ -1762,7 +1877,9 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
     P.elim[k] = mj ? m->mj_frc_limit[k] : c->effort_limit[k];
     P.dimpl[k] = mj ? m->damping[k] : 0.f;
     P.dgroup[k] = c->delay_group[k];
+    P.vmax[k] = (c->max_joint_vel[k] > 0.f && c->max_joint_vel_damping > 0.f) ? c->max_joint_vel[k] : 3.0e38f;
   }
+  P.cv = c->max_joint_vel_damping;
   P.g = m->gravity;
   P.mode = c->mode;
   P.fix_base = c->fix_base;
@@ -1782,6 +1899,15 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.soft_f = c->soft_limit_factor;
   P.ck = c->contact_k; P.cc = c->contact_c; P.fk = c->friction_k; P.fc = c->friction_c;
   P.mus = c->mu_static; P.mud = c->mu_dynamic; P.lk = c->limit_k; P.lc = c->limit_c;
+  P.fc_v = c->friction_c;
+  P.impl = c->implicit_penalty != 0;
+  P.dl = 0.f;
+  if (P.impl) {  // the springs act at the end of the substep: extra damping h k (oracle contact_point)
+    P.cc = c->contact_c + P.h * c->contact_k;
+    P.fc = c->friction_c + P.h * c->friction_k;
+    P.lc = c->limit_c + P.h * c->limit_k;
+    P.dl = P.h * P.lc;
+  }
   P.cthr = c->contact_threshold;
   P.cmd_T = c->cmd_resample_time;
   P.cmd_x0 = c->cmd_lin_x[0]; P.cmd_x1 = c->cmd_lin_x[1];
@@ -1939,7 +2065,8 @@ int h12env_config_default(h12env_config* c) {
   c->mode = H12_MODE_ISAACLAB;
   c->physics_dt = 0.005f;
   c->decimation = 4;
-  c->inner_steps = 2;
+  c->inner_steps = 1;
+  c->implicit_penalty = 1;
   c->max_episode_length = 1000;
   c->action_scale = 0.5f;
   const float kp[6] = {200, 200, 200, 300, 40, 40}, kd[6] = {2.5f, 2.5f, 2.5f, 4, 2, 2};
@@ -1949,6 +2076,9 @@ int h12env_config_default(h12env_config* c) {
     c->kp[j] = kp[j % 6]; c->kd[j] = kd[j % 6]; c->effort_limit[j] = E[j % 6]; c->delay_group[j] = grp[j % 6];
   }
   c->min_delay = 0; c->max_delay = 5;
+  const float vmax[6] = {23, 23, 23, 14, 9, 9};  // URDF velocity limits as the USD / PhysX hold them
+  for (int j = 0; j < H12_NJ; ++j) c->max_joint_vel[j] = vmax[j % 6];
+  c->max_joint_vel_damping = 1.0e3f;
   c->contact_k = 3e4f; c->contact_c = 100.f; c->friction_k = 3e4f; c->friction_c = 100.f;
   c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1000.f; c->limit_c = 2.f; c->contact_threshold = 1.f;
   c->cmd_resample_time = 10.f;

@@ -20,7 +20,7 @@ NCSTR = 10       # CaT constraint terms (CONSTRAINT_TERMS)
 NCSTR_COLS = 56
 NLOG = 44        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare,
                  # then per constraint term the summed violation rates (10) and mean probabilities (10)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -185,6 +185,9 @@ class H12Config(C.Structure):
         ("cstr_height_std", f32),
         ("cstr_clearance_min", f32),
         ("cstr_clearance_deadzone", f32),
+        ("implicit_penalty", i32),
+        ("max_joint_vel", f32 * NJ),
+        ("max_joint_vel_damping", f32),
     ]
 
 

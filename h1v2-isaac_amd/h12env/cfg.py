@@ -30,7 +30,14 @@ class SimCfg:
     device: str = "cuda:0"
     render_interval: int = 4
     # contact / integration parameters of the build's penalty model (DESIGN.md "Physics model")
-    inner_steps: int = 2
+    # one integration step per 5 ms physics step (PhysX's sim.dt) with the contact springs integrated
+    # implicitly; inner_steps = 2 / implicit_penalty = False is the round-1 explicit scheme
+    inner_steps: int = 1
+    implicit_penalty: bool = True
+    # PhysX enforces the articulation's max joint velocities (RobotCfg.joint_vel_limits, from the USD);
+    # here: a stiff joint damper above the limit, integrated implicitly
+    joint_velocity_limit: bool = True
+    joint_velocity_limit_damping: float = 1.0e3
     contact_k: float = 3.0e4
     contact_c: float = 100.0
     friction_k: float = 3.0e4
@@ -488,6 +495,10 @@ class H12FlatEnvCfg:
         c.physics_dt = self.sim.dt
         c.decimation = self.decimation
         c.inner_steps = self.sim.inner_steps
+        c.implicit_penalty = int(self.sim.implicit_penalty)
+        if self.mode == MODE_ISAACLAB and self.sim.joint_velocity_limit:
+            c.max_joint_vel[:] = self.robot.joint_vel_limits
+            c.max_joint_vel_damping = self.sim.joint_velocity_limit_damping
         c.max_episode_length = self.max_episode_length
         c.action_scale = self.actions.joint_pos.scale
         import re
@@ -808,7 +819,7 @@ def mujoco_cfg(**kw) -> H12FlatEnvCfg:
     """sim2sim semantics (scripts/deploy/config.yaml:7, policies/demo_rsl/env.yaml): dt 1 ms x 20,
     PD every physics step, no delay, MJCF clamps, q_ref = q0 + 0.25 a."""
     c = H12FlatEnvCfg(mode=MODE_MUJOCO, decimation=20)
-    c.sim = replace(c.sim, dt=0.001, inner_steps=1)
+    c.sim = replace(c.sim, dt=0.001, inner_steps=1, implicit_penalty=False)
     c.actions.joint_pos.scale = 0.25
     for k, v in kw.items():
         setattr(c, k, v)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 4
+#define H12ENV_ABI_VERSION 5
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -60,6 +60,11 @@ extern "C" {
 #define H12_SCAN_NY 11
 #define H12_NSCAN (H12_SCAN_NX * H12_SCAN_NY) /* 187 */
 #define H12_NOBS_ROUGH (H12_ROUGH_FRAME + H12_NSCAN) /* 235 */
+
+/* max-joint-velocity damper: over the first H12_VLIM_RAMP rad/s of excess e the torque is -c e^2 / (2 ramp)
+ * (its slope, and with it the implicit joint inertia h dtau/dqd, grows from 0 to c), beyond it -c (e - ramp/2),
+ * so the dynamics stay continuous where a joint crosses its limit */
+#define H12_VLIM_RAMP 1.0f
 
 /* error codes */
 #define H12_OK 0
@@ -219,6 +224,17 @@ typedef struct h12env_config {
   float cstr_height, cstr_height_std; /* 1.0, 0.05 */
   float cstr_clearance_min;     /* 0.1 m */
   float cstr_clearance_deadzone;/* 0.2 */
+  /* ABI 5: the penalty springs / dampers (ground contacts, joint limits) integrated implicitly over the
+   * integration substep h: the force at the end of the substep, f(x + h v', v'), linearised in the
+   * acceleration -> an added point inertia h (c + h k) at each active contact and an added joint
+   * inertia h (c + h k) at each active limit in the dynamics solve */
+  int32_t implicit_penalty;
+  /* ABI 5: PhysX maxJointVelocity (the USD's joint velocity limits, converted from the URDF: 23 / 14 / 9 rad/s,
+   * IsaacLab write_joint_velocity_limit_to_sim).  Enforced like the other penalties, through the dynamics
+   * solve (so the reaction reaches the whole articulation): above the limit a joint damper
+   * -max_joint_vel_damping (|qd| - max) sign(qd), integrated implicitly; 0 = no limit (MuJoCo mode) */
+  float max_joint_vel[H12_NJ];
+  float max_joint_vel_damping; /* [N m s / rad]; C1 ramp-in over the first H12_VLIM_RAMP of excess (see below) */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */

@@ -256,9 +256,21 @@ static void kinematics(const h12env_model* m, const orc_phys* s, kin_t* k) {
  * capped by the Coulomb cone (mu_static to stick, mu_dynamic while slipping, anchor dragged
  * along when slipping); for knee / torso a viscous term capped at mu_dynamic.  Accumulates the
  * spatial force (body coords) into fext[b] and the world force into fw.  Returns 1 in contact. */
+/* implicit-penalty contacts of one solve: after the accelerations are known, the reported contact force
+ * gets the implicit part -Mw a_p (the force the linearised spring-damper applied over the substep) */
+typedef struct impl_rec {
+  int b;
+  double pl[3], Mw[3][3];
+  double* fw;
+} impl_rec;
+typedef struct impl_set {
+  int n;
+  impl_rec r[16];
+} impl_set;
+
 static int contact_point(const h12env_config* c, const kin_t* k, int b, const double pl[3], double rad,
                          double fext[NB][6], double fw[3], const double* anc_in, int was_in, double* anc_out,
-                         double mus, double mud) {
+                         double mus, double mud, double hi, m6 Madd[NB], double g, impl_set* rec) {
   double xw[3];
   m3v(k->R[b], pl, xw);
   for (int a = 0; a < 3; ++a) xw[a] += k->p[b][a];
@@ -272,13 +284,19 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   double vw[3];
   m3v(k->R[b], vl, vw);
   double vn = nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2];
-  double fn = c->contact_k * depth - c->contact_c * vn;
+  /* implicit contact (hi > 0): the spring-damper force at the END of the substep, k (d - hi vn') - c vn'
+   * with vn' = vn + hi an, is the explicit force with damping c + hi k plus the term -hi (c + hi k) an,
+   * linear in the contact point's acceleration: an added point inertia (alpha along the normal, beta
+   * tangentially while the stiction spring sticks / the viscous drag is below its cap) */
+  double cn = c->contact_c + hi * c->contact_k;
+  double fn = c->contact_k * depth - cn * vn;
   if (fn <= 0) return 0;
-  double ft0, ft1;
+  double ft0, ft1, beta = 0;
   if (anc_out) {
     double ax = was_in ? anc_in[0] : xw[0], ay = was_in ? anc_in[1] : xw[1];
-    ft0 = -c->friction_k * (xw[0] - ax) - c->friction_c * vw[0];
-    ft1 = -c->friction_k * (xw[1] - ay) - c->friction_c * vw[1];
+    double ct = c->friction_c + hi * c->friction_k;
+    ft0 = -c->friction_k * (xw[0] - ax) - ct * vw[0];
+    ft1 = -c->friction_k * (xw[1] - ay) - ct * vw[1];
     double ftn = sqrt(ft0 * ft0 + ft1 * ft1);
     if (ftn > mus * fn) {
       double sc = mud * fn / ftn;
@@ -286,6 +304,8 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
       ft1 *= sc;
       ax = xw[0] + ft0 / c->friction_k;
       ay = xw[1] + ft1 / c->friction_k;
+    } else {
+      beta = hi * ct;
     }
     anc_out[0] = ax;
     anc_out[1] = ay;
@@ -294,21 +314,64 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
     ft1 = -c->friction_c * vw[1];
     double ftn = sqrt(ft0 * ft0 + ft1 * ft1), cap = mud * fn;
     if (ftn > cap) { ft0 *= cap / ftn; ft1 *= cap / ftn; }
+    else beta = hi * c->friction_c;
   }
   /* normal force along the ground normal, tangential (stiction / drag) force in world xy */
   double F[3] = {ft0 + fn * nrm[0], ft1 + fn * nrm[1], fn * nrm[2]}, fl[3], nl[3];
+  if (hi > 0) {
+    /* world mass tensor Mw = alpha n n^T + beta (I - n n^T) -> body coords Mb = R^T Mw R; point inertia at
+     * pl: [[-px Mb px, px Mb], [-Mb px, Mb]].  The dynamics run with gravity as a base acceleration, which
+     * would weigh the added inertia: cancel with the force g Mw e_z at the point. */
+    double alpha = hi * cn, Mw[3][3], Mb[3][3], T[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Mw[i][j] = (alpha - beta) * nrm[i] * nrm[j] + (i == j ? beta : 0.0);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double t = 0;
+        for (int a = 0; a < 3; ++a) t += Mw[i][a] * k->R[b][a][j];
+        T[i][j] = t;
+      }
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double t = 0;
+        for (int a = 0; a < 3; ++a) t += k->R[b][a][i] * T[a][j];
+        Mb[i][j] = t;
+      }
+    m3 px = {{0, -pl[2], pl[1]}, {pl[2], 0, -pl[0]}, {-pl[1], pl[0], 0}}, PM, MP, PMP;
+    m3mul(px, Mb, PM);
+    m3mul(Mb, px, MP);
+    m3mul(PM, px, PMP);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        Madd[b][i][j] -= PMP[i][j];
+        Madd[b][i][3 + j] += PM[i][j];
+        Madd[b][3 + i][j] -= MP[i][j];
+        Madd[b][3 + i][3 + j] += Mb[i][j];
+      }
+    for (int a = 0; a < 3; ++a) F[a] += g * Mw[a][2];
+    if (rec && rec->n < 16) {
+      impl_rec* ir = &rec->r[rec->n++];
+      ir->b = b;
+      memcpy(ir->pl, pl, sizeof ir->pl);
+      memcpy(ir->Mw, Mw, sizeof ir->Mw);
+      ir->fw = fw;
+    }
+  }
+  /* reported force: the applied one (with the implicit part -Mw a added after the solve, implicit_report) */
+  for (int a = 0; a < 3; ++a) fw[a] += F[a];
   m3tv(k->R[b], F, fl);
   cross3(pl, fl, nl);
-  for (int a = 0; a < 3; ++a) { fext[b][a] += nl[a]; fext[b][3 + a] += fl[a]; fw[a] += F[a]; }
+  for (int a = 0; a < 3; ++a) { fext[b][a] += nl[a]; fext[b][3 + a] += fl[a]; }
   return 1;
 }
 
 /* evaluates every contact primitive; s->anchor/cmask are read, next_anchor/next_mask written */
 static void contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
                      double fext[NB][6], orc_contact_report* rep, double next_anchor[2][H12_NFOOT_PTS][2],
-                     int32_t* next_mask) {
-  orc_contact_report r;
-  memset(&r, 0, sizeof r);
+                     int32_t* next_mask, double hi, m6 Madd[NB], impl_set* rec) {
+  orc_contact_report local, *rr = rep ? rep : &local; /* written in place: implicit corrections follow */
+  memset(rr, 0, sizeof *rr);
+  if (!rep) rec = NULL;
   int32_t mask = 0;
   for (int f = 0; f < 2; ++f) {
     int b = 6 * f + 6; /* ankle roll link of leg f */
@@ -318,8 +381,8 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
       double tmp[2];
       double* out = next_anchor ? next_anchor[f][p] : tmp;
       double mus = s->env_params ? s->mu[f][0] : c->mu_static, mud = s->env_params ? s->mu[f][1] : c->mu_dynamic;
-      if (contact_point(c, k, b, pl, m->foot_radius, fext, r.foot_force[f], s->anchor[f][p], (s->cmask >> bit) & 1, out,
-                        mus, mud))
+      if (contact_point(c, k, b, pl, m->foot_radius, fext, rr->foot_force[f], s->anchor[f][p], (s->cmask >> bit) & 1, out,
+                        mus, mud, hi, Madd, m->gravity, rec))
         mask |= 1 << bit;
     }
     /* knee capsule: lower end point of the segment in world z */
@@ -328,8 +391,8 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
     double w0[3], w1[3];
     m3v(k->R[bk], a0, w0);
     m3v(k->R[bk], a1, w1);
-    contact_point(c, k, bk, (w0[2] <= w1[2]) ? a0 : a1, m->knee_radius, fext, r.knee_force[f], 0, 0, 0,
-                  c->mu_static, c->mu_dynamic);
+    contact_point(c, k, bk, (w0[2] <= w1[2]) ? a0 : a1, m->knee_radius, fext, rr->knee_force[f], 0, 0, 0,
+                  c->mu_static, c->mu_dynamic, hi, Madd, m->gravity, rec);
   }
   /* torso box (welded to the base): lowest corner */
   double corner[3];
@@ -337,15 +400,15 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
     double sg = k->R[0][2][a] > 0 ? -1.0 : 1.0;
     corner[a] = m->torso_center[a] + sg * m->torso_half[a];
   }
-  contact_point(c, k, 0, corner, 0.0, fext, r.torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic);
-  if (rep) *rep = r;
+  contact_point(c, k, 0, corner, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic, hi, Madd,
+                m->gravity, rec);
   if (next_mask) *next_mask = mask;
 }
 
 /* ------------------------------------------------------------------ dynamics */
 /* RNEA: generalised force for accelerations nudot (base spatial accel + qdd), with external forces */
 static void rnea(const h12env_model* m, const kin_t* k, const orc_phys* s, const double nudot[18],
-                 double fext[NB][6], double out[18]) {
+                 double fext[NB][6], m6 Madd[NB], double out[18]) {
   double a[NB][6], f[NB][6];
   for (int i = 0; i < 6; ++i) a[0][i] = nudot[i] - k->ag[i];
   for (int j = 0; j < NJ; ++j) {
@@ -363,6 +426,11 @@ static void rnea(const h12env_model* m, const kin_t* k, const orc_phys* s, const
     m6v(k->I[b], a[b], Ia);
     crf(k->v[b], Iv, t);
     for (int i = 0; i < 6; ++i) f[b][i] = Ia[i] + t[i] - fext[b][i];
+    if (Madd) {
+      double Ma[6];
+      m6v(Madd[b], a[b], Ma);
+      for (int i = 0; i < 6; ++i) f[b][i] += Ma[i];
+    }
   }
   for (int j = NJ - 1; j >= 0; --j) {
     int b = j + 1, par = m->parent[j] + 1;
@@ -374,9 +442,13 @@ static void rnea(const h12env_model* m, const kin_t* k, const orc_phys* s, const
   for (int i = 0; i < 6; ++i) out[i] = f[0][i];
 }
 
-static void crba(const h12env_model* m, const kin_t* k, double H[18 * 18]) {
+static void crba(const h12env_model* m, const kin_t* k, m6 Madd[NB], double H[18 * 18]) {
   m6 Ic[NB];
   memcpy(Ic, k->I, sizeof Ic);
+  if (Madd)
+    for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) Ic[b][i][j] += Madd[b][i][j];
   for (int j = NJ - 1; j >= 0; --j) {
     int b = j + 1, par = m->parent[j] + 1;
     m6 T;
@@ -407,12 +479,13 @@ static void crba(const h12env_model* m, const kin_t* k, double H[18 * 18]) {
 }
 
 static int aba(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
-               const double tau[NJ], const double dimpl[NJ], double fext[NB][6], double nudot[18]) {
+               const double tau[NJ], const double dimpl[NJ], double fext[NB][6], m6 Madd[NB], double nudot[18]) {
   m6 IA[NB];
   double pA[NB][6], cb[NB][6], U[NB][6], D[NB], u[NB];
   for (int b = 0; b < NB; ++b) {
     double Iv[6];
-    memcpy(IA[b], k->I[b], sizeof(m6));
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) IA[b][i][j] = k->I[b][i][j] + Madd[b][i][j];
     m6v(k->I[b], k->v[b], Iv);
     crf(k->v[b], Iv, pA[b]);
     for (int i = 0; i < 6; ++i) pA[b][i] -= fext[b][i];
@@ -470,28 +543,75 @@ static int aba(const h12env_model* m, const h12env_config* c, const kin_t* k, co
 int orc_mass_matrix(const h12env_model* m, const orc_phys* s, double M[18 * 18]) {
   kin_t k;
   kinematics(m, s, &k);
-  crba(m, &k, M);
+  crba(m, &k, NULL, M);
   for (int j = 0; j < NJ; ++j) M[(6 + j) * 18 + 6 + j] += m->armature[j];
   return 0;
 }
 
-static void joint_limit_torque(const h12env_model* m, const h12env_config* c, const orc_phys* s, double tau[NJ]) {
+/* joint-limit penalty (one-sided spring-damper outside the MJCF range).  With the implicit penalty (hi > 0)
+ * the torque at the end of the substep is linearised like the contacts: damping lc + hi lk, and dl[j]
+ * receives the added joint inertia hi (lc + hi lk) of an active limit. */
+static void joint_limit_torque(const h12env_model* m, const h12env_config* c, const orc_phys* s, double hi,
+                               double hdyn, double tau[NJ], double dl[NJ]) {
+  double cl = c->limit_c + hi * c->limit_k;
   for (int j = 0; j < NJ; ++j) {
     double q = s->q[j], qd = s->qd[j], t = 0;
-    if (q > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - c->limit_c * qd; if (t > 0) t = 0; }
-    else if (q < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - c->limit_c * qd; if (t < 0) t = 0; }
+    dl[j] = 0;
+    if (q > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - cl * qd; if (t > 0) t = 0; else dl[j] = hi * cl; }
+    else if (q < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - cl * qd; if (t < 0) t = 0; else dl[j] = hi * cl; }
+    /* PhysX max joint velocity: stiff damper on the excess, implicit over the substep (always: the solve
+     * must carry the reaction; h = 0 would make it explicit and unstable) */
+    double vm = c->max_joint_vel[j], cv = c->max_joint_vel_damping, ex = fabs(qd) - vm, rp = H12_VLIM_RAMP;
+    if (vm > 0 && cv > 0 && ex > 0) {
+      double mag = ex < rp ? cv * ex * ex / (2 * rp) : cv * (ex - 0.5 * rp);
+      t += qd > 0 ? -mag : mag;
+      dl[j] += hdyn * cv * (ex < rp ? ex / rp : 1.0);
+    }
     tau[j] += t;
   }
 }
 
+/* add the implicit part of every implicit-penalty contact to its reported force.  The linearised force is
+ * F_e - Mw a_p (a_p: the point's true acceleration); the solve runs in the gravity-shifted frame
+ * (accelerations a' = a - ag) where -Mw a_p = g Mw e_z - Mw a'_p: contact_point already added g Mw e_z
+ * (the weight-cancelling force), this adds -Mw a'_p */
+static void implicit_report(const h12env_model* m, const kin_t* k, const orc_phys* s, int fix_base,
+                            const double nudot[18], impl_set* rec) {
+  if (!rec->n) return;
+  double a[NB][6];
+  for (int i = 0; i < 6; ++i) a[0][i] = (fix_base ? 0.0 : nudot[i]) - k->ag[i];
+  for (int j = 0; j < NJ; ++j) {
+    int b = j + 1, par = m->parent[j] + 1;
+    double sq[6] = {0, 0, 0, 0, 0, 0}, t[6];
+    sq[m->axis[j]] = s->qd[j];
+    m6v(k->X[b], a[par], a[b]);
+    a[b][m->axis[j]] += nudot[6 + j];
+    crm(k->v[b], sq, t);
+    for (int i = 0; i < 6; ++i) a[b][i] += t[i];
+  }
+  for (int i = 0; i < rec->n; ++i) {
+    const impl_rec* r = &rec->r[i];
+    double ap[3], aw[3];
+    cross3(a[r->b], r->pl, ap);
+    for (int q = 0; q < 3; ++q) ap[q] += a[r->b][3 + q];
+    m3v(k->R[r->b], ap, aw);
+    for (int q = 0; q < 3; ++q) r->fw[q] -= r->Mw[q][0] * aw[0] + r->Mw[q][1] * aw[1] + r->Mw[q][2] * aw[2];
+  }
+}
+
 static int forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s, const double tau[NJ],
-                            int algo, double dt_impl, int with_contact, double nudot[18], orc_contact_report* rep,
-                            double next_anchor[2][H12_NFOOT_PTS][2], int32_t* next_mask) {
+                            int algo, double dt_impl, const double* dl, int with_contact, double nudot[18],
+                            orc_contact_report* rep, double next_anchor[2][H12_NFOOT_PTS][2], int32_t* next_mask) {
   kin_t k;
   kinematics(m, s, &k);
   double fext[NB][6];
+  m6 Madd[NB];
   memset(fext, 0, sizeof fext);
-  if (with_contact) contacts(m, c, &k, s, fext, rep, next_anchor, next_mask);
+  memset(Madd, 0, sizeof Madd);
+  impl_set rec;
+  rec.n = 0;
+  if (with_contact)
+    contacts(m, c, &k, s, fext, rep, next_anchor, next_mask, c->implicit_penalty ? dt_impl : 0.0, Madd, &rec);
   else {
     if (rep) memset(rep, 0, sizeof *rep);
     if (next_mask) *next_mask = 0;
@@ -500,14 +620,18 @@ static int forward_dynamics(const h12env_model* m, const h12env_config* c, const
   int mj = (c->mode == H12_MODE_MUJOCO);
   for (int j = 0; j < NJ; ++j) {
     double d = mj ? m->damping[j] : 0.0;
-    dimpl[j] = dt_impl * d;
+    dimpl[j] = dt_impl * d + (dl ? dl[j] : 0.0);
     tq[j] = tau[j] - d * s->qd[j];
     if (c->use_frictionloss) tq[j] -= m->frictionloss[j] * tanh(s->qd[j] / 0.01);
   }
-  if (algo == 1) return aba(m, c, &k, s, tq, dimpl, fext, nudot);
+  if (algo == 1) {
+    if (aba(m, c, &k, s, tq, dimpl, fext, Madd, nudot)) return -1;
+    implicit_report(m, &k, s, c->fix_base, nudot, &rec);
+    return 0;
+  }
   double H[18 * 18], C[18], zero[18] = {0};
-  crba(m, &k, H);
-  rnea(m, &k, s, zero, fext, C);
+  crba(m, &k, Madd, H);
+  rnea(m, &k, s, zero, fext, Madd, C);
   for (int j = 0; j < NJ; ++j) H[(6 + j) * 18 + 6 + j] += m->armature[j] + dimpl[j];
   double b[18];
   for (int i = 0; i < 6; ++i) b[i] = -C[i];
@@ -526,12 +650,13 @@ static int forward_dynamics(const h12env_model* m, const h12env_config* c, const
   }
   if (chol_solve(H, 18, b)) return -1;
   memcpy(nudot, b, sizeof b);
+  implicit_report(m, &k, s, 0, nudot, &rec);
   return 0;
 }
 
 int orc_forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s, const double tau[NJ],
                          int algo, double dt_impl, int with_contact, double nudot[18], orc_contact_report* rep) {
-  return forward_dynamics(m, c, s, tau, algo, dt_impl, with_contact, nudot, rep, 0, 0);
+  return forward_dynamics(m, c, s, tau, algo, dt_impl, NULL, with_contact, nudot, rep, 0, 0);
 }
 
 int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy, double lin[3], double ang[3]) {
@@ -602,12 +727,13 @@ int orc_physics_step(const h12env_model* m, const h12env_config* c, orc_phys* s,
   for (int it = 0; it < n; ++it) {
     double tau[NJ], nd[18];
     memcpy(tau, tau_pd, sizeof tau);
-    joint_limit_torque(m, c, s, tau);
+    double dl[NJ];
+    joint_limit_torque(m, c, s, c->implicit_penalty ? h : 0.0, h, tau, dl);
     orc_contact_report r;
     double nanc[2][H12_NFOOT_PTS][2];
     int32_t nmask = 0;
     memcpy(nanc, s->anchor, sizeof nanc);
-    if (forward_dynamics(m, c, s, tau, algo, h, with_contact, nd, &r, nanc, &nmask)) return -1;
+    if (forward_dynamics(m, c, s, tau, algo, h, dl, with_contact, nd, &r, nanc, &nmask)) return -1;
     double* pa = (double*)&acc;
     const double* pr = (const double*)&r;
     for (size_t i = 0; i < sizeof acc / sizeof(double); ++i) pa[i] += pr[i] / n;

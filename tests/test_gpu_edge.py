@@ -38,7 +38,8 @@ def test_ragged_env_counts_match_oracle(gpu, n):
         r_obs, r_rew, r_term, r_trunc, _ = ref.step(a, t)
         go = obs["policy"].cpu().numpy()
         ok = (np.abs(go - r_obs) <= 2e-3 * np.maximum(1, np.abs(r_obs))).all(axis=1)
-        assert ok.mean() >= (0.99 if n > 50 else 1.0 - 1.0 / n), (t, ok.mean())
+        # the suite's contact-state criterion (>= 99 % of envs), with at least one env of slack for small n
+        assert ok.mean() >= 1.0 - max(1.0, 0.01 * n) / n, (t, ok.mean())
         assert (trunc.cpu().numpy() == r_trunc).all()
         assert np.isfinite(rew.cpu().numpy()).all()
     env.close()

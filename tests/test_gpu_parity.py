@@ -37,6 +37,16 @@ def phys_fields(Fm):
     return out
 
 
+# the default integrator (one implicit-contact step per physics step) and the round-1 explicit scheme
+INTEGRATORS = {"implicit1": (1, True), "explicit2": (2, False)}
+
+
+def integrator_cfg(kind):
+    cfg = H12FlatEnvCfg()
+    cfg.sim.inner_steps, cfg.sim.implicit_penalty = INTEGRATORS[kind]
+    return cfg
+
+
 def scatter_states(env, ref, rng, height=(0.9, 1.3), contact=True):
     """Random but physical states written identically into the GPU workspace and the oracle."""
     n = env.num_envs
@@ -103,10 +113,11 @@ def test_physics_step_parity_free_flight(gpu):
     env.close()
 
 
-def test_physics_step_parity_contact(gpu):
+@pytest.mark.parametrize("integrator", list(INTEGRATORS))
+def test_physics_step_parity_contact(gpu, integrator):
     """States around standing height: penalty contact + stiction on most envs."""
     n = 1024
-    env = make(n)
+    env = make(n, integrator_cfg(integrator))
     env.reset()
     ref = O.OracleEnv(env._model, env._ccfg, n)
     ref.reset()
@@ -126,10 +137,11 @@ def test_physics_step_parity_contact(gpu):
     env.close()
 
 
-def test_env_step_parity(gpu):
+@pytest.mark.parametrize("integrator", list(INTEGRATORS))
+def test_env_step_parity(gpu, integrator):
     """Full MDP step (delayed PD, physics, sensor, terminations, rewards, resets, commands, obs)."""
     n = 512
-    env = make(n)
+    env = make(n, integrator_cfg(integrator))
     obs, _ = env.reset()
     ref = O.OracleEnv(env._model, env._ccfg, n)
     ref.reset()
