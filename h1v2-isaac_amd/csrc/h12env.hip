@@ -596,19 +596,19 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   for (int k = 0; k < NL; ++k) {
     float q = lg.q[k], qd = lg.qd[k];
     float t = tau_pd[k];
-    float tl = 0.f;
-    if (q > h12m::QHI[k]) tl = fminf(0.f, -P.lk * (q - h12m::QHI[k]) - P.lc * qd);
-    else if (q < h12m::QLO[k]) tl = fmaxf(0.f, -P.lk * (q - h12m::QLO[k]) - P.lc * qd);
+    // joint-limit penalty, branch-free (selects instead of divergent branches)
+    const float dhi = q - h12m::QHI[k], dlo = q - h12m::QLO[k];
+    const float thi = fminf(0.f, -P.lk * dhi - P.lc * qd), tlo = fmaxf(0.f, -P.lk * dlo - P.lc * qd);
+    const float tl = dhi > 0.f ? thi : (dlo < 0.f ? tlo : 0.f);
     t += tl;
     dl[k] = tl != 0.f ? P.dl : 0.f;
-    // PhysX max joint velocity: implicit stiff damper on the excess (oracle joint_limit_torque)
-    const float ex = fabsf(qd) - P.vmax[k];
-    if (ex > 0.f) {  // C1 ramp-in over H12_VLIM_RAMP (h12env.h)
-      const float r = fminf(ex * (1.f / H12_VLIM_RAMP), 1.f);
-      const float mag = ex < H12_VLIM_RAMP ? 0.5f * P.cv * ex * r : P.cv * (ex - 0.5f * H12_VLIM_RAMP);
-      t -= copysignf(mag, qd);
-      dl[k] += h * P.cv * r;
-    }
+    // PhysX max joint velocity: implicit stiff damper on the excess with a C1 ramp-in over H12_VLIM_RAMP
+    // (h12env.h; oracle joint_limit_torque); zero below the limit
+    const float ex = fmaxf(fabsf(qd) - P.vmax[k], 0.f);
+    const float r = fminf(ex * (1.f / H12_VLIM_RAMP), 1.f);
+    const float mag = ex < H12_VLIM_RAMP ? 0.5f * P.cv * ex * r : P.cv * (ex - 0.5f * H12_VLIM_RAMP);
+    t -= copysignf(mag, qd);
+    dl[k] += h * P.cv * r;
     t -= P.dimpl[k] * qd;
     if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
     tau[k] = t;
@@ -717,8 +717,24 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
 }
 
 // ------------------------------------------------------------------ state load / store
-H12_DEV float ldf(const Workspace& W, int f, int e) { return W.F[(size_t)f * W.n + e]; }
-H12_DEV void stf(const Workspace& W, int f, int e, float x) { W.F[(size_t)f * W.n + e] = x; }
+// Workspace access through buffer resources built from the kernargs (wave-uniform): the env's byte offset
+// e*4 is the one per-lane VGPR (voffset), the field offset f*n*4 an SGPR (soffset).  Flat global accesses
+// would keep a 64-bit address per field alive from the state loads to the stores (~200 registers).
+// h12env_create bounds n so that every offset fits in 32 bits.
+H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc(void* base) { return __builtin_amdgcn_make_buffer_rsrc(base, 0, -1, 0x00020000); }
+// f must be wave-uniform (soffset); a lane-dependent part of the field index (the leg) goes into lf
+H12_DEV float ldf(const Workspace& W, int f, int e, int lf = 0) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0));
+}
+H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), ws_rsrc(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0);
+}
+H12_DEV int ldi(const Workspace& W, int f, int e) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
+}
+H12_DEV void sti(const Workspace& W, int f, int e, int x) {
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
+}
 
 struct EnvSt {
   Base b;
@@ -743,19 +759,19 @@ H12_DEV void load_phys(const KParams& P, const Workspace& W, int e, int leg, Env
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
-    s.lg.q[k] = js * ldf(W, H12_F_Q + NL * leg + k, e);
-    s.lg.qd[k] = js * ldf(W, H12_F_QD + NL * leg + k, e);
-    s.act[k] = js * ldf(W, H12_F_ACT + NL * leg + k, e);
-    s.act1[k] = js * ldf(W, H12_F_ACT_PREV + NL * leg + k, e);
+    s.lg.q[k] = js * ldf(W, H12_F_Q + k, e, NL * leg);
+    s.lg.qd[k] = js * ldf(W, H12_F_QD + k, e, NL * leg);
+    s.act[k] = js * ldf(W, H12_F_ACT + k, e, NL * leg);
+    s.act1[k] = js * ldf(W, H12_F_ACT_PREV + k, e, NL * leg);
   }
-  int pk = W.I[(size_t)H12_I_PACK * W.n + e];
+  int pk = ldi(W, H12_I_PACK, e);
   int cm = (pk >> (13 + 4 * leg)) & 0xF;
   s.lg.cmask = 0;
 #pragma unroll
   for (int q = 0; q < H12_NFOOT_PTS; ++q) {
     int qr = leg ? (q ^ 1) : q;  // mirrored sole sphere q is real sphere q^1
-    s.lg.anc[q][0] = ldf(W, H12_F_ANCHOR + 8 * leg + 2 * qr, e);
-    s.lg.anc[q][1] = sg * ldf(W, H12_F_ANCHOR + 8 * leg + 2 * qr + 1, e);
+    s.lg.anc[q][0] = ldf(W, H12_F_ANCHOR + 2 * q, e, 8 * leg + 2 * (qr - q));
+    s.lg.anc[q][1] = sg * ldf(W, H12_F_ANCHOR + 2 * q + 1, e, 8 * leg + 2 * (qr - q));
     s.lg.cmask |= ((cm >> qr) & 1) << q;
   }
   for (int g = 0; g < 3; ++g) s.lag[g] = (pk >> (3 * g)) & 7;
@@ -763,8 +779,8 @@ H12_DEV void load_phys(const KParams& P, const Workspace& W, int e, int leg, Env
   s.is_heading = (pk >> 11) & 1;
   s.is_standing = (pk >> 12) & 1;
   const bool mu = Feat<K>::ext && P.env_mu;
-  s.lg.mus = mu ? ldf(W, H12_F_MU + 2 * leg, e) : P.mus;
-  s.lg.mud = mu ? ldf(W, H12_F_MU + 2 * leg + 1, e) : P.mud;
+  s.lg.mus = mu ? ldf(W, H12_F_MU, e, 2 * leg) : P.mus;
+  s.lg.mud = mu ? ldf(W, H12_F_MU + 1, e, 2 * leg) : P.mud;
   s.lg.dmass = (Feat<K>::ext && P.env_mass) ? ldf(W, H12_F_DMASS, e) : 0.f;
 }
 
@@ -774,18 +790,18 @@ H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvS
   for (int i = 0; i < 3; ++i) s.cmd[i] = ldf(W, H12_F_CMD + i, e);
   s.heading = ldf(W, H12_F_HEADING, e);
   s.cmd_time = ldf(W, H12_F_CMD_TIME, e);
-  s.air = ldf(W, H12_F_AIR + leg, e);
-  s.con = ldf(W, H12_F_CONTACT + leg, e);
-  s.last_air = ldf(W, H12_F_LAST_AIR + leg, e);
-  s.last_con = ldf(W, H12_F_LAST_CONTACT + leg, e);
+  s.air = ldf(W, H12_F_AIR, e, leg);
+  s.con = ldf(W, H12_F_CONTACT, e, leg);
+  s.last_air = ldf(W, H12_F_LAST_AIR, e, leg);
+  s.last_con = ldf(W, H12_F_LAST_CONTACT, e, leg);
   for (int t = 0; t < H12_NREW_FLAT; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
   for (int t = H12_NREW_FLAT; t < H12_NREW; ++t)
     s.epsum[t] = (Feat<K>::ext && P.rsl) ? ldf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e) : 0.f;
   s.push_t = (Feat<K>::ext && P.push) ? ldf(W, H12_F_PUSH_TIME, e) : 0.f;
-  s.eplen = W.I[(size_t)H12_I_EPLEN * W.n + e];
+  s.eplen = ldi(W, H12_I_EPLEN, e);
   if (Feat<K>::terrain) {
     for (int i = 0; i < 3; ++i) s.origin[i] = ldf(W, H12_F_ORIGIN + i, e);
-    s.tcell = W.I[(size_t)H12_I_TERRAIN * W.n + e];
+    s.tcell = ldi(W, H12_I_TERRAIN, e);
   } else {
     s.origin[0] = s.origin[1] = s.origin[2] = 0.f;
     s.tcell = 0;
@@ -799,11 +815,15 @@ H12_DEV void load_env(const KParams& P, const Workspace& W, int e, int leg, EnvS
 }
 
 template <int K>
-H12_DEV void store_env(const KParams& P, const Workspace& W, int e, int leg, const EnvSt& s) {
+H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, const EnvSt& s) {
   const float sg = leg ? -1.f : 1.f;
+  // an opaque copy of n made here: the field offsets of the stores are then computed here, not shared with the
+  // loads at the top of the kernel (68 SGPRs kept live across the physics loop spill to VGPR lanes)
+  Workspace W = W0;
+  asm volatile("" : "+s"(W.n));
   if (Feat<K>::terrain && leg == 0) {
     for (int i = 0; i < 3; ++i) stf(W, H12_F_ORIGIN + i, e, s.origin[i]);
-    W.I[(size_t)H12_I_TERRAIN * W.n + e] = s.tcell;
+    sti(W, H12_I_TERRAIN, e, s.tcell);
   }
   if (leg == 0) {
     for (int i = 0; i < 3; ++i) stf(W, H12_F_POS + i, e, s.b.pos[i]);
@@ -817,28 +837,28 @@ H12_DEV void store_env(const KParams& P, const Workspace& W, int e, int leg, con
     if (Feat<K>::ext && P.rsl)
       for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) stf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e, s.epsum[t]);
     if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
-    W.I[(size_t)H12_I_EPLEN * W.n + e] = s.eplen;
+    sti(W, H12_I_EPLEN, e, s.eplen);
   }
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
-    stf(W, H12_F_Q + NL * leg + k, e, js * s.lg.q[k]);
-    stf(W, H12_F_QD + NL * leg + k, e, js * s.lg.qd[k]);
-    stf(W, H12_F_ACT + NL * leg + k, e, js * s.act[k]);
-    stf(W, H12_F_ACT_PREV + NL * leg + k, e, js * s.act1[k]);
+    stf(W, H12_F_Q + k, e, js * s.lg.q[k], NL * leg);
+    stf(W, H12_F_QD + k, e, js * s.lg.qd[k], NL * leg);
+    stf(W, H12_F_ACT + k, e, js * s.act[k], NL * leg);
+    stf(W, H12_F_ACT_PREV + k, e, js * s.act1[k], NL * leg);
   }
   int cm_real = 0;
 #pragma unroll
   for (int q = 0; q < H12_NFOOT_PTS; ++q) {
     int qr = leg ? (q ^ 1) : q;
-    stf(W, H12_F_ANCHOR + 8 * leg + 2 * qr, e, s.lg.anc[q][0]);
-    stf(W, H12_F_ANCHOR + 8 * leg + 2 * qr + 1, e, sg * s.lg.anc[q][1]);
+    stf(W, H12_F_ANCHOR + 2 * q, e, s.lg.anc[q][0], 8 * leg + 2 * (qr - q));
+    stf(W, H12_F_ANCHOR + 2 * q + 1, e, sg * s.lg.anc[q][1], 8 * leg + 2 * (qr - q));
     cm_real |= ((s.lg.cmask >> q) & 1) << qr;
   }
-  stf(W, H12_F_AIR + leg, e, s.air);
-  stf(W, H12_F_CONTACT + leg, e, s.con);
-  stf(W, H12_F_LAST_AIR + leg, e, s.last_air);
-  stf(W, H12_F_LAST_CONTACT + leg, e, s.last_con);
+  stf(W, H12_F_AIR, e, s.air, leg);
+  stf(W, H12_F_CONTACT, e, s.con, leg);
+  stf(W, H12_F_LAST_AIR, e, s.last_air, leg);
+  stf(W, H12_F_LAST_CONTACT, e, s.last_con, leg);
   int cm_other = pair_swap_i(cm_real);
   if (leg == 0) {
     int pk = 0;
@@ -848,7 +868,7 @@ H12_DEV void store_env(const KParams& P, const Workspace& W, int e, int leg, con
     pk |= (s.is_standing & 1) << 12;
     pk |= (cm_real & 0xF) << 13;
     pk |= (cm_other & 0xF) << 17;
-    W.I[(size_t)H12_I_PACK * W.n + e] = pk;
+    sti(W, H12_I_PACK, e, pk);
   }
 }
 
@@ -2158,6 +2178,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   if (!model || !cfg || !out) return set_err(H12_E_ARG, "null argument");
   *out = nullptr;
   if (n_envs <= 0) return set_err(H12_E_ARG, "n_envs must be > 0 (got %d)", n_envs);
+  if ((int64_t)n_envs * H12_NF_FLOAT * 4 >= (int64_t)0x7FFFFFFF)  // buffer offsets of the workspace (ldf / stf)
+    return set_err(H12_E_ARG, "n_envs %d too large for one handle (max %d)", n_envs, 0x7FFFFFFF / (H12_NF_FLOAT * 4));
   if (env_offset < 0 || env_offset + (int64_t)n_envs > (int64_t)0xFFFFFFFFll)
     return set_err(H12_E_ARG, "global env ids must fit in 32 bits");
   if (cfg->abi_version != H12ENV_ABI_VERSION)
