@@ -2253,8 +2253,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->observe_calls = 0;
   // counted algorithmic FLOPs per env step (DESIGN.md "Roofline"): per inner step and leg lane
   // ~2.9k (pass 1 0.6k, contacts 0.35k, pass 2 1.5k, pass 3 0.25k, integration 0.1k), base combine +
-  // 6x6 solve ~0.3k per lane; MDP (rewards, resets, commands, obs, RNG) ~3k per env
-  h->flops_per_env = (double)cfg->decimation * cfg->inner_steps * 2.0 * (2900.0 + 300.0) + 3000.0;
+  // 6x6 solve ~0.3k per lane, implicit penalty terms (contact inertias and their force report, limit
+  // dampers) ~0.6k per lane; MDP (rewards, resets, commands, obs, RNG) ~3k per env
+  h->flops_per_env = (double)cfg->decimation * cfg->inner_steps * 2.0 *
+                         (2900.0 + 300.0 + (cfg->implicit_penalty ? 600.0 : 0.0)) + 3000.0;
   *out = (h12env*)h;
   return 0;
 }
