@@ -265,6 +265,8 @@ class H12VelocityEnv:
         self.reset_buf = self.reset_terminated
         self._log_ring = torch.zeros(_LOG_RING, NLOG, device=self.device)
         self._applied_torque = torch.zeros(n, NJ, device=self.device)
+        # |net contact force| of the left / right foot over the last physics step (ContactSensor of the feet)
+        self.foot_contact_force = torch.zeros(n, 2, device=self.device)
         self._out = H12StepOut()
         self.common_step_counter = 0
         self.extras: dict = {}
@@ -470,7 +472,7 @@ class H12VelocityEnv:
         o.truncated = self.reset_time_outs.data_ptr()
         o.log_acc = acc.data_ptr()
         o.applied_torque = self._applied_torque.data_ptr()
-        o.foot_force = None
+        o.foot_force = self.foot_contact_force.data_ptr()
         o.cstr_prob = self._dones.data_ptr() if self._cat else None
         rc = self._lib.h12env_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(prev.data_ptr()), C.byref(o),
                                    self.common_step_counter, self._stream())

@@ -162,6 +162,33 @@ def test_env_step_parity(gpu, integrator):
     env.close()
 
 
+@pytest.mark.parametrize("integrator", list(INTEGRATORS))
+def test_contact_force_and_torque_parity(gpu, integrator):
+    """One MDP step from identical generated near-ground states: the feet's reported net contact force (with the
+    implicit part -M a_p of the implicit integrator, added after the solve) and the applied joint torques agree
+    with the oracle (>= 99 % of envs; contact / slip decisions can flip within fp32 rounding)."""
+    n = 1024
+    env = make(n, integrator_cfg(integrator))
+    env.reset()
+    ref = O.OracleEnv(env._model, env._ccfg, n)
+    ref.reset()
+    rng = np.random.default_rng(7)
+    scatter_states(env, ref, rng, height=(0.95, 1.04))
+    a = rng.normal(size=(n, 12)).astype(np.float32) * 0.5
+    env.step(torch.from_numpy(a).cuda())
+    _, _, _, _, info = ref.step(a, 1)
+    torch.cuda.synchronize()
+    gf = env.foot_contact_force.cpu().numpy()
+    of = info["foot_force"]
+    assert (of > 1.0).mean() > 0.3  # most envs have a foot on the ground
+    okf = (np.abs(gf - of) <= 1e-2 * np.maximum(10.0, np.abs(of))).all(axis=1)
+    assert okf.mean() >= 0.99, okf.mean()
+    gt = env._applied_torque.cpu().numpy()
+    okt = (np.abs(gt - info["applied_torque"]) <= 2e-3 * np.maximum(1.0, np.abs(info["applied_torque"]))).all(axis=1)
+    assert okt.mean() >= 0.99, okt.mean()
+    env.close()
+
+
 def test_mujoco_mode_fixed_base_1000_steps(gpu):
     """north_star criterion on a contact-free segment: sim2sim semantics (1 kHz PD, x20 decimation,
     MJCF clamps, implicit joint damping), base welded 2 m up, 1000 policy steps of random actions:
