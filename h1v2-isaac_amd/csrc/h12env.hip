@@ -726,14 +726,19 @@ H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc(void* base) { return __builtin_amdgcn_mak
 H12_DEV float ldf(const Workspace& W, int f, int e, int lf = 0) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0));
 }
+#ifdef H12_DROP_STATE_STORES  // experiment builds only: price the state write-back (zero-record descriptor)
+H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0, 0x00020000); }
+#else
+H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return ws_rsrc(base); }
+#endif
 H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), ws_rsrc(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), ws_rsrc_st(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0);
 }
 H12_DEV int ldi(const Workspace& W, int f, int e) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
 }
 H12_DEV void sti(const Workspace& W, int f, int e, int x) {
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc_st(W.I), e * 4, f * W.n * 4, 0);
 }
 
 struct EnvSt {
@@ -1114,13 +1119,24 @@ H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, 
     for (int a = 0; a < 3; ++a) frame[(size_t)(o + 3 + a) * n + e] = -R[2][a];
     for (int a = 0; a < 3; ++a) frame[(size_t)(o + 6 + a) * n + e] = s.cmd[a];
   }
+  // joint rows: values materialised first, then stored back to back through a buffer resource (see store_env)
+  float jv[3 * NL];
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
-    int j = NL * leg + k;
-    frame[(size_t)(o + 9 + j) * n + e] = js * (s.lg.q[k] - h12m::Q0[k]);
-    frame[(size_t)(o + 21 + j) * n + e] = js * s.lg.qd[k];
-    frame[(size_t)(o + 33 + j) * n + e] = js * s.act[k];
+    jv[k] = js * (s.lg.q[k] - h12m::Q0[k]);
+    jv[NL + k] = js * s.lg.qd[k];
+    jv[2 * NL + k] = js * s.act[k];
+  }
+  for (auto& x : jv) asm volatile("" : "+v"(x));
+  __builtin_amdgcn_sched_barrier(0);
+  const auto rs = ws_rsrc(frame);
+  const int vo = (e + NL * leg * n) * 4;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, jv[k]), rs, vo, (o + 9 + k) * n * 4, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, jv[NL + k]), rs, vo, (o + 21 + k) * n * 4, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, jv[2 * NL + k]), rs, vo, (o + 33 + k) * n * 4, 0);
   }
 }
 
