@@ -737,8 +737,8 @@ H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
 H12_DEV int ldi(const Workspace& W, int f, int e) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
 }
-H12_DEV void sti(const Workspace& W, int f, int e, int x) {
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc_st(W.I), e * 4, f * W.n * 4, 0);
+H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) {
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc_st(W.I), (e + lf * W.n) * 4, f * W.n * 4, 0);
 }
 
 struct EnvSt {
@@ -830,19 +830,39 @@ H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, co
     for (int i = 0; i < 3; ++i) stf(W, H12_F_ORIGIN + i, e, s.origin[i]);
     sti(W, H12_I_TERRAIN, e, s.tcell);
   }
-  if (leg == 0) {
-    for (int i = 0; i < 3; ++i) stf(W, H12_F_POS + i, e, s.b.pos[i]);
-    for (int i = 0; i < 4; ++i) stf(W, H12_F_QUAT + i, e, s.b.quat[i]);
-    for (int i = 0; i < 3; ++i) stf(W, H12_F_VLIN + i, e, s.b.vlin[i]);
-    for (int i = 0; i < 3; ++i) stf(W, H12_F_WANG + i, e, s.b.wang[i]);
-    for (int i = 0; i < 3; ++i) stf(W, H12_F_CMD + i, e, s.cmd[i]);
-    stf(W, H12_F_HEADING, e, s.heading);
-    stf(W, H12_F_CMD_TIME, e, s.cmd_time);
-    for (int t = 0; t < H12_NREW_FLAT; ++t) stf(W, H12_F_EPSUM + t, e, s.epsum[t]);
-    if (Feat<K>::ext && P.rsl)
-      for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) stf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e, s.epsum[t]);
-    if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
-    sti(W, H12_I_EPLEN, e, s.eplen);
+  // Env-level fields (base, command, episode sums) hold bit-identical copies in both legs' lanes: each store
+  // instruction writes two of them, field f from the left lane and f + D from the right (lane offset leg * D).
+  // The write-back is bound by the chip-wide rate of store instructions, so this halves
+  // the 30 single-lane stores of this block.
+  // the right lane's value selected by bit masking: a ?: chain over neighbouring fields of one struct is turned
+  // into a dynamic index (scratch)
+  const uint32_t lm = 0u - (uint32_t)leg;
+  auto lsel = [lm](float a, float b) {
+    const uint32_t ua = __float_as_uint(a);
+    return __uint_as_float(ua ^ ((ua ^ __float_as_uint(b)) & lm));
+  };
+  {
+    const float bb[13] = {s.b.pos[0],  s.b.pos[1],  s.b.pos[2],  s.b.quat[0], s.b.quat[1], s.b.quat[2], s.b.quat[3],
+                          s.b.vlin[0], s.b.vlin[1], s.b.vlin[2], s.b.wang[0], s.b.wang[1], s.b.wang[2]};
+    static_assert(H12_F_QUAT == H12_F_POS + 3 && H12_F_VLIN == H12_F_POS + 7 && H12_F_WANG == H12_F_POS + 10,
+                  "base fields contiguous");
+#pragma unroll
+    for (int i = 0; i < 6; ++i) stf(W, H12_F_POS + i, e, lsel(bb[i], bb[i + 7]), 7 * leg);
+    static_assert(H12_F_HEADING == H12_F_CMD + 3 && H12_F_CMD_TIME == H12_F_CMD + 4, "command fields contiguous");
+    stf(W, H12_F_CMD, e, lsel(s.cmd[0], s.heading), 3 * leg);
+    stf(W, H12_F_CMD + 1, e, lsel(s.cmd[1], s.cmd_time), 3 * leg);
+#pragma unroll
+    for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(s.epsum[t], s.epsum[t + 6]), 6 * leg);
+    if (Feat<K>::ext && P.rsl) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        stf(W, H12_F_EPSUM2 + t, e, lsel(s.epsum[H12_NREW_FLAT + t], s.epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+    }
+    if (leg == 0) {
+      stf(W, H12_F_POS + 6, e, bb[6]);
+      stf(W, H12_F_CMD + 2, e, s.cmd[2]);
+      if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
+    }
   }
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
@@ -865,16 +885,16 @@ H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, co
   stf(W, H12_F_LAST_AIR, e, s.last_air, leg);
   stf(W, H12_F_LAST_CONTACT, e, s.last_con, leg);
   int cm_other = pair_swap_i(cm_real);
-  if (leg == 0) {
-    int pk = 0;
-    for (int g = 0; g < 3; ++g) pk |= (s.lag[g] & 7) << (3 * g);
-    pk |= (s.since_reset & 3) << 9;
-    pk |= (s.is_heading & 1) << 11;
-    pk |= (s.is_standing & 1) << 12;
-    pk |= (cm_real & 0xF) << 13;
-    pk |= (cm_other & 0xF) << 17;
-    sti(W, H12_I_PACK, e, pk);
-  }
+  int pk = 0;
+  for (int g = 0; g < 3; ++g) pk |= (s.lag[g] & 7) << (3 * g);
+  pk |= (s.since_reset & 3) << 9;
+  pk |= (s.is_heading & 1) << 11;
+  pk |= (s.is_standing & 1) << 12;
+  pk |= (cm_real & 0xF) << 13;  // the left lane's own masks are the left foot's: its pack is the one stored
+  pk |= (cm_other & 0xF) << 17;
+  // one instruction: the left lane stores the pack word, the right lane the (identical) episode length
+  static_assert(H12_I_EPLEN == 0 && H12_I_PACK == 1, "int fields");
+  sti(W, H12_I_EPLEN, e, (int)(((uint32_t)pk & ~lm) | ((uint32_t)s.eplen & lm)), 1 - leg);
 }
 
 // ------------------------------------------------------------------ MDP pieces
