@@ -45,34 +45,43 @@ class _SplitKLinearFn(torch.autograd.Function):
     """y = x W^T + b whose weight gradient dW = dY^T X is computed as SPLIT_K batched GEMMs over slices of the
     minibatch and summed: a (out x in) GEMM with K = 24576 gives hipBLASLt only ~17 output tiles for the 256
     CUs (measured 20 TFLOP/s); split 16 ways it runs 1.5x faster end to end (exp: fwd+bwd of both MLPs
-    2.19 -> 1.48 ms per minibatch).  Same math, fp32 summation order differs."""
+    2.19 -> 1.48 ms per minibatch).  Same math, fp32 summation order differs.  dt: the GEMM operand type
+    (float32, or bfloat16 under the bf16 learner's autocast: the partial products are summed in fp32 and the
+    gradients of the fp32 master weights are fp32)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, split):
-        ctx.save_for_backward(x, w)
-        ctx.split = split
-        return torch.addmm(b, x, w.t())
+    def forward(ctx, x, w, b, split, dt):
+        with torch.autocast(device_type="cuda", enabled=False):
+            xc, wc = x.to(dt), w.to(dt)
+            ctx.save_for_backward(xc, wc)
+            ctx.split, ctx.x_dtype = split, x.dtype
+            return torch.addmm(b.to(dt), xc, wc.t())
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
-        s, n = ctx.split, x.shape[0]
-        gx = gy @ w if ctx.needs_input_grad[0] else None
-        gw = torch.bmm(gy.view(s, n // s, -1).transpose(1, 2), x.view(s, n // s, -1)).sum(0)
-        return gx, gw, gy.sum(0), None
+        xc, wc = ctx.saved_tensors
+        s, n = ctx.split, xc.shape[0]
+        with torch.autocast(device_type="cuda", enabled=False):
+            gy = gy.to(wc.dtype)
+            gx = (gy @ wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+            gw = torch.bmm(gy.view(s, n // s, -1).transpose(1, 2), xc.view(s, n // s, -1))
+            gw = gw.sum(0) if gw.dtype == torch.float32 else gw.float().sum(0)
+            return gx, gw, gy.float().sum(0), None, None
 
 
 class SplitKLinear(nn.Linear):
-    """nn.Linear (same parameters / state dict) with the split-K weight gradient for large fp32 GPU batches."""
+    """nn.Linear (same parameters / state dict) with the split-K weight gradient for large GPU batches
+    (fp32, or bf16 operands under autocast)."""
 
     SPLIT_K = 16
     MIN_BATCH = 8192
 
     def forward(self, x):
-        if (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and self.weight.dtype == torch.float32
-                and torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda")
+        if (x.is_cuda and x.dim() == 2 and self.weight.dtype == torch.float32 and torch.is_grad_enabled()
                 and x.shape[0] >= self.MIN_BATCH and x.shape[0] % self.SPLIT_K == 0):
-            return _SplitKLinearFn.apply(x, self.weight, self.bias, self.SPLIT_K)
+            dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+            if x.dtype in (torch.float32, dt):
+                return _SplitKLinearFn.apply(x, self.weight, self.bias, self.SPLIT_K, dt)
         return nn.functional.linear(x, self.weight, self.bias)
 
 
