@@ -524,6 +524,139 @@ H12_DEV void link_pass3(const Leg& lg, const float (&cs)[NL][2], const float (&v
   a[A] += x;
 }
 
+// ---- flat ground: the 4 sole spheres of the foot in one pass.  On a plane every sphere has the same ground
+// normal (u = R^T e_z in foot coords), so the forces are summed in world axes (one rotation back for the
+// force, one for the moment: sum_q p_q x R^T F_q = R^T sum_q (R p_q) x F_q) and the implicit point
+// inertias M_q = beta_q I + gamma_q u u^T enter through their moments: sum beta, sum gamma, sum beta p,
+// sum gamma p, sum beta (|p|^2 I - p p^T), sum gamma p p^T (the p_q are model constants).  Same contact law
+// as contact_sphere<true, false> + ai_add_contact per sphere; only the summation order differs.
+struct SoleSums {
+  float sb, sg, pb[3], pg[3];  // sum beta, sum gamma, sum beta p, sum gamma p (foot coords)
+};
+constexpr float sole_j(int q, int k) {  // |p|^2 I - p p^T of sole sphere q, symmetric packing
+  const float* f = h12m::FOOT[q];
+  const float p2 = f[0] * f[0] + f[1] * f[1] + f[2] * f[2];
+  return k < 3 ? p2 - f[k] * f[k] : -(k == 3 ? f[0] * f[1] : (k == 4 ? f[0] * f[2] : f[1] * f[2]));
+}
+constexpr float sole_pp(int q, int k) {  // p p^T, symmetric packing
+  const float* f = h12m::FOOT[q];
+  return k < 3 ? f[k] * f[k] : (k == 3 ? f[0] * f[1] : (k == 4 ? f[0] * f[2] : f[1] * f[2]));
+}
+
+H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const float* pf, const float* vb, Leg& lg,
+                                AInertia& IA, float* pAcc, float* fw, SoleSums& ss) {
+  float ww[3], v0[3];  // foot angular velocity and origin velocity, world axes
+  mv(R, vb, ww);
+  mv(R, vb + 3, v0);
+  float F[3] = {0.f, 0.f, 0.f}, T[3] = {0.f, 0.f, 0.f};
+  float J[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, G[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ss = {};
+  int nmask = 0;
+  const float alpha = P.h * P.cc, hb = P.h * P.fc;
+#pragma unroll
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+    float r[3];
+    mv(R, h12m::FOOT[q], r);
+    const float depth = h12m::FOOT_R - (r[2] + pf[2]);
+    if (!(depth > 0.f)) continue;
+    float vw[3];
+    cross(ww, r, vw);
+    vw[0] += v0[0]; vw[1] += v0[1]; vw[2] += v0[2];
+    const float fn = P.ck * depth - P.cc * vw[2];
+    if (!(fn > 0.f)) continue;
+    const float x0 = r[0] + pf[0], x1 = r[1] + pf[1];
+    const bool was = (lg.cmask >> q) & 1;
+    float ax = was ? lg.anc[q][0] : x0, ay = was ? lg.anc[q][1] : x1;
+    float ft0 = -P.fk * (x0 - ax) - P.fc * vw[0];
+    float ft1 = -P.fk * (x1 - ay) - P.fc * vw[1];
+    const float ftn2 = ft0 * ft0 + ft1 * ft1, cap = lg.mus * fn;
+    const bool stick = !(ftn2 > cap * cap);
+    if (!stick) {
+      const float sc = lg.mud * fn * __builtin_amdgcn_rsqf(ftn2);
+      ft0 *= sc;
+      ft1 *= sc;
+      const float ik = frcp(P.fk);
+      ax = x0 + ft0 * ik;
+      ay = x1 + ft1 * ik;
+    }
+    lg.anc[q][0] = ax;
+    lg.anc[q][1] = ay;
+    nmask |= 1 << q;
+    float Fw[3] = {ft0, ft1, fn};
+    if (P.impl) {  // g M_w e_z = g (beta + gamma) e_z on a plane
+      const float beta = stick ? hb : 0.f, gam = alpha - beta;
+      Fw[2] += P.g * alpha;
+      ss.sb += beta;
+      ss.sg += gam;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ss.pb[i] += beta * h12m::FOOT[q][i];
+        ss.pg[i] += gam * h12m::FOOT[q][i];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        J[k] += beta * sole_j(q, k);
+        G[k] += gam * sole_pp(q, k);
+      }
+    }
+    float rf[3];
+    cross(r, Fw, rf);
+    F[0] += Fw[0]; F[1] += Fw[1]; F[2] += Fw[2];
+    T[0] += rf[0]; T[1] += rf[1]; T[2] += rf[2];
+  }
+  lg.cmask = nmask;
+  float fl[3], tl[3];
+  mtv(R, F, fl);
+  mtv(R, T, tl);
+  pAcc[0] -= tl[0]; pAcc[1] -= tl[1]; pAcc[2] -= tl[2];
+  pAcc[3] -= fl[0]; pAcc[4] -= fl[1]; pAcc[5] -= fl[2];
+  fw[0] += fl[0]; fw[1] += fl[1]; fw[2] += fl[2];
+  if (P.impl) {
+    const float u[3] = {R[2][0], R[2][1], R[2][2]};
+    // C += sum beta I + sum gamma u u^T
+    const float gu[3] = {ss.sg * u[0], ss.sg * u[1], ss.sg * u[2]};
+    IA.C[0] += ss.sb + gu[0] * u[0]; IA.C[1] += ss.sb + gu[1] * u[1]; IA.C[2] += ss.sb + gu[2] * u[2];
+    IA.C[3] += gu[0] * u[1]; IA.C[4] += gu[0] * u[2]; IA.C[5] += gu[1] * u[2];
+    // B += [sum beta p]x + (sum gamma p x u) u^T
+    IA.B[0][1] -= ss.pb[2]; IA.B[0][2] += ss.pb[1];
+    IA.B[1][0] += ss.pb[2]; IA.B[1][2] -= ss.pb[0];
+    IA.B[2][0] -= ss.pb[1]; IA.B[2][1] += ss.pb[0];
+    float c[3];
+    cross(ss.pg, u, c);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) IA.B[i][j] += c[i] * u[j];
+    // A += sum beta (|p|^2 I - p p^T) + [u]x G [u]x^T, G = sum gamma p p^T ((p x u)(p x u)^T = [u]x p p^T [u]x^T)
+    float Gf[3][3], Kx[3][3];
+    sym_full(G, Gf);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Kx[0][j] = -u[2] * Gf[1][j] + u[1] * Gf[2][j];
+      Kx[1][j] = u[2] * Gf[0][j] - u[0] * Gf[2][j];
+      Kx[2][j] = -u[1] * Gf[0][j] + u[0] * Gf[1][j];
+    }
+    auto mx = [&](int i, int j) {
+      return j == 0 ? -u[2] * Kx[i][1] + u[1] * Kx[i][2]
+                    : (j == 1 ? u[2] * Kx[i][0] - u[0] * Kx[i][2] : -u[1] * Kx[i][0] + u[0] * Kx[i][1]);
+    };
+    IA.A[0] += J[0] + mx(0, 0); IA.A[1] += J[1] + mx(1, 1); IA.A[2] += J[2] + mx(2, 2);
+    IA.A[3] += J[3] + mx(0, 1); IA.A[4] += J[4] + mx(0, 2); IA.A[5] += J[5] + mx(1, 2);
+  }
+}
+
+// implicit part of the sole forces from the moments of SoleSums (sum over q of impl_force)
+H12_DEV void sole_impl_force_flat(const float* a, const float R[3][3], const SoleSums& ss, float* f) {
+  const float u[3] = {R[2][0], R[2][1], R[2][2]};
+  float xb[3], xg[3];
+  cross(a, ss.pb, xb);
+  cross(a, ss.pg, xg);
+  const float gn = u[0] * xg[0] + u[1] * xg[1] + u[2] * xg[2] + ss.sg * (u[0] * a[3] + u[1] * a[4] + u[2] * a[5]);
+  f[0] -= xb[0] + ss.sb * a[3] + gn * u[0];
+  f[1] -= xb[1] + ss.sb * a[4] + gn * u[1];
+  f[2] -= xb[2] + ss.sb * a[5] + gn * u[2];
+}
+
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
 // lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
 template <int K>
@@ -570,7 +703,10 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
   float pAcc[6];
   bias<5>(v[5], pAcc);
-  {
+  SoleSums ss;
+  if constexpr (!Feat<K>::terrain) {
+    sole_contacts_flat(P, R, p, v[5], lg, IA, pAcc, fr.foot, ss);
+  } else {
     float fext[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int nmask = 0;
 #pragma unroll
@@ -688,7 +824,9 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   }
   link_pass3<4>(lg, cs, v, U, Dinv, u, a, qdd);
   link_pass3<5>(lg, cs, v, U, Dinv, u, a, qdd);
-  if (P.impl && lg.cmask) {  // implicit part of the sole forces (a = foot acceleration, shifted frame)
+  if constexpr (!Feat<K>::terrain) {
+    if (P.impl && lg.cmask) sole_impl_force_flat(a, R, ss, fr.foot);
+  } else if (P.impl && lg.cmask) {  // implicit part of the sole forces (a = foot acceleration, shifted frame)
     const float hb = P.h * P.fc, ha = P.h * P.cc;
 #pragma unroll
     for (int q = 0; q < H12_NFOOT_PTS; ++q) {
