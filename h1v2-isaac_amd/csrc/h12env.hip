@@ -1328,6 +1328,7 @@ struct AsmArgs {
   const uint8_t* sel;
   int reset_mode;
   int vec;  // obs and the source rows are 16-byte aligned
+  const int16_t* tab;  // gather table (asm_gather_table) for the whole-block path of step / observe, or null
   int n;
   int64_t env_offset;
   uint32_t lo, hi;
@@ -1379,8 +1380,9 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   constexpr int ROW = H12_OBS_FRAME * NH;
   constexpr int ASM_F4 = ASM_ROWS * ROW / 4;
   constexpr int ASM_CHUNKS = (ASM_F4 + 63) / 64;  // 1 KB LDS-DMA chunks (64 lanes x 16 B) per block
-  __shared__ __attribute__((aligned(16))) float s_hist[ASM_CHUNKS * 64 * 4];
-  __shared__ float s_frame[ASM_ROWS * H12_OBS_FRAME];  // noisy, scaled new frames
+  // rows, then the noisy scaled frames right behind them (the gather table addresses both from s_hist)
+  __shared__ __attribute__((aligned(16))) float s_hist[ASM_ROWS * (ROW + H12_OBS_FRAME)];
+  float* s_frame = s_hist + ASM_ROWS * ROW;
   __shared__ float s_noise[ASM_ROWS * 32];
   __shared__ uint32_t s_col[ROW];
   __shared__ int s_write[ASM_ROWS], s_fill[ASM_ROWS];
@@ -1402,12 +1404,22 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   float fv[NFR];
   if (full) {
     // rows -> LDS by LDS-DMA (global_load_lds_dwordx4): no register round trip, drained at the barrier
+    // (the last chunk's surplus lanes are masked off: the frames live right behind the rows)
     const int wave = tid >> 6, lane = tid & 63;
     for (int ch = wave; ch < ASM_CHUNKS; ch += ASM_BLOCK / 64) {
-      const float4* g = reinterpret_cast<const float4*>(src) + min(ch * 64 + lane, ASM_F4 - 1);
-      __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(s_hist + ch * 256),
-                                       16, 0, 0);
+      const float4* g = reinterpret_cast<const float4*>(src) + ch * 64 + lane;
+      if (ch * 64 + lane < ASM_F4)
+        __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(s_hist + ch * 256),
+                                         16, 0, 0);
     }
+  }
+  // gather path (step / observe, whole aligned blocks): each output float4 reads 4 int16 source offsets
+  const bool gather = full && !A.reset_mode && A.tab;
+  constexpr int NG = (ASM_F4 + ASM_BLOCK - 1) / ASM_BLOCK;
+  uint2 gt[NG];
+  if (gather) {
+#pragma unroll
+    for (int u = 0; u < NG; ++u) gt[u] = reinterpret_cast<const uint2*>(A.tab)[min(u * ASM_BLOCK + tid, ASM_F4 - 1)];
   }
 #pragma unroll
   for (int u = 0; u < NFR; ++u) {
@@ -1452,6 +1464,30 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   __syncthreads();
   // phase 3: assemble + store (obs may alias obs_prev: every read of these rows happened in phase 1)
   float* dst = A.obs + base;
+  if (gather) {
+    // a refilled row first gets its new frame in every slot of its LDS copy; then one branch-free gather
+    // (history slot -> the next-newer slot, newest slot -> the frame behind the rows) serves every row
+    int any_fill = 0;
+#pragma unroll
+    for (int r = 0; r < ASM_ROWS; ++r) any_fill |= s_fill[r];
+    if (any_fill) {  // block-uniform
+      for (int r = 0; r < ASM_ROWS; ++r)
+        if (s_fill[r])
+          for (int col = tid; col < ROW; col += ASM_BLOCK) s_hist[r * ROW + col] = s_frame[r * H12_OBS_FRAME + (s_col[col] & 0xFFu)];
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+      const int j = u * ASM_BLOCK + tid;
+      if (j < ASM_F4) {
+        const float* pb = s_hist + 4 * j;
+        const uint2 t = gt[u];
+        reinterpret_cast<float4*>(dst)[j] = make_float4(pb[0 + (int)(int16_t)(t.x & 0xFFFFu)], pb[1 + ((int)t.x >> 16)],
+                                                        pb[2 + (int)(int16_t)(t.y & 0xFFFFu)], pb[3 + ((int)t.y >> 16)]);
+      }
+    }
+    return;
+  }
   auto value = [&](int row, int col) -> float {
     const uint32_t t = s_col[col];
     const int p = row * ROW + col;
@@ -2001,6 +2037,7 @@ struct Handle {
   uint64_t dz_step = 0;
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
+  int16_t* asm_tab = nullptr;  // obs_assemble_kernel gather table for P.hist (Flat / Rsl layouts)
   std::vector<hipEvent_t> ev;  // 3 per timed step: before env kernel, between, after assembly
   size_t n_timed = 0;
 };
@@ -2183,6 +2220,32 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
 
 int n_blocks(const Handle* h) { return (h->W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
 
+// obs_assemble_kernel gather table for history length nh: for every float of an ASM_ROWS-row block (row r,
+// column col), the offset from its own position in the block's LDS copy to its source -- the next-newer
+// history slot (+3 / +12), or, for the newest slot, frame component c stored behind the rows
+// (asm_col_entry's mapping); 4 int16 per output float4
+std::vector<int16_t> asm_gather_table(int nh) {
+  const int row = H12_OBS_FRAME * nh, nf = ASM_ROWS * row;
+  std::vector<int16_t> t((size_t)nf, 0);
+  for (int p = 0; p < nf; ++p) {
+    const int r = p / row, col = p - r * row;
+    int hh, c, d;
+    if (col < 9 * nh) {
+      const int k = col / (3 * nh), q = col - 3 * nh * k;
+      hh = q / 3;
+      c = 3 * k + (q - 3 * hh);
+      d = 3;
+    } else {
+      const int k = (col - 9 * nh) / (12 * nh), q = col - 9 * nh - 12 * nh * k;
+      hh = q / 12;
+      c = 9 + 12 * k + (q - 12 * hh);
+      d = 12;
+    }
+    t[(size_t)p] = (int16_t)(hh == nh - 1 ? nf + H12_OBS_FRAME * r + c - p : d);
+  }
+  return t;
+}
+
 // feature level of the env kernels (Feat<K>)
 int feature_level(const KParams& P) {
   if (P.terrain) return 2;
@@ -2209,6 +2272,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.fill_b = fill_b;
   A.sel = sel;
   A.reset_mode = reset_mode;
+  A.tab = h->asm_tab;
   A.n = h->W.n;
   A.env_offset = h->env_offset;
   A.lo = lo;
@@ -2422,6 +2486,15 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     }
   }
   h->device = device;
+  if (h->P.task == H12_TASK_FLAT) {
+    const std::vector<int16_t> t = asm_gather_table(h->P.hist);
+    e = hipMalloc(&h->asm_tab, t.size() * sizeof(int16_t));
+    if (e == hipSuccess) e = hipMemcpy(h->asm_tab, t.data(), t.size() * sizeof(int16_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      h12env_destroy((h12env*)h);
+      return set_err(H12_E_ALLOC, "gather table: %s", hipGetErrorString(e));
+    }
+  }
   h->env_offset = env_offset;
   h->reset_calls = 0;
   h->observe_calls = 0;
@@ -2442,6 +2515,7 @@ void h12env_destroy(h12env* hh) {
   if (h->frame) (void)hipFree(h->frame);
   if (h->dz_cnt) (void)hipFree(h->dz_cnt);
   if (h->cat_mem) (void)hipFree(h->cat_mem);
+  if (h->asm_tab) (void)hipFree(h->asm_tab);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   delete h;
 }
