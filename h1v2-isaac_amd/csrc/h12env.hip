@@ -352,19 +352,20 @@ H12_DEV void solve6(const AInertia& I, const float* b, float* x) {
       M[3 + i][j] = I.B[j][i];
       M[3 + i][3 + j] = sget(I.C, i, j);
     }
-  float L[6][6], D[6], Dinv[6];
+  // T[i][j] = L[i][j] D[j] is the un-normalised column entry itself: one fma per term
+  float L[6][6], T[6][6], Dinv[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     float d = M[j][j];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
-    D[j] = d;
+    for (int k = 0; k < j; ++k) d -= L[j][k] * T[j][k];
     Dinv[j] = frcp(d);
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       float t = M[i][j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k] * D[k];
+      for (int k = 0; k < j; ++k) t -= L[i][k] * T[j][k];
+      T[i][j] = t;
       L[i][j] = t * Dinv[j];
     }
   }
