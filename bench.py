@@ -4,13 +4,20 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-One step = one ManagerBasedRLEnv.step of every env on the GPU (4 physics steps x 2 inner integration
-steps, delayed PD, contact, sensor, rewards, terminations, resets, commands, 450-float observations).
-Actions ~ N(0,1) are pre-generated and resident in HBM before timing.  Envs shard across ranks
-(4096 per GPU, weak scaling, RNG keyed by global env id); no collective inside the timed region.
+One step = one ManagerBasedRLEnv.step of every env on the GPU (4 physics steps of one implicit
+integration step each, delayed PD, contact, sensor, rewards, terminations, resets, commands,
+450-float observations).  Actions ~ N(0,1) are pre-generated and resident in HBM before timing.
+Envs shard across ranks (4096 per GPU, weak scaling, RNG keyed by global env id); no collective
+inside the timed region.
 
-Rank 0 prints ONE JSON line with the contract fields plus `roofline` (dominant kernel, measured with
-HIP events on the env's stream) and `cpu_baseline` (the CPU oracle on host cores, bounded sample).
+Steady state: episode_length_buf is randomised first (rsl_rl's init_at_random_ep_len) and a fixed
+burn-in (--burn-in, untimed, on top of --warmup) lets falls and time-outs reach their steady rate, so
+any --steps window sees representative resets.  After the timed window the workspace snapshot taken
+before it is restored and the SAME window is replayed (bit-identical, checked) to count its resets
+and to time each kernel with HIP events bound to the dispatches (the interval rocprofv3 reports).
+
+Rank 0 prints ONE JSON line with the contract fields plus `roofline` (dominant kernel) and
+`cpu_baseline` (the CPU oracle on host cores, bounded sample).
 """
 from __future__ import annotations
 
@@ -27,13 +34,17 @@ sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 METRIC = "env-steps/sec at 4096 envs, Velocity-Flat-H12_12dof, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: peak FP32 vector
+CLOCK_GHZ = 2.4             # MI355X_MICROARCH.md: max clock
+N_SIMD = 1024               # 256 CUs x 4 SIMDs
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=500)
+    p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--burn-in", type=int, default=300,
+                   help="untimed steps after randomising episode_length_buf, before --warmup (steady state)")
     p.add_argument("--envs", type=int, default=None, help="envs per GPU (the metric is quoted at 4096; C5 at 8192)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,19 +71,30 @@ def parse():
 
 
 def load_pmc(path):
-    """HBM bytes per launch of step_kernel / obs_assemble_kernel from a tools/profile.sh summary, used
-    only if it was measured on the current kernel source (sha256 of csrc/h12env.hip)."""
+    """Per-launch PMC figures of step_kernel / obs_assemble_kernel from a tools/profile.sh summary, used
+    only if they were measured on the current kernel source (sha256 of csrc/h12env.hip): HBM bytes
+    (FETCH_SIZE doubled + WRITE_SIZE per MI355X_MICROARCH.md) and the SQ wave / VALU-instruction counts."""
     import hashlib
     p = Path(path) if path else ROOT / "profiles" / "latest_pmc.json"
     if not p.exists():
-        return None, None, None
+        return {}, None
     d = json.loads(p.read_text())
     src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
     if d.get("source_sha256") != src:
-        return None, None, f"{p.name}: stale (kernel source changed)"
-    k = d.get("kernels", {})
-    return (k.get("step_kernel", {}).get("hbm_bytes_per_launch"), k.get("obs_assemble_kernel", {}).get("hbm_bytes_per_launch"),
-            f"{p.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH doubled per MI355X_MICROARCH.md)")
+        return {}, f"{p.name}: stale (kernel source changed)"
+    return d.get("kernels", {}), (f"{p.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH doubled "
+                                  f"per MI355X_MICROARCH.md; SQ_INSTS_VALU / SQ_WAVES)")
+
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(seconds: float):
@@ -119,6 +141,7 @@ def cpu_baseline(seconds: float):
               "sample": "C1: oracle MuJoCo mode (sim2sim semantics), 1 env x 1000 policy steps x 20 substeps, "
                         f"random q_ref, ground contact ({dt1:.2f} s)"}
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "single_env_sim2sim": mujoco,
             "sample": f"oracle/h12_oracle.c (fp64, OpenMP) on {n} envs x {steps} env steps "
                       f"({dt:.1f} s) of the same random-action Flat-H12 workload, {threads} host threads"}
@@ -234,11 +257,13 @@ def main():
     env = H12VelocityEnv(cfg, env_offset=rank * n)
     env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    K, W = args.steps, args.warmup
-    pool = min(K + W, 256)
+    K, W, B = args.steps, args.warmup, args.burn_in
+    pool = min(K + W + B, 256)
     actions = torch.randn(pool, n, 12, device=dev, generator=g)  # resident in HBM before timing
-
-    for i in range(W):
+    # rsl_rl OnPolicyRunner.learn(init_at_random_ep_len=True): spread the time-outs over the episode
+    env.episode_length_buf = torch.randint(0, env.max_episode_length, (n,), device=dev, generator=g,
+                                           dtype=torch.int32)
+    for i in range(B + W):
         env.step(actions[i % pool])
 
     def barrier():
@@ -247,9 +272,10 @@ def main():
         torch.cuda.synchronize(dev)
 
     barrier()
+    snap = env.snapshot()  # replayed below (reset count + kernel timing of the same window)
     t0 = time.perf_counter()
     for i in range(K):
-        env.step(actions[(W + i) % pool])
+        env.step(actions[(B + W + i) % pool])
     barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev)
@@ -260,15 +286,27 @@ def main():
         if rank == 0:
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * dt / K}))
         return
+    final_obs = env.get_observations()["policy"].clone()
 
-    # per-launch kernel durations with HIP events recorded by the library on the env's stream around
-    # each of its two kernels (separate pass, so the timed region above is not perturbed)
-    M = min(K, 200)
+    # replay of the timed window from the snapshot: count its resets and time each launch with HIP
+    # events bound to the dispatches (kernel begin / end, as rocprofv3 reports them); the replay must
+    # reproduce the timed window bit for bit
+    env.restore(snap)
+    resets = torch.zeros((), dtype=torch.int64, device=dev)
     env.set_kernel_timing(True)
-    for i in range(M):
-        env.step(actions[i % pool])
-    env_ms, obs_ms, n_timed = env.kernel_times()
+    env_ms = obs_ms = 0.0
+    n_timed = 0
+    for i in range(K):
+        env.step(actions[(B + W + i) % pool])
+        resets += (env.reset_terminated | env.reset_time_outs).sum()
+        if (i + 1) % 2048 == 0:  # the library keeps at most 4096 timed steps
+            a_ms, b_ms, c = env.kernel_times()
+            env_ms, obs_ms, n_timed = env_ms + a_ms, obs_ms + b_ms, n_timed + c
+    a_ms, b_ms, c = env.kernel_times()
+    env_ms, obs_ms, n_timed = env_ms + a_ms, obs_ms + b_ms, n_timed + c
     env.set_kernel_timing(False)
+    replay_exact = bool(torch.equal(env.get_observations()["policy"], final_obs))
+    resets_in_window = int(resets.item())
     kern_ms_avg = env_ms / n_timed
     obs_ms_avg = obs_ms / n_timed
     bytes_env, flops_env = env.kernel_cost(0)
@@ -278,7 +316,22 @@ def main():
     value = world * n * K / dt
     if rank == 0:
         achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
-        traffic, obs_traffic, pmc_src = load_pmc(args.pmc_file)
+        pmc, pmc_src = load_pmc(args.pmc_file)
+        traffic = pmc.get("step_kernel", {}).get("hbm_bytes_per_launch")
+        obs_traffic = pmc.get("obs_assemble_kernel", {}).get("hbm_bytes_per_launch")
+        # VALU issue roofline of step_kernel: one wave per SIMD issues at most one VALU instruction per
+        # 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost', one wave's stream on one SIMD), so
+        # the kernel's floor is (VALU instructions per wave) x 4 cycles at the 2.4 GHz max clock
+        sq = pmc.get("step_kernel", {}).get("SQ", {})
+        issue = None
+        if sq.get("SQ_WAVES") and sq.get("SQ_INSTS_VALU") and args.task == "flat" and n == 4096:
+            per_wave = sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]
+            floor_ms = per_wave * 4.0 / (CLOCK_GHZ * 1e9) * 1e3
+            issue = {"bound": "valu-issue, one wave per SIMD", "valu_insts_per_wave": per_wave,
+                     "waves": sq["SQ_WAVES"], "simds_in_use_frac": sq["SQ_WAVES"] / N_SIMD,
+                     "floor_ms": floor_ms, "frac": floor_ms / kern_ms_avg,
+                     "wait_frac": sq.get("SQ_WAIT_ANY", 0.0) / sq.get("SQ_WAVE_CYCLES", 1.0),
+                     "source": pmc_src}
         metric, workload = METRIC, "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X"
         if args.task in ("rsl", "cat"):
             tid = {"rsl": "Rsl-H12_12dof", "cat": "CaT-Flat-H12_12dof"}[args.task]
@@ -312,8 +365,14 @@ def main():
                 "implicit_penalty": bool(cfg.sim.implicit_penalty),
                 "parallelism": f"env-shard x{world}",
             },
+            "burn_in": B,
+            "resets_in_window": resets_in_window,
+            "replay_bit_exact": replay_exact,
             "roofline": {
+                # the contract prices the dominant kernel against HBM (the north_star's roofline); the
+                # binding limit of step_kernel at 4096 envs is VALU issue latency ("issue" below)
                 "bound": "hbm",
+                "binding": "valu-issue latency (one wave per SIMD, 1/8 of the SIMDs at 4096 envs)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -321,7 +380,9 @@ def main():
                 "traffic": traffic,
                 "kernel": "step_kernel",
                 "kernel_ms_avg": kern_ms_avg,
+                "kernel_timing": "HIP event pair bound to each dispatch (hipExtLaunchKernelGGL), replayed window",
                 "algorithmic_bytes_per_launch": bytes_env * n,
+                "issue": issue,
                 "traffic_source": pmc_src,
                 "valu_flops_per_env_step": flops_env,
                 "valu_tflops": flops_env * n / (kern_ms_avg * 1e-3) / 1e12,

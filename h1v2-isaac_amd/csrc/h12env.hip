@@ -19,6 +19,7 @@
 // between passes (bias forces and velocity-product accelerations are recomputed from them), MDP state
 // is loaded after the physics loop, and the contact-sensor timers are replayed from per-substep flags.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -2039,22 +2040,29 @@ struct Handle {
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
   int16_t* asm_tab = nullptr;  // obs_assemble_kernel gather table for P.hist (Flat / Rsl layouts)
-  std::vector<hipEvent_t> ev;  // 3 per timed step: before env kernel, between, after assembly
+  // kernel timing: 4 events per timed step bound to the launches themselves (hipExtLaunchKernelGGL:
+  // the events take the dispatch packet's begin / end timestamps, as rocprofv3's kernel trace does) --
+  // step_kernel begin / end, observation kernel begin / end
+  std::vector<hipEvent_t> ev;
   size_t n_timed = 0;
 };
 
 constexpr size_t MAX_TIMED_STEPS = 4096;
 
-void timing_mark(Handle* h, int k, hipStream_t stream) {
-  if (!h->timing || h->n_timed >= MAX_TIMED_STEPS) return;
-  size_t i = 3 * h->n_timed + k;
-  while (h->ev.size() <= i) {
+// the event pair of kernel k (0 = env kernel, 1 = observation kernel) of the current timed step, or nulls
+bool timing_events(Handle* h, int k, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!h->timing || h->n_timed >= MAX_TIMED_STEPS) return false;
+  const size_t i = 4 * h->n_timed + 2 * k;
+  while (h->ev.size() <= i + 1) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) { h->timing = false; return; }
+    if (hipEventCreate(&e) != hipSuccess) { h->timing = false; return false; }
     h->ev.push_back(e);
   }
-  (void)hipEventRecord(h->ev[i], stream);
-  if (k == 2) h->n_timed++;
+  *e0 = h->ev[i];
+  *e1 = h->ev[i + 1];
+  if (k == 1) h->n_timed++;
+  return true;
 }
 
 bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
@@ -2261,10 +2269,20 @@ int feature_level(const KParams& P) {
       default: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;               \
     }                                                                           \
   } while (0)
+// launch with an optional event pair bound to the dispatch (kernel timing)
+#define LAUNCH_KT(KERNEL, E0, E1, GRID, BLK, SHM, STREAM, ...)                                              \
+  do {                                                                                                      \
+    switch (feature_level(h->P)) {                                                                          \
+      case 0: hipExtLaunchKernelGGL(KERNEL<0>, GRID, BLK, SHM, STREAM, E0, E1, 0, __VA_ARGS__); break;      \
+      case 1: hipExtLaunchKernelGGL(KERNEL<1>, GRID, BLK, SHM, STREAM, E0, E1, 0, __VA_ARGS__); break;      \
+      default: hipExtLaunchKernelGGL(KERNEL<2>, GRID, BLK, SHM, STREAM, E0, E1, 0, __VA_ARGS__); break;     \
+    }                                                                                                       \
+  } while (0)
 
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
-                    const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream) {
+                    const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
+                    hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
   AsmArgs A = {};
   A.obs_prev = obs_prev;
   A.obs = obs;
@@ -2280,7 +2298,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.hi = hi;
   if (h->P.task == H12_TASK_ROUGH) {
     const int nb = (int)(((size_t)h->W.n * H12_NOBS_ROUGH + ASM_BLOCK - 1) / ASM_BLOCK);
-    hipLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A);
+    hipExtLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, h->P, A);
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -2288,7 +2306,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.vec = (((uintptr_t)obs | (uintptr_t)src) & 15u) == 0;
   const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
 #define H12_ASM_CASE(NH) \
-  case NH: hipLaunchKernelGGL(obs_assemble_kernel<NH>, dim3(nb), dim3(ASM_BLOCK), 0, stream, h->P, A); break;
+  case NH: hipExtLaunchKernelGGL(obs_assemble_kernel<NH>, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, h->P, A); break;
   switch (h->P.hist) {
     H12_ASM_CASE(1) H12_ASM_CASE(2) H12_ASM_CASE(3) H12_ASM_CASE(4) H12_ASM_CASE(5)
     H12_ASM_CASE(6) H12_ASM_CASE(7) H12_ASM_CASE(8) H12_ASM_CASE(9) H12_ASM_CASE(10)
@@ -2563,8 +2581,9 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   A.frame = h->frame;
   A.dz_slot = (int)(h->dz_step++ % 3);
-  timing_mark(h, 0, (hipStream_t)stream);
-  LAUNCH_K(step_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  hipEvent_t t0, t1;
+  timing_events(h, 0, &t0, &t1);
+  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (h->P.cat) {
     const dim3 cg((h->W.n + CAT_CHUNK - 1) / CAT_CHUNK, H12_NCSTR_COLS);
@@ -2577,12 +2596,10 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
                        (hipStream_t)stream, h->P, h->W, C);
     HIP_TRY(hipGetLastError());
   }
-  timing_mark(h, 1, (hipStream_t)stream);
+  timing_events(h, 1, &t0, &t1);
   // fill = terminated | truncated: the envs reset inside the step restart their history
-  int rc = launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
-                           (hipStream_t)stream);
-  timing_mark(h, 2, (hipStream_t)stream);
-  return rc;
+  return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
+                         (hipStream_t)stream, t0, t1);
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
@@ -2726,11 +2743,11 @@ int h12env_kernel_times(h12env* hh, double* env_ms, double* obs_ms, int* n_steps
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
   double a = 0.0, b = 0.0;
-  if (h->n_timed > 0) HIP_TRY(hipEventSynchronize(h->ev[3 * h->n_timed - 1]));
+  if (h->n_timed > 0) HIP_TRY(hipEventSynchronize(h->ev[4 * h->n_timed - 1]));
   for (size_t i = 0; i < h->n_timed; ++i) {
     float t0 = 0.f, t1 = 0.f;
-    HIP_TRY(hipEventElapsedTime(&t0, h->ev[3 * i], h->ev[3 * i + 1]));
-    HIP_TRY(hipEventElapsedTime(&t1, h->ev[3 * i + 1], h->ev[3 * i + 2]));
+    HIP_TRY(hipEventElapsedTime(&t0, h->ev[4 * i], h->ev[4 * i + 1]));
+    HIP_TRY(hipEventElapsedTime(&t1, h->ev[4 * i + 2], h->ev[4 * i + 3]));
     a += t0;
     b += t1;
   }

@@ -10,9 +10,9 @@ config:
   - actuators: packages/biped_assets/biped_assets/robots/h12.py:58-112 (DelayedPD, Kp/Kd/E, 0-5 delay)
   - commands: velocity_env_cfg.py:90-104 + flat_env_cfg.py:46-48
   - observations: velocity_env_cfg.py:124-132, flat_env_cfg.py:25-27 (no lin vel, history 10, noise on)
-  - events: rough_env_cfg.py:140-155 (x,y +-0.5, yaw +-3.14, joints x1.0, no push, no mass)
-  - rewards: rough_env_cfg.py:82-125, 174-183 + flat_env_cfg.py:35-44
-  - terminations: velocity_env_cfg.py:264-268 + rough_env_cfg.py:158-172
+  - events: rough_env_cfg.py:80-92 (x,y +-0.5, yaw +-3.14, joints x1.0, no push, no mass)
+  - rewards: rough_env_cfg.py:18-62 (term table), 111-120 (weights) + flat_env_cfg.py:35-44
+  - terminations: velocity_env_cfg.py:264-268 + rough_env_cfg.py:95-109 (illegal-contact bodies)
 """
 from __future__ import annotations
 

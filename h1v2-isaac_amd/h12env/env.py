@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import weakref
 from types import SimpleNamespace
 
 import torch
@@ -264,6 +265,7 @@ class H12VelocityEnv:
         self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=self.device)
         self.reset_buf = self.reset_terminated
         self._log_ring = torch.zeros(_LOG_RING, NLOG, device=self.device)
+        self._live_logs: dict = {}  # ring slot -> weakref of the _LazyLog reading it
         self._applied_torque = torch.zeros(n, NJ, device=self.device)
         # |net contact force| of the left / right foot over the last physics step (ContactSensor of the feet)
         self.foot_contact_force = torch.zeros(n, 2, device=self.device)
@@ -286,6 +288,8 @@ class H12VelocityEnv:
         self._cat = self.cfg.constraints is not None
         self._cstr_terms = self.cfg.constraints.active() if self._cat else []
         self._cp_terms = list(getattr(self.cfg.curriculum, "constraint_p", []) or []) if self._cat else []
+        self._cstr_p_pushed = None
+        self._cstr_p_buf = (C.c_float * NCSTR)()
         if self._cat:
             self.constraint_manager = _ConstraintManager(self)
             self._dones = torch.zeros(n, device=self.device)
@@ -388,9 +392,17 @@ class H12VelocityEnv:
         self._reward_map = m
 
     def _push_constraint_p(self):
-        c = self.cfg.to_c()
-        p = (C.c_float * NCSTR)(*c.cstr_max_p)
-        check(self._lib, self._lib.h12env_set_constraint_max_p(self._h, p, NCSTR), "h12env_set_constraint_max_p")
+        """max_p of the active constraint terms -> the kernel, only when a value changed (no config rebuild)."""
+        terms = dict(self.cfg.constraints.items())
+        vals = list(self._cstr_p_pushed) if self._cstr_p_pushed is not None else list(self._ccfg.cstr_max_p)
+        for name, cid in self._cstr_terms:
+            vals[cid] = float(terms[name].max_p)
+        if vals == self._cstr_p_pushed:
+            return
+        self._cstr_p_buf[:] = vals
+        check(self._lib, self._lib.h12env_set_constraint_max_p(self._h, self._cstr_p_buf, NCSTR),
+              "h12env_set_constraint_max_p")
+        self._cstr_p_pushed = vals
 
     def _constraint_curriculum(self):
         """modify_constraint_p runs in _reset_idx after the constraints of a step: step t uses the max_p
@@ -463,6 +475,13 @@ class H12VelocityEnv:
         obs = self._obs[self._k]
         slot = self.common_step_counter % _LOG_RING
         if slot % _LOG_CHUNK == 0:
+            # a step's _LazyLog reads its slot lazily: materialise (device ops, no sync) every log still
+            # alive in the chunk before the chunk is recycled
+            for s0 in range(slot, slot + _LOG_CHUNK):
+                ref = self._live_logs.pop(s0, None)
+                log = ref() if ref is not None else None
+                if log is not None:
+                    log._fill()
             self._log_ring[slot:slot + _LOG_CHUNK].zero_()
         acc = self._log_ring[slot]
         o = self._out
@@ -479,9 +498,9 @@ class H12VelocityEnv:
         if rc:
             check(self._lib, rc, "h12env_step")
         extra = {"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()} if self.terrain is not None else None
-        self.extras = {"log": _LazyLog(acc, self.max_episode_length_s, self._reward_terms, self._reward_map,
-                                       self._cstr_terms, extra),
-                       "time_outs": self.reset_time_outs}
+        log = _LazyLog(acc, self.max_episode_length_s, self._reward_terms, self._reward_map, self._cstr_terms, extra)
+        self._live_logs[slot] = weakref.ref(log)
+        self.extras = {"log": log, "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
         if self._cat:  # CaTEnv.step: dones = constraint termination probability, 1 where reset (cat_env.py:153-193)
             return {"policy": obs_out}, self.reward_buf, self._dones, self.reset_time_outs, self.extras
@@ -506,6 +525,20 @@ class H12VelocityEnv:
 
     def get_observations(self):
         return {"policy": self._obs[self._k]}
+
+    def snapshot(self) -> dict:
+        """Device copy of everything step() reads (workspace, both observation buffers, step counter), so a
+        window of steps can be replayed bit for bit with restore().  The library-internal carries of the
+        deadzone command count and the CaT running maxima are not included (Flat / Rough tasks only)."""
+        return {"state": self._state.clone(), "obs": [o.clone() for o in self._obs], "k": self._k,
+                "counter": self.common_step_counter}
+
+    def restore(self, snap: dict):
+        self._state.copy_(snap["state"])
+        for o, s in zip(self._obs, snap["obs"]):
+            o.copy_(s)
+        self._k = snap["k"]
+        self.common_step_counter = snap["counter"]
 
     def render(self, recompute: bool = False):
         return None

@@ -188,13 +188,24 @@ class EmpiricalNormalization(nn.Module):
 
     @torch.jit.unused
     def update(self, x):
+        """Running update from one batch; under torch.distributed (world > 1) the batch is the union of
+        every rank's shard (count, mean and variance all-reduced), so all ranks keep identical statistics."""
         if self.until is not None and self.count >= self.until:
             return
         n = x.shape[0]
-        self.count += n
-        rate = n / self.count
         var_x = torch.var(x, dim=0, unbiased=False, keepdim=True)
         mean_x = torch.mean(x, dim=0, keepdim=True)
+        if torch.distributed.is_available() and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            s = torch.cat([mean_x, var_x + mean_x * mean_x]) * n   # per-rank sum and sum of squares
+            cnt = torch.tensor([float(n)], device=x.device)
+            torch.distributed.all_reduce(s)
+            torch.distributed.all_reduce(cnt)
+            n = int(cnt.item())
+            mean_x = s[:1] / n
+            var_x = s[1:] / n - mean_x * mean_x
+        self.count += n
+        rate = n / self.count
         delta = mean_x - self._mean
         self._mean += rate * delta
         self._var += rate * (var_x - self._var + delta * (mean_x - self._mean))
@@ -612,8 +623,11 @@ class OnPolicyRunner:
         self.device = device
         self.env = env
         self.shard = getattr(env, "shard", None) or _shard_from_env()
+        # learner RNG per rank (IsaacLab's distributed train.py: seed + local rank), so the exploration noise
+        # and init_at_random_ep_len draws differ between shards; parameters are broadcast from rank 0 below.
+        # The env's own streams stay keyed by the global env id (shard-invariant trajectories).
         seed = int(train_cfg.get("seed", 1))
-        torch.manual_seed(seed)
+        torch.manual_seed(seed + self.shard.rank)
         obs, extras = env.get_observations()
         num_obs = obs.shape[1]
         critic_obs = extras["observations"].get("critic")

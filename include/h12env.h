@@ -11,7 +11,7 @@
  *                      .../velocity/config/h12_12dof/flat_env_cfg.py:13-48, rough_env_cfg.py:128-188;
  *                      robot cfg packages/biped_assets/biped_assets/robots/h12.py:18-114)
  *   h12env_reset       ManagerBasedRLEnv._reset_idx + reset events + ObservationManager.compute
- *                      (cat_env.py:195-248; rough_env_cfg.py:140-155; observation_manager.py:271-355)
+ *                      (cat_env.py:195-248; rough_env_cfg.py:80-92; observation_manager.py:271-355)
  *   h12env_step        ManagerBasedRLEnv.step (cat_env.py:95-193): action processing, 4 x (delayed PD
  *                      actuator -> PhysX step -> sensor update), terminations, rewards, resets,
  *                      commands, observations with 10-frame history (circular_buffer.py:79-170)
@@ -333,10 +333,11 @@ int h12env_step_cost(const h12env* h, double* bytes_per_env, double* flops_per_e
 /* Per-kernel accounting: kernel 0 = the env kernel of h12env_step (physics + MDP), 1 = the observation
  * assembly kernel (history shift + noise + fills).  Compulsory HBM bytes and counted FLOPs per env. */
 int h12env_kernel_cost(const h12env* h, int kernel, double* bytes_per_env, double* flops_per_env);
-/* Instrumentation (off by default): while enabled, h12env_step records HIP events around its two
- * kernels on the caller's stream (at most 4096 steps are kept).  h12env_kernel_times synchronises on
- * the last event, returns the summed milliseconds of each kernel and the number of timed steps, and
- * clears the record. */
+/* Instrumentation (off by default): while enabled, h12env_step launches step_kernel and the observation
+ * kernel with HIP event pairs bound to their dispatches (hipExtLaunchKernelGGL: begin / end of the kernel's
+ * execution, the interval rocprofv3's kernel trace reports; at most 4096 steps are kept).
+ * h12env_kernel_times synchronises on the last event, returns the summed milliseconds of each kernel and
+ * the number of timed steps, and clears the record. */
 int h12env_set_kernel_timing(h12env* h, int enable);
 int h12env_kernel_times(h12env* h, double* env_ms, double* obs_ms, int* n_steps);
 const char* h12env_last_error(void);

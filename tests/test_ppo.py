@@ -75,16 +75,34 @@ def test_runner_learns_toy_task(tmp_path):
 
 
 def _dp_worker(rank, world, port, q):
+    _dp_run(rank, world, port, q, empirical=False)
+
+
+def _dp_worker_norm(rank, world, port, q):
+    _dp_run(rank, world, port, q, empirical=True)
+
+
+def _dp_run(rank, world, port, q, empirical):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(100 + rank)  # different per-rank init: the broadcast must unify them
     env = RslRlVecEnvWrapper(ToyEnv(ToyEnvCfg(seed=rank, scene=type(ToyEnvCfg().scene)(num_envs=32))))
-    runner = OnPolicyRunner(env, small_cfg().to_dict(), log_dir=None, device="cpu")
+    runner = OnPolicyRunner(env, small_cfg(empirical_normalization=empirical).to_dict(), log_dir=None, device="cpu")
     runner.learn(3)
     flat = torch.cat([p.detach().reshape(-1) for p in runner.alg.policy.parameters()])
-    q.put((rank, flat.numpy().tobytes()))
+    if empirical:
+        # learner RNG seeded with seed + rank: the same observation draws different exploration noise on
+        # each rank; the observation normaliser sees the union of the shards: identical statistics
+        x = torch.zeros(4, 6)
+        with torch.inference_mode():
+            a = runner.alg.act(x, x).clone()
+        stats = torch.cat([runner.obs_normalizer._mean.reshape(-1), runner.obs_normalizer._var.reshape(-1),
+                           runner.obs_normalizer.count.reshape(-1).float()])
+        q.put((rank, (flat.numpy().tobytes(), a.numpy().tobytes(), stats.numpy().tobytes())))
+    else:
+        q.put((rank, flat.numpy().tobytes()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -104,3 +122,22 @@ def test_two_rank_data_parallel_ranks_stay_identical():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0] == res[1]
+
+
+def test_two_rank_noise_differs_and_normaliser_is_shared():
+    import multiprocessing as mp
+    import random
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    ps = [ctx.Process(target=_dp_worker_norm, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0]          # parameters identical
+    assert res[0][1] != res[1][1]          # exploration noise differs between ranks
+    assert res[0][2] == res[1][2]          # normaliser statistics identical
