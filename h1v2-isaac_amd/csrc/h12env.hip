@@ -1561,6 +1561,117 @@ __global__ void __launch_bounds__(ASM_BLOCK) rough_obs_kernel(KParams P, AsmArgs
 }
 
 // ------------------------------------------------------------------ kernels
+// The reward terms of one env on its post-physics, pre-reset state (RewardManager.compute's term functions,
+// unweighted; SURVEY.md a8.1-a8.12 + the Rsl extras), shared by step_kernel and the term-evaluation hook
+// (terms_kernel).  The lane pair holds the two legs: leg sums are combined with one DPP swap (psum).
+template <int K>
+H12_DEV void mdp_terms(const KParams& P, const EnvSt& s, int leg, const float R[3][3], const float* tau,
+                       const float* jacc, float fmax_foot, int term, float* terms) {
+  const float sg = leg ? -1.f : 1.f;
+  float ww[3];
+  mv(R, s.b.wang, ww);
+  float vcom[3];
+  base_com_vel<K>(P, s, R, vcom);
+  // yaw frame: heading direction of the body x axis in the world xy-plane
+  float hx = R[0][0], hy = R[1][0];
+  float hn = __builtin_amdgcn_rsqf(hx * hx + hy * hy);
+  float cy = hx * hn, sy = hy * hn;
+  float vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
+  float ex = s.cmd[0] - vy0, ey = s.cmd[1] - vy1, ew = s.cmd[2] - ww[2];
+  terms[H12_R_TRACK_LIN_VEL_XY] = __expf(-(ex * ex + ey * ey) * P.std2_inv);
+  terms[H12_R_TRACK_ANG_VEL_Z] = __expf(-(ew * ew) * P.std2_inv);
+  terms[H12_R_ANG_VEL_XY_L2] = s.b.wang[0] * s.b.wang[0] + s.b.wang[1] * s.b.wang[1];
+  float st_ = 0.f, sa_ = 0.f, sr_ = 0.f, sl_ = 0.f, sd_ = 0.f;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    st_ += tau[k] * tau[k];
+    sa_ += jacc[k] * jacc[k];
+    float dr = s.act[k] - s.act1[k];
+    sr_ += dr * dr;
+  }
+#pragma unroll
+  for (int k = 4; k < 6; ++k) {  // ankle pitch / roll soft limits (symmetric under the mirror)
+    float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
+    sl_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
+  }
+  sd_ = fabsf(s.lg.q[0] - h12m::Q0[0]) + fabsf(s.lg.q[2] - h12m::Q0[2]);  // hip yaw, hip roll
+  auto psum = [&](float x) {
+    float y = pair_swap(x);
+    return leg ? (y + x) : (x + y);
+  };
+  terms[H12_R_DOF_TORQUES_L2] = psum(st_);
+  terms[H12_R_DOF_ACC_L2] = psum(sa_);
+  terms[H12_R_ACTION_RATE_L2] = psum(sr_);
+  {
+    float con_o = pair_swap(s.con), air_o = pair_swap(s.air);
+    float conL = leg ? con_o : s.con, conR = leg ? s.con : con_o;
+    float airL = leg ? air_o : s.air, airR = leg ? s.air : air_o;
+    int incL = conL > 0.f, incR = conR > 0.f;
+    float mL = incL ? conL : airL, mR = incR ? conR : airR;
+    float r = ((incL + incR) == 1) ? fminf(mL, mR) : 0.f;
+    r = fminf(r, P.air_thr);
+    float cn2 = s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1];
+    terms[H12_R_FEET_AIR_TIME] = cn2 > 0.01f ? r : 0.f;
+  }
+  terms[H12_R_FLAT_ORIENTATION_L2] = R[2][0] * R[2][0] + R[2][1] * R[2][1];
+  terms[H12_R_DOF_POS_LIMITS] = psum(sl_);
+  terms[H12_R_TERMINATION] = term ? 1.f : 0.f;
+  {
+    // feet_slide: |v_xy| of the foot COM (lane frame; the norm is mirror-invariant) where max_h |F| > 1
+    float fs = 0.f;
+    if (fmax_foot > 1.0f) {
+      const float mm[3] = {1.f, sg, 1.f};
+      float Rf[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Rf[i][j] = mm[i] * mm[j] * R[i][j];
+      float vb[3];
+      mtv(R, s.b.vlin, vb);
+      float v0[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
+      for (int i = 0; i < 6; ++i) v0[i] *= s6(i, sg);
+      float csd[NL][2], vd[NL][6], pd[3] = {0.f, 0.f, 0.f};
+      link_pass1<0>(s.lg, csd, v0, vd, Rf, pd);
+      link_pass1<1>(s.lg, csd, vd[0], vd, Rf, pd);
+      link_pass1<2>(s.lg, csd, vd[1], vd, Rf, pd);
+      link_pass1<3>(s.lg, csd, vd[2], vd, Rf, pd);
+      link_pass1<4>(s.lg, csd, vd[3], vd, Rf, pd);
+      link_pass1<5>(s.lg, csd, vd[4], vd, Rf, pd);
+      float vc[3], vw[3];
+      cross(vd[5], h12m::COM[5], vc);
+      vc[0] += vd[5][3]; vc[1] += vd[5][4]; vc[2] += vd[5][5];
+      mv(Rf, vc, vw);
+      fs = fsqrt(vw[0] * vw[0] + vw[1] * vw[1]);
+    }
+    terms[H12_R_FEET_SLIDE] = psum(fs);
+  }
+  terms[H12_R_JOINT_DEV_HIP] = psum(sd_);
+  // terms of the Rsl table (rsl_env_cfg.py:279-407), base-frame tracking and the extra penalties
+  if (Feat<K>::ext) {
+    for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) terms[t] = 0.f;
+    if (P.rsl) {
+      float vb[3];
+      mtv(R, vcom, vb);  // root_lin_vel_b (composite COM velocity in the base frame)
+      float bx = s.cmd[0] - vb[0], by = s.cmd[1] - vb[1], bw = s.cmd[2] - s.b.wang[2];
+      terms[H12_R_TRACK_LIN_VEL_XY_BASE] = __expf(-(bx * bx + by * by) * P.std2_inv);
+      terms[H12_R_TRACK_ANG_VEL_Z_BASE] = __expf(-(bw * bw) * P.std2_inv);
+      float dh = s.b.pos[2] - P.h_target;
+      terms[H12_R_BASE_HEIGHT_L2] = dh * dh;
+      float sv_ = 0.f, sh_ = 0.f;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) sv_ += s.lg.qd[k] * s.lg.qd[k];
+#pragma unroll
+      for (int k = 0; k < 3; k += 2) {  // hip yaw (0), hip roll (2) soft limits
+        float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
+        sh_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
+      }
+      terms[H12_R_JOINT_VEL_L2] = psum(sv_);
+      terms[H12_R_JOINT_DEV_ANKLE] = psum(fabsf(s.lg.q[4] - h12m::Q0[4]) + fabsf(s.lg.q[5] - h12m::Q0[5]));
+      terms[H12_R_DOF_POS_LIMITS_HIP] = psum(sh_);
+      terms[H12_R_CONTACT_FORCES] = psum(fmaxf(fmax_foot - P.cf_thr, 0.f));
+      terms[H12_R_LIN_VEL_Z_L2] = vb[2] * vb[2];
+    }
+  }
+}
+
 struct StepArgs {
   const float* actions;
   const float* obs_prev;
@@ -1668,110 +1779,9 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     // ---- rewards on the pre-reset state
     float R[3][3];
     quat_R(s.b.quat, R);
-    float ww[3];
-    mv(R, s.b.wang, ww);
-    float vcom[3];
-    base_com_vel<K>(P, s, R, vcom);
-    // yaw frame: heading direction of the body x axis in the world xy-plane
-    float hx = R[0][0], hy = R[1][0];
-    float hn = __builtin_amdgcn_rsqf(hx * hx + hy * hy);
-    float cy = hx * hn, sy = hy * hn;
-    float vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
     float terms[H12_NREW];
-    float ex = s.cmd[0] - vy0, ey = s.cmd[1] - vy1, ew = s.cmd[2] - ww[2];
-    terms[H12_R_TRACK_LIN_VEL_XY] = __expf(-(ex * ex + ey * ey) * P.std2_inv);
-    terms[H12_R_TRACK_ANG_VEL_Z] = __expf(-(ew * ew) * P.std2_inv);
-    terms[H12_R_ANG_VEL_XY_L2] = s.b.wang[0] * s.b.wang[0] + s.b.wang[1] * s.b.wang[1];
-    float st_ = 0.f, sa_ = 0.f, sr_ = 0.f, sl_ = 0.f, sd_ = 0.f;
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      st_ += tau[k] * tau[k];
-      sa_ += jacc[k] * jacc[k];
-      float dr = s.act[k] - s.act1[k];
-      sr_ += dr * dr;
-    }
-#pragma unroll
-    for (int k = 4; k < 6; ++k) {  // ankle pitch / roll soft limits (symmetric under the mirror)
-      float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
-      sl_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
-    }
-    sd_ = fabsf(s.lg.q[0] - h12m::Q0[0]) + fabsf(s.lg.q[2] - h12m::Q0[2]);  // hip yaw, hip roll
-    auto psum = [&](float x) {
-      float y = pair_swap(x);
-      return leg ? (y + x) : (x + y);
-    };
-    terms[H12_R_DOF_TORQUES_L2] = psum(st_);
-    terms[H12_R_DOF_ACC_L2] = psum(sa_);
-    terms[H12_R_ACTION_RATE_L2] = psum(sr_);
-    {
-      float con_o = pair_swap(s.con), air_o = pair_swap(s.air);
-      float conL = leg ? con_o : s.con, conR = leg ? s.con : con_o;
-      float airL = leg ? air_o : s.air, airR = leg ? s.air : air_o;
-      int incL = conL > 0.f, incR = conR > 0.f;
-      float mL = incL ? conL : airL, mR = incR ? conR : airR;
-      float r = ((incL + incR) == 1) ? fminf(mL, mR) : 0.f;
-      r = fminf(r, P.air_thr);
-      float cn2 = s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1];
-      terms[H12_R_FEET_AIR_TIME] = cn2 > 0.01f ? r : 0.f;
-    }
-    terms[H12_R_FLAT_ORIENTATION_L2] = R[2][0] * R[2][0] + R[2][1] * R[2][1];
-    terms[H12_R_DOF_POS_LIMITS] = psum(sl_);
-    terms[H12_R_TERMINATION] = term ? 1.f : 0.f;
-    {
-      // feet_slide: |v_xy| of the foot COM (lane frame; the norm is mirror-invariant) where max_h |F| > 1
-      float fs = 0.f;
-      if (fmax_foot > 1.0f) {
-        const float mm[3] = {1.f, sg, 1.f};
-        float Rf[3][3];
-        for (int i = 0; i < 3; ++i)
-          for (int j = 0; j < 3; ++j) Rf[i][j] = mm[i] * mm[j] * R[i][j];
-        float vb[3];
-        mtv(R, s.b.vlin, vb);
-        float v0[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
-        for (int i = 0; i < 6; ++i) v0[i] *= s6(i, sg);
-        float csd[NL][2], vd[NL][6], pd[3] = {0.f, 0.f, 0.f};
-        link_pass1<0>(s.lg, csd, v0, vd, Rf, pd);
-        link_pass1<1>(s.lg, csd, vd[0], vd, Rf, pd);
-        link_pass1<2>(s.lg, csd, vd[1], vd, Rf, pd);
-        link_pass1<3>(s.lg, csd, vd[2], vd, Rf, pd);
-        link_pass1<4>(s.lg, csd, vd[3], vd, Rf, pd);
-        link_pass1<5>(s.lg, csd, vd[4], vd, Rf, pd);
-        float vc[3], vw[3];
-        cross(vd[5], h12m::COM[5], vc);
-        vc[0] += vd[5][3]; vc[1] += vd[5][4]; vc[2] += vd[5][5];
-        mv(Rf, vc, vw);
-        fs = fsqrt(vw[0] * vw[0] + vw[1] * vw[1]);
-      }
-      terms[H12_R_FEET_SLIDE] = psum(fs);
-    }
-    terms[H12_R_JOINT_DEV_HIP] = psum(sd_);
-    // terms of the Rsl table (rsl_env_cfg.py:279-407), base-frame tracking and the extra penalties
+    mdp_terms<K>(P, s, leg, R, tau, jacc, fmax_foot, term, terms);
     constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
-    if (Feat<K>::ext) {
-      for (int t = H12_NREW_FLAT; t < H12_NREW; ++t) terms[t] = 0.f;
-      if (P.rsl) {
-        float vb[3];
-        mtv(R, vcom, vb);  // root_lin_vel_b (composite COM velocity in the base frame)
-        float bx = s.cmd[0] - vb[0], by = s.cmd[1] - vb[1], bw = s.cmd[2] - s.b.wang[2];
-        terms[H12_R_TRACK_LIN_VEL_XY_BASE] = __expf(-(bx * bx + by * by) * P.std2_inv);
-        terms[H12_R_TRACK_ANG_VEL_Z_BASE] = __expf(-(bw * bw) * P.std2_inv);
-        float dh = s.b.pos[2] - P.h_target;
-        terms[H12_R_BASE_HEIGHT_L2] = dh * dh;
-        float sv_ = 0.f, sh_ = 0.f;
-#pragma unroll
-        for (int k = 0; k < NL; ++k) sv_ += s.lg.qd[k] * s.lg.qd[k];
-#pragma unroll
-        for (int k = 0; k < 3; k += 2) {  // hip yaw (0), hip roll (2) soft limits
-          float q = s.lg.q[k], lo_s = soft_lo(P, k), hi_s = soft_hi(P, k);
-          sh_ += (q < lo_s ? lo_s - q : 0.f) + (q > hi_s ? q - hi_s : 0.f);
-        }
-        terms[H12_R_JOINT_VEL_L2] = psum(sv_);
-        terms[H12_R_JOINT_DEV_ANKLE] = psum(fabsf(s.lg.q[4] - h12m::Q0[4]) + fabsf(s.lg.q[5] - h12m::Q0[5]));
-        terms[H12_R_DOF_POS_LIMITS_HIP] = psum(sh_);
-        terms[H12_R_CONTACT_FORCES] = psum(fmaxf(fmax_foot - P.cf_thr, 0.f));
-        terms[H12_R_LIN_VEL_Z_L2] = vb[2] * vb[2];
-      }
-    }
     float r = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -1819,6 +1829,49 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
     store_env<K>(P, W, e, leg, s);
     PH(7);
   }
+}
+
+// Term-evaluation hook (h12env_eval_terms, parity tests only): the reward terms, terminations and CaT constraint
+// values of step_kernel's code on a state written into the workspace (post-physics, pre-reset; EPLEN already
+// counted) plus injected per-step quantities: applied torques, joint accelerations, and the per-body maxima over
+// the contact history (left / right foot, left / right knee, torso).
+struct TermArgs {
+  const float* tau;   // (n, 12) real joint frame
+  const float* jacc;  // (n, 12)
+  const float* fmax;  // (n, 5)
+  float* terms;       // [H12_NREW][n]
+  uint8_t* term;      // (n,)
+  uint8_t* trunc;     // (n,)
+};
+template <int K>
+__global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, TermArgs T) {
+  const int leg = threadIdx.x & 1;
+  const float sg = leg ? -1.f : 1.f;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);
+  if (e >= W.n) return;
+  EnvSt s;
+  load_phys<K>(P, W, e, leg, s);
+  load_mdp<K>(P, W, e, leg, s);
+  float tau[NL], jacc[NL];
+  for (int k = 0; k < NL; ++k) {
+    tau[k] = jsign(k, sg) * T.tau[(size_t)e * NJ + NL * leg + k];
+    jacc[k] = jsign(k, sg) * T.jacc[(size_t)e * NJ + NL * leg + k];
+  }
+  const float fmax_foot = T.fmax[5 * (size_t)e + leg], fmax_knee = T.fmax[5 * (size_t)e + 2 + leg];
+  const float fmax_torso = T.fmax[5 * (size_t)e + 4];
+  int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
+  const int term = ill | pair_swap_i(ill);
+  float R[3][3];
+  quat_R(s.b.quat, R);
+  float terms[H12_NREW];
+  for (int t = 0; t < H12_NREW; ++t) terms[t] = 0.f;
+  mdp_terms<K>(P, s, leg, R, tau, jacc, fmax_foot, term, terms);
+  if (leg == 0) {
+    for (int t = 0; t < H12_NREW; ++t) T.terms[(size_t)t * W.n + e] = terms[t];
+    T.term[e] = (uint8_t)term;
+    T.trunc[e] = (uint8_t)(s.eplen >= P.max_len);
+  }
+  if (Feat<K>::ext && P.cat) cat_constraints(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
 }
 
 // CaT, after step_kernel: per-column maxima over the envs (CaT.add: constraint.max(dim=0)).  Grid
@@ -2629,6 +2682,21 @@ int h12env_step_physics(h12env* hh, const float* q_ref, int n_substeps, void* st
   A.q_ref = q_ref;
   A.n_substeps = n_substeps;
   LAUNCH_K(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_eval_terms(h12env* hh, const float* tau, const float* jacc, const float* fmax, float* terms,
+                      uint8_t* terminated, uint8_t* truncated, float* cstr, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!tau || !jacc || !fmax || !terms || !terminated || !truncated)
+    return set_err(H12_E_ARG, "tau, jacc, fmax, terms, terminated, truncated are required");
+  if (h->P.cat && !cstr) return set_err(H12_E_ARG, "cstr is required on a CaT env");
+  KParams P = h->P;
+  if (P.cat) P.cscr = cstr;  // the constraint rows go to the caller's buffer, not the step's scratch
+  TermArgs T = {tau, jacc, fmax, terms, terminated, truncated};
+  LAUNCH_K(terms_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, P, h->W, T);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -252,6 +252,8 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_step_physics.restype = C.c_int
     lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
     lib.h12env_field_ptr.restype = vp
+    lib.h12env_eval_terms.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.h12env_eval_terms.restype = C.c_int
     lib.h12env_num_envs.argtypes = [vp]
     lib.h12env_num_envs.restype = C.c_int
     lib.h12env_obs_dim.argtypes = [vp]
@@ -295,5 +297,5 @@ EXPORTED_SYMBOLS = [
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
-    "h12env_set_reward_weights", "h12env_set_constraint_max_p",
+    "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms",
 ]

@@ -512,6 +512,24 @@ class H12VelocityEnv:
         check(self._lib, self._lib.h12env_step_physics(self._h, C.c_void_p(q.data_ptr()), int(n_substeps),
                                                        self._stream()), "h12env_step_physics")
 
+    def eval_terms(self, tau: torch.Tensor, jacc: torch.Tensor, fmax: torch.Tensor):
+        """Parity hook (h12env_eval_terms): step()'s reward-term / termination / CaT-constraint code on the
+        workspace state as it stands, with injected applied torques (N, 12), joint accelerations (N, 12) and
+        per-body contact-history maxima (N, 5: feet L/R, knees L/R, torso).  Returns (terms (NREW, N),
+        terminated (N,) bool, truncated (N,) bool, constraint rows (NCSTR_COLS + 2, N) or None)."""
+        n = self.num_envs
+        f = lambda x, k: x.to(device=self.device, dtype=torch.float32).contiguous().reshape(n, k)  # noqa: E731
+        tau, jacc, fmax = f(tau, NJ), f(jacc, NJ), f(fmax, 5)
+        terms = torch.zeros(NREW, n, device=self.device)
+        term = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        trunc = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        cstr = torch.zeros(_abi.NCSTR_COLS + 2, n, device=self.device) if self._cat else None
+        check(self._lib, self._lib.h12env_eval_terms(
+            self._h, C.c_void_p(tau.data_ptr()), C.c_void_p(jacc.data_ptr()), C.c_void_p(fmax.data_ptr()),
+            C.c_void_p(terms.data_ptr()), C.c_void_p(term.data_ptr()), C.c_void_p(trunc.data_ptr()),
+            None if cstr is None else C.c_void_p(cstr.data_ptr()), self._stream()), "h12env_eval_terms")
+        return terms, term.bool(), trunc.bool(), cstr
+
     def observe(self, fill_mask: torch.Tensor | None = None):
         """ObservationManager.compute(): append a frame of the current state to the history."""
         prev = self._obs[self._k]

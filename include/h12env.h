@@ -317,6 +317,15 @@ int h12env_set_terrain(h12env* h, const float* heights, int nx, int ny, float hs
 /* Parity hook: n_substeps physics steps with a held joint target q_ref (N x 12) using the
  * configured mode (PD, limits, contact), no MDP.  Mirrors H12Mujoco.step. */
 int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* stream);
+/* Parity hook: the MDP term code of h12env_step (unweighted reward terms [H12_NREW][N], terminated, truncated
+ * and, on a CaT env, the constraint rows [H12_NCSTR_COLS + 2][N] into cstr) evaluated on the workspace state as
+ * it stands (post-physics, pre-reset; EPLEN already counted) with injected tau (N x 12, applied torque), jacc
+ * (N x 12, joint acceleration) and fmax (N x 5: max over the contact history of |F| on the left / right foot,
+ * left / right knee, torso).  Writes foot_clearance's swing height like a step.  Replaces nothing in the
+ * reference: it exposes RewardManager / TerminationManager / ConstraintManager term functions
+ * (velocity/mdp/rewards.py, utils/cat/constraints.py) for the reference-fixture tests. */
+int h12env_eval_terms(h12env* h, const float* tau, const float* jacc, const float* fmax, float* terms,
+                      uint8_t* terminated, uint8_t* truncated, float* cstr, void* stream);
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);

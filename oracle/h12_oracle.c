@@ -854,6 +854,29 @@ static void cmd_resample(const h12env_config* c, orc_env* e, int64_t g, uint32_t
   e->is_standing = (float)u01(r1[1]) <= c->rel_standing_envs;
   e->cmd_time = uab(r1[2], c->cmd_resample_time, c->cmd_resample_time_max);
 }
+/* UniformVelocityCommand._update_command given its decisions (utils/mdp/commands.py:83-138, the heading part
+ * :89-101 being the twin of the Flat task's IsaacLab command): heading envs get
+ * cmd_z = clip(stiffness * wrap_to_pi(heading - heading_w), ang_vel_z range); then, for the deadzone subclass,
+ * deactivate -> cmd_xy = 0, flip -> cmd_z *= -1; the plain command zeroes standing envs.  Returns 1 when the
+ * deadzone subclass asks for a resample of this env (activate). */
+int orc_cmd_update_decided(const h12env_config* c, double cmd[3], double heading_target, const double quat[4],
+                           int is_heading, int is_standing, int deactivate, int activate, int flip) {
+  if (is_heading) {
+    orc_phys p;
+    memcpy(p.quat, quat, sizeof p.quat);
+    double err = wrap_to_pi(heading_target - heading_w(&p));
+    double w = c->heading_stiffness * err;
+    cmd[2] = w < c->cmd_ang_z[0] ? c->cmd_ang_z[0] : (w > c->cmd_ang_z[1] ? c->cmd_ang_z[1] : w);
+  }
+  if (c->cmd_deadzone) {
+    if (deactivate) cmd[0] = cmd[1] = 0;
+    if (flip) cmd[2] = -cmd[2];
+    return activate;
+  }
+  if (is_standing) cmd[0] = cmd[1] = cmd[2] = 0;
+  return 0;
+}
+
 /* UniformVelocityCommand._update_command; with cmd_deadzone the Rsl/CaT subclass
  * (utils/mdp/commands.py:41-96): the reference picks exactly (target - count) of the active envs
  * (or (count - target) of the deadzone ones) by randperm; here each env draws the per-env marginal
@@ -861,27 +884,23 @@ static void cmd_resample(const h12env_config* c, orc_env* e, int64_t g, uint32_t
  * with the count of the previous step (dz_prev; exact for the shipped velocity_deadzone = 0, where the
  * count is always 0).  Then cmd_z *= -1 with probability ang_flip_prob.  No standing-env zeroing. */
 static void cmd_update(const h12env_config* c, orc_env* e, int64_t g, uint32_t lo, uint32_t hi, int dz_prev, int n) {
-  if (e->is_heading) {
-    double err = wrap_to_pi(e->heading - heading_w(&e->p));
-    double w = c->heading_stiffness * err;
-    e->cmd[2] = w < c->cmd_ang_z[0] ? c->cmd_ang_z[0] : (w > c->cmd_ang_z[1] ? c->cmd_ang_z[1] : w);
-  }
+  int deact = 0, act = 0, flip = 0;
   if (c->cmd_deadzone) {
     uint32_t r[4];
     rng_block(c->seed, g, lo, hi, ST_CMD, 2, r);
     int target = n / 2;
     double v = (double)c->velocity_deadzone;
+    /* membership uses cmd_xy, which the heading law (run first in the reference) does not change */
     int in_dz = (float)e->cmd[0] * (float)e->cmd[0] + (float)e->cmd[1] * (float)e->cmd[1] < (float)(v * v);
     uint64_t u24 = r[0] >> 8;
-    if (dz_prev < target) {
-      if (!in_dz && u24 * (uint64_t)(n - dz_prev) < ((uint64_t)(target - dz_prev) << 24)) e->cmd[0] = e->cmd[1] = 0;
-    } else if (dz_prev > target) {
-      if (in_dz && u24 * (uint64_t)dz_prev < ((uint64_t)(dz_prev - target) << 24)) cmd_resample(c, e, g, lo, hi, 3);
-    }
-    if (u01(r[1]) < (double)c->ang_flip_prob) e->cmd[2] = -e->cmd[2];
-    return;
+    if (dz_prev < target) deact = !in_dz && u24 * (uint64_t)(n - dz_prev) < ((uint64_t)(target - dz_prev) << 24);
+    else if (dz_prev > target) act = in_dz && u24 * (uint64_t)dz_prev < ((uint64_t)(dz_prev - target) << 24);
+    flip = u01(r[1]) < (double)c->ang_flip_prob;
   }
-  if (e->is_standing) e->cmd[0] = e->cmd[1] = e->cmd[2] = 0;
+  if (orc_cmd_update_decided(c, e->cmd, e->heading, e->p.quat, e->is_heading, e->is_standing, deact, act, 0)) {
+    cmd_resample(c, e, g, lo, hi, 3);
+  }
+  if (flip) e->cmd[2] = -e->cmd[2];
 }
 
 /* push_by_setting_velocity interval event (EventManager.apply(mode="interval"), rsl_env_cfg.py:262-273) */
@@ -897,6 +916,18 @@ static void push_event(const h12env_config* c, orc_env* e, int64_t g, uint32_t l
   }
 }
 
+/* terrain_levels_vel (velocity/mdp/curriculums.py:27-58): move up when the distance walked from the env origin
+ * exceeds half the sub-terrain size, down when it is below half the commanded distance of an episode (and
+ * not up) */
+void orc_terrain_move(const h12env_config* c, const double pos[3], const double origin[3], const double cmd[3], int* up,
+                      int* down) {
+  double dx = pos[0] - origin[0], dy = pos[1] - origin[1];
+  double dist = sqrt(dx * dx + dy * dy);
+  double ep_s = c->max_episode_length * c->physics_dt * c->decimation;
+  *up = dist > 0.5 * c->terrain_size;
+  *down = !*up && dist < sqrt(cmd[0] * cmd[0] + cmd[1] * cmd[1]) * ep_s * 0.5;
+}
+
 /* _reset_idx: scene reset (delay lags, sensor), reset events, manager resets (cat_env.py:195-248) */
 static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env* e, int64_t g, uint32_t lo,
                           uint32_t hi) {
@@ -906,11 +937,8 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   if (c->terrain_curriculum && g_terrain.origins) {
     /* terrain_levels_vel (velocity/mdp/curriculums.py:21-52) on the pre-reset state, then
      * TerrainImporter.update_env_origins (solvers of the last level go to a random one) */
-    double dx = e->p.pos[0] - e->origin[0], dy = e->p.pos[1] - e->origin[1];
-    double dist = sqrt(dx * dx + dy * dy);
-    double ep_s = c->max_episode_length * c->physics_dt * c->decimation;
-    int up = dist > 0.5 * c->terrain_size;
-    int down = !up && dist < sqrt(e->cmd[0] * e->cmd[0] + e->cmd[1] * e->cmd[1]) * ep_s * 0.5;
+    int up, down;
+    orc_terrain_move(c, e->p.pos, e->origin, e->cmd, &up, &down);
     int lvl = (e->tcell & 0xFFFF) + up - down, typ = e->tcell >> 16;
     if (lvl >= g_terrain.rows) {
       uint32_t r2[4];
@@ -964,6 +992,28 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   cmd_resample(c, e, g, lo, hi, 0);
 }
 
+/* ObservationManager.compute_group per term (observation_manager.py:318-337): noise (Unoise: value + n_min +
+ * (n_max - n_min) u, u the term's uniform draw), then scale.  raw: the 45 noise-free frame components (base_ang_vel,
+ * projected_gravity, velocity_commands, joint_pos_rel, joint_vel_rel, last_action); u: the 30 draws of the noisy
+ * components in order (commands and actions carry no noise). */
+void orc_obs_frame_from(const h12env_config* c, const double raw[H12_OBS_FRAME], const double u[30],
+                        double fr[H12_OBS_FRAME]) {
+  for (int k = 0; k < H12_OBS_FRAME; ++k) fr[k] = raw[k];
+  if (c->enable_corruption) {
+    const int idx[30] = {0, 1, 2, 3, 4, 5, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20,
+                         21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32};
+    for (int t = 0; t < 30; ++t) {
+      double nmax = t < 3 ? c->noise_ang_vel : t < 6 ? c->noise_gravity : t < 18 ? c->noise_joint_pos : c->noise_joint_vel;
+      fr[idx[t]] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)u[t]);
+    }
+  }
+  /* ObsTerm scale, after noise (observation_manager.py:327-336) */
+  for (int k2 = 0; k2 < H12_OBS_FRAME; ++k2) {
+    int t = k2 < 9 ? k2 / 3 : 3 + (k2 - 9) / NJ;
+    fr[k2] *= (double)c->obs_scale[t];
+  }
+}
+
 /* observation frame (ObservationManager.compute_group, observation_manager.py:318-351) */
 static void obs_frame(const h12env_model* m, const h12env_config* c, const orc_env* e, int64_t g, uint32_t lo,
                       uint32_t hi, double fr[H12_OBS_FRAME]) {
@@ -977,26 +1027,15 @@ static void obs_frame(const h12env_model* m, const h12env_config* c, const orc_e
     rng_block(c->seed, g, lo, hi, ST_OBS, b, r);
     for (int a = 0; a < 4; ++a) noise[4 * b + a] = u01(r[a]);
   }
+  double raw[H12_OBS_FRAME];
   int k = 0;
-  for (int a = 0; a < 3; ++a) fr[k++] = e->p.wang[a];
-  for (int a = 0; a < 3; ++a) fr[k++] = gb[a];
-  for (int a = 0; a < 3; ++a) fr[k++] = e->cmd[a];
-  for (int j = 0; j < NJ; ++j) fr[k++] = e->p.q[j] - m->q_default[j];
-  for (int j = 0; j < NJ; ++j) fr[k++] = e->p.qd[j];
-  for (int j = 0; j < NJ; ++j) fr[k++] = e->act[j];
-  if (c->enable_corruption) {
-    const int idx[30] = {0, 1, 2, 3, 4, 5, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20,
-                         21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32};
-    for (int t = 0; t < 30; ++t) {
-      double nmax = t < 3 ? c->noise_ang_vel : t < 6 ? c->noise_gravity : t < 18 ? c->noise_joint_pos : c->noise_joint_vel;
-      fr[idx[t]] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)noise[t]);
-    }
-  }
-  /* ObsTerm scale, after noise (observation_manager.py:327-336) */
-  for (int k2 = 0; k2 < H12_OBS_FRAME; ++k2) {
-    int t = k2 < 9 ? k2 / 3 : 3 + (k2 - 9) / NJ;
-    fr[k2] *= (double)c->obs_scale[t];
-  }
+  for (int a = 0; a < 3; ++a) raw[k++] = e->p.wang[a];
+  for (int a = 0; a < 3; ++a) raw[k++] = gb[a];
+  for (int a = 0; a < 3; ++a) raw[k++] = e->cmd[a];
+  for (int j = 0; j < NJ; ++j) raw[k++] = e->p.q[j] - m->q_default[j];
+  for (int j = 0; j < NJ; ++j) raw[k++] = e->p.qd[j];
+  for (int j = 0; j < NJ; ++j) raw[k++] = e->act[j];
+  orc_obs_frame_from(c, raw, noise, fr);
 }
 static const int TERM_DIM[6] = {3, 3, 3, NJ, NJ, NJ};
 /* CircularBuffer append + buffer() flattening of a term-major row, nh frames per term (oldest first) */
@@ -1028,6 +1067,24 @@ static void base_com_vel(const h12env_model* m, const orc_phys* p, const m3 R, d
   for (int a = 0; a < 3; ++a) vcom[a] = p->vlin[a] + wxc[a];
 }
 
+/* ObservationManager.compute_group of the rough policy group (observation_manager.py:318-337): per noisy
+ * component t (all but velocity_commands and actions: 220) value + n_min + (n_max - n_min) u[t], then the
+ * height scan's clip (velocity_env_cfg.py:133-137); no scales, no history. */
+void orc_rough_row_from(const h12env_config* c, const double raw[H12_NOBS_ROUGH], const double u[H12_NOBS_ROUGH - 15],
+                        float* out) {
+  for (int kk = 0; kk < H12_NOBS_ROUGH; ++kk) {
+    double v = raw[kk];
+    int t = kk < 9 ? kk : ((kk >= 12 && kk < 36) ? kk - 3 : (kk >= H12_ROUGH_FRAME ? kk - 15 : -1));
+    if (t >= 0 && c->enable_corruption) {
+      double nmax = t < 3 ? c->noise_lin_vel : t < 6 ? c->noise_ang_vel : t < 9 ? c->noise_gravity
+                  : t < 21 ? c->noise_joint_pos : t < 33 ? c->noise_joint_vel : c->noise_height_scan;
+      v += (double)(float)(-nmax + 2.0 * nmax * (double)(float)u[t]);
+    }
+    if (kk >= H12_ROUGH_FRAME) v = v < -c->scan_clip ? -c->scan_clip : (v > c->scan_clip ? c->scan_clip : v);
+    out[kk] = (float)v;
+  }
+}
+
 /* Rough task observation row (velocity_env_cfg.py:118-137): base_lin_vel, base_ang_vel, projected_gravity,
  * velocity_commands, joint_pos_rel, joint_vel_rel, last_action, height_scan; noise then clip.  Height scan:
  * 17 x 11 rays at 0.1 m around the torso_link origin (= pelvis origin), yaw-aligned, x fastest;
@@ -1057,18 +1114,13 @@ static void obs_row_rough(const h12env_model* m, const h12env_config* c, const o
       double hz = orc_ground(c, e->p.pos[0] + cy * xl - sy * yl, e->p.pos[1] + sy * xl + cy * yl, &gx, &gy);
       v[k++] = e->p.pos[2] - hz - c->scan_offset;
     }
-  for (int kk = 0; kk < H12_NOBS_ROUGH; ++kk) {
-    int t = kk < 9 ? kk : ((kk >= 12 && kk < 36) ? kk - 3 : (kk >= H12_ROUGH_FRAME ? kk - 15 : -1));
-    if (t >= 0 && c->enable_corruption) {
-      uint32_t r[4];
-      rng_block(c->seed, g, lo, hi, ST_OBS, t >> 2, r);
-      double nmax = t < 3 ? c->noise_lin_vel : t < 6 ? c->noise_ang_vel : t < 9 ? c->noise_gravity
-                  : t < 21 ? c->noise_joint_pos : t < 33 ? c->noise_joint_vel : c->noise_height_scan;
-      v[kk] += (double)(float)(-nmax + 2.0 * nmax * (double)(float)u01(r[t & 3]));
-    }
-    if (kk >= H12_ROUGH_FRAME) v[kk] = v[kk] < -c->scan_clip ? -c->scan_clip : (v[kk] > c->scan_clip ? c->scan_clip : v[kk]);
-    out[kk] = (float)v[kk];
+  double u[H12_NOBS_ROUGH - 15];
+  for (int t = 0; t < H12_NOBS_ROUGH - 15; ++t) {
+    uint32_t r[4];
+    rng_block(c->seed, g, lo, hi, ST_OBS, t >> 2, r);
+    u[t] = u01(r[t & 3]);
   }
+  orc_rough_row_from(c, v, u, out);
 }
 
 /* DelayBuffer = CircularBuffer(max_delay + 1)[lag] (circular_buffer.py:139-170) with one push per
@@ -1083,6 +1135,9 @@ int orc_delay_source(int lag, int since_reset, int substep, int decimation) {
 
 void orc_history_write(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill) {
   obs_write(frame, prev_row, out_row, fill, H12_NHIST);
+}
+void orc_history_write_n(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill, int nh) {
+  obs_write(frame, prev_row, out_row, fill, nh);
 }
 
 /* ObservationManager.compute() outside step(): one new frame per env, history shifted (or filled
@@ -1131,6 +1186,114 @@ int orc_env_reset(const h12env_model* m, const h12env_config* c, int n, int64_t 
 
 static double sq(double x) { return x * x; }
 
+/* The MDP terms of one env on its post-physics, pre-reset state (the code orc_env_step runs): the
+ * time_out / illegal_contact terminations (velocity_env_cfg.py:264-268; bodies rough_env_cfg.py:95-109,
+ * threshold 1 N on max_h |F| over net_forces_w_history) and the 20 reward terms of the kernel table (unweighted;
+ * the Flat 12 of SURVEY.md a8.1-a8.12 + the Rsl extras).  Reference code among them:
+ * feet_air_time_positive_biped (velocity/mdp/rewards.py:38-62), action_rate_l2 (utils/mdp/rewards.py:23-30). */
+int orc_mdp_terms(const h12env_model* m, const h12env_config* c, const orc_term_in* in, double terms[H12_NREW],
+                  int* terminated, int* time_out) {
+  int tout = in->eplen >= c->max_episode_length;
+  int term = 0;
+  if (c->illegal_contact_knees && (in->fmax_knee[0] > c->contact_threshold || in->fmax_knee[1] > c->contact_threshold)) term = 1;
+  if (c->illegal_contact_torso && in->fmax_torso > c->contact_threshold) term = 1;
+  /* rewards (pre-reset state) */
+  m3 R;
+  quat_to_R(in->p.quat, R);
+  double wb[3] = {in->p.wang[0], in->p.wang[1], in->p.wang[2]}, ww[3];
+  m3v(R, wb, ww);
+  double gw[3] = {0, 0, -1}, gb[3];
+  m3tv(R, gw, gb);
+  double vcom[3];
+  base_com_vel(m, &in->p, R, vcom);
+  double yaw = atan2(R[1][0], R[0][0]);
+  double cy = cos(yaw), sy = sin(yaw);
+  double vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
+  double std2 = c->track_std * c->track_std;
+  terms[H12_R_TRACK_LIN_VEL_XY] = exp(-(sq(in->cmd[0] - vy0) + sq(in->cmd[1] - vy1)) / std2);
+  terms[H12_R_TRACK_ANG_VEL_Z] = exp(-sq(in->cmd[2] - ww[2]) / std2);
+  terms[H12_R_ANG_VEL_XY_L2] = sq(wb[0]) + sq(wb[1]);
+  double s_t = 0, s_a = 0, s_r = 0, s_lim = 0, s_dev = 0;
+  for (int j = 0; j < NJ; ++j) {
+    s_t += sq(in->tau[j]);
+    s_a += sq(in->jacc[j]);
+    s_r += sq(in->act[j] - in->act_prev[j]);
+  }
+  terms[H12_R_DOF_TORQUES_L2] = s_t;
+  terms[H12_R_DOF_ACC_L2] = s_a;
+  terms[H12_R_ACTION_RATE_L2] = s_r;
+  /* feet_air_time_positive_biped (mdp/rewards.py:38-62) */
+  {
+    int inc[2] = {in->con[0] > 0, in->con[1] > 0};
+    double mode_t[2] = {inc[0] ? in->con[0] : in->air[0], inc[1] ? in->con[1] : in->air[1]};
+    int single = (inc[0] + inc[1]) == 1;
+    double r = single ? (mode_t[0] < mode_t[1] ? mode_t[0] : mode_t[1]) : 0.0;
+    if (r > c->air_time_threshold) r = c->air_time_threshold;
+    double cn = sqrt(sq(in->cmd[0]) + sq(in->cmd[1]));
+    terms[H12_R_FEET_AIR_TIME] = cn > 0.1 ? r : 0.0;
+  }
+  terms[H12_R_FLAT_ORIENTATION_L2] = sq(gb[0]) + sq(gb[1]);
+  for (int f = 0; f < 2; ++f)
+    for (int k = 4; k < 6; ++k) { /* ankle pitch, ankle roll */
+      int j = 6 * f + k;
+      double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+      double lo_s = mid - half, hi_s = mid + half, q = in->p.q[j];
+      s_lim += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
+    }
+  terms[H12_R_DOF_POS_LIMITS] = s_lim;
+  terms[H12_R_TERMINATION] = term ? 1.0 : 0.0;
+  {
+    /* feet_slide: |v_xy| of the ankle-roll link COM where max_h |F| > 1 */
+    kin_t k;
+    kinematics(m, &in->p, &k);
+    double fs = 0;
+    for (int f = 0; f < 2; ++f) {
+      int b = 6 * f + 6;
+      if (!(in->fmax_foot[f] > 1.0)) continue;
+      double cl[3] = {m->link_com[b - 1][0], m->link_com[b - 1][1], m->link_com[b - 1][2]}, vl[3], vw[3];
+      cross3(k.v[b], cl, vl);
+      for (int a = 0; a < 3; ++a) vl[a] += k.v[b][3 + a];
+      m3v(k.R[b], vl, vw);
+      fs += sqrt(sq(vw[0]) + sq(vw[1]));
+    }
+    terms[H12_R_FEET_SLIDE] = fs;
+  }
+  for (int f = 0; f < 2; ++f) {
+    int j0 = 6 * f + 0, j2 = 6 * f + 2; /* hip yaw, hip roll */
+    s_dev += fabs(in->p.q[j0] - m->q_default[j0]) + fabs(in->p.q[j2] - m->q_default[j2]);
+  }
+  terms[H12_R_JOINT_DEV_HIP] = s_dev;
+  /* Rsl table (rsl_env_cfg.py:279-407) */
+  {
+    double vb[3];
+    m3tv(R, vcom, vb); /* root_lin_vel_b */
+    terms[H12_R_TRACK_LIN_VEL_XY_BASE] = exp(-(sq(in->cmd[0] - vb[0]) + sq(in->cmd[1] - vb[1])) / std2);
+    terms[H12_R_TRACK_ANG_VEL_Z_BASE] = exp(-sq(in->cmd[2] - wb[2]) / std2);
+    terms[H12_R_BASE_HEIGHT_L2] = sq(in->p.pos[2] - c->base_height_target);
+    double s_v = 0, s_da = 0, s_lh = 0, s_cf = 0;
+    for (int j = 0; j < NJ; ++j) s_v += sq(in->p.qd[j]);
+    for (int f = 0; f < 2; ++f) {
+      for (int k = 4; k < 6; ++k) s_da += fabs(in->p.q[6 * f + k] - m->q_default[6 * f + k]);
+      for (int k = 0; k < 3; k += 2) { /* hip yaw, hip roll soft limits */
+        int j = 6 * f + k;
+        double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
+        double lo_s = mid - half, hi_s = mid + half, q = in->p.q[j];
+        s_lh += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
+      }
+      double viol = in->fmax_foot[f] - c->contact_force_threshold;
+      s_cf += viol > 0 ? viol : 0.0;
+    }
+    terms[H12_R_JOINT_VEL_L2] = s_v;
+    terms[H12_R_JOINT_DEV_ANKLE] = s_da;
+    terms[H12_R_DOF_POS_LIMITS_HIP] = s_lh;
+    terms[H12_R_CONTACT_FORCES] = s_cf;
+    terms[H12_R_LIN_VEL_Z_L2] = sq(vb[2]);
+  }
+  if (terminated) *terminated = term;
+  if (time_out) *time_out = tout;
+  return 0;
+}
+
 /* ---------------------------------------------------------------- CaT (T/utils/cat, cat_env_cfg.py) */
 enum { CAT_ROW_NOMOVE = H12_NCSTR_COLS, CAT_ROW_EPLEN = H12_NCSTR_COLS + 1, CAT_ROWS = H12_NCSTR_COLS + 2 };
 static const int C_COL0[H12_NCSTR + 1] = {0, 1, 13, 25, 37, 39, 51, 52, 53, 54, 56};
@@ -1147,52 +1310,65 @@ int orc_cat_last_constraints(double* out, int n) {
 }
 void orc_cat_running_max(double out[H12_NCSTR_COLS]) { memcpy(out, g_crun, sizeof g_crun); }
 
-/* constraints.py:18-308 for one env on its pre-reset state; cs is [CAT_ROWS][n] */
-static void cat_constraints(const h12env_model* m, const h12env_config* c, const orc_env* e, const double tau[NJ],
-                            const double fmax_foot[2], int term, const double gb[3], int n, int i, float* F,
-                            double step_dt, double* cs) {
-#define CS(col) cs[(size_t)(col) * n + i]
+/* constraints.py:24-308 for one env on its pre-reset state (the ten terms of cat_env_cfg.py:336-425):
+ * joint_position_limits :24-33, joint_velocity_limits :36-44, joint_torque_limits :47-55, contact :86-99
+ * (= the illegal-contact termination: same bodies, same 1 N test), base_orientation :102-108, no_move :196-228
+ * (raw |qd| - limit of THIS env; the repeat-remap over still envs is orc_cat_probs'), base_height :251-266,
+ * foot_contact :171-193, foot_clearance :269-308 (swing_h = swing_max_height in/out), foot_contact_force
+ * :161-168; plus the still flag of no_move (all |cmd| < deadzone) and the episode length.
+ * out[col * stride], col in 0 .. H12_NCSTR_COLS + 1. */
+int orc_cat_row(const h12env_model* m, const h12env_config* c, const orc_term_in* in, int terminated,
+                double swing_h[2], double* out, size_t stride) {
+#define CS(col) out[(size_t)(col) * stride]
+  const double step_dt = c->physics_dt * c->decimation;
   for (int j = 0; j < NJ; ++j) {
     double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
-    double q = e->p.q[j], qd = fabs(e->p.qd[j]);
+    double q = in->p.q[j], qd = fabs(in->p.qd[j]);
     double lo_v = (mid - half) - q, hi_v = q - (mid + half);
     CS(C_COL0[H12_C_JOINT_POS_LIMITS] + j) = lo_v > hi_v ? lo_v : hi_v;
     CS(C_COL0[H12_C_JOINT_VEL_LIMITS] + j) = qd - c->cstr_joint_vel_limit[j];
-    CS(C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j) = fabs(tau[j]) - c->cstr_joint_effort_limit[j];
+    CS(C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j) = fabs(in->tau[j]) - c->cstr_joint_effort_limit[j];
     CS(C_COL0[H12_C_NO_MOVE] + j) = qd - c->cstr_nomove_vel;
   }
   kin_t k;
-  kinematics(m, &e->p, &k);
-  int active = fabs(e->cmd[0]) > c->cstr_clearance_deadzone || fabs(e->cmd[1]) > c->cstr_clearance_deadzone ||
-               fabs(e->cmd[2]) > c->cstr_clearance_deadzone;
+  kinematics(m, &in->p, &k);
+  m3 R;
+  quat_to_R(in->p.quat, R);
+  double gw[3] = {0, 0, -1}, gb[3];
+  m3tv(R, gw, gb);
+  int active = fabs(in->cmd[0]) > c->cstr_clearance_deadzone || fabs(in->cmd[1]) > c->cstr_clearance_deadzone ||
+               fabs(in->cmd[2]) > c->cstr_clearance_deadzone;
   int nfeet = 0;
   for (int f = 0; f < 2; ++f) {
-    CS(C_COL0[H12_C_FOOT_CONTACT_FORCE] + f) = fmax_foot[f] - c->cstr_foot_force_limit;
-    nfeet += fmax_foot[f] > 1.0;
+    CS(C_COL0[H12_C_FOOT_CONTACT_FORCE] + f) = in->fmax_foot[f] - c->cstr_foot_force_limit;
+    nfeet += in->fmax_foot[f] > 1.0;
     /* foot_clearance: touchdown = compute_first_contact(step_dt); swing max height of the ankle-roll link */
-    int touchdown = e->con[f] > 0 && e->con[f] < step_dt + 1e-8;
-    float* sw = &F[(size_t)(H12_F_SWING_H + f) * n + i];
-    double sh = *sw, foot_z = k.p[6 * f + 6][2];
+    int touchdown = in->con[f] > 0 && in->con[f] < step_dt + 1e-8;
+    double sh = swing_h[f], foot_z = k.p[6 * f + 6][2];
     CS(C_COL0[H12_C_FOOT_CLEARANCE] + f) = (touchdown && active) ? c->cstr_clearance_min - sh : 0.0;
-    *sw = (float)(touchdown ? 0.0 : (foot_z > sh ? foot_z : sh));
+    swing_h[f] = touchdown ? 0.0 : (foot_z > sh ? foot_z : sh);
   }
-  CS(C_COL0[H12_C_CONTACT]) = term ? 1.0 : 0.0;
+  CS(C_COL0[H12_C_CONTACT]) = terminated ? 1.0 : 0.0;
   CS(C_COL0[H12_C_BASE_ORIENTATION]) = sqrt(sq(gb[0]) + sq(gb[1])) - c->cstr_orient_limit;
-  double z = e->p.pos[2];
+  double z = in->p.pos[2];
   CS(C_COL0[H12_C_BASE_HEIGHT]) = (z < c->cstr_height - c->cstr_height_std || z > c->cstr_height + c->cstr_height_std) ? 1.0 : 0.0;
   CS(C_COL0[H12_C_FOOT_CONTACT]) = (nfeet < 1 || nfeet > 2) ? 1.0 : 0.0;
   double dz = c->cstr_nomove_deadzone;
-  CS(CAT_ROW_NOMOVE) = (fabs(e->cmd[0]) < dz && fabs(e->cmd[1]) < dz && fabs(e->cmd[2]) < dz) ? 1.0 : 0.0;
-  CS(CAT_ROW_EPLEN) = e->eplen;
+  CS(CAT_ROW_NOMOVE) = (fabs(in->cmd[0]) < dz && fabs(in->cmd[1]) < dz && fabs(in->cmd[2]) < dz) ? 1.0 : 0.0;
+  CS(CAT_ROW_EPLEN) = in->eplen;
 #undef CS
+  return 0;
 }
 
-/* ConstraintManager.compute + CaTEnv.step's use of it (constraint_manager.py:42-78, 222-237; cat_env.py:148-153,
- * 164-166) over the whole batch: column maxima (no_move: env i takes the row of the (i mod m)-th still env),
- * running maxima, probabilities, reward scaling, dones, episode statistics. */
-static void cat_pass(const h12env_config* c, int n, float* F, const double* cs, float* rew, const uint8_t* terminated,
-                     const uint8_t* truncated, float* cstr_prob, float* log_acc) {
+/* CaT.add / get_probs over the batch (constraint_manager.py:40-82) with no_move's row remap
+ * (constraints.py:214-228: env i takes the row of the (i mod m)-th still env, zeros when none):
+ * column maxima clamped at 1e-6, running maxima (Polyak tau; the first call sets them), per-term
+ * probabilities min_p + clamp(c / running_max, 0, 1) (max_p - min_p) where c > 0, their max over terms.
+ * cs is [CAT_ROWS][n]; pterm [H12_NCSTR][n] and ceff [H12_NCSTR_COLS][n] (the values CaT.add saw) may be NULL. */
+int orc_cat_probs(const h12env_config* c, int n, const double* cs, double run_max[H12_NCSTR_COLS], int* run_init,
+                  double* pmax, double* pterm, double* ceff) {
   int* list = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  if (!list) return -1;
   int mcount = 0;
   for (int i = 0; i < n; ++i)
     if (cs[(size_t)CAT_ROW_NOMOVE * n + i] != 0) list[mcount++] = i;
@@ -1206,48 +1382,81 @@ static void cat_pass(const h12env_config* c, int n, float* F, const double* cs, 
       for (int i = 0; i < n; ++i) { double v = cs[(size_t)col * n + i]; if (v > cm) cm = v; }
     }
     if (cm < 1e-6) cm = 1e-6;
-    g_crun[col] = g_crun_init ? c->cat_tau * g_crun[col] + (1.0 - (double)c->cat_tau) * cm : cm;
+    run_max[col] = *run_init ? c->cat_tau * run_max[col] + (1.0 - (double)c->cat_tau) * cm : cm;
   }
-  g_crun_init = 1;
+  *run_init = 1;
   for (int i = 0; i < n; ++i) {
     int src = mcount > 0 ? list[i % mcount] : -1;
-    double pt[H12_NCSTR], pmax = 0;
+    double pm = 0;
     for (int t = 0; t < H12_NCSTR; ++t) {
-      pt[t] = 0;
-      if (!((c->cstr_mask >> t) & 1u)) continue;
+      double pt = 0;
       for (int col = C_COL0[t]; col < C_COL0[t + 1]; ++col) {
         double v = t == H12_C_NO_MOVE ? (src >= 0 ? cs[(size_t)col * n + src] : 0.0) : cs[(size_t)col * n + i];
+        if (ceff) ceff[(size_t)col * n + i] = v;
+        if (!((c->cstr_mask >> t) & 1u)) continue;
         double p = 0;
         if (v > 0) {
-          double r = v / g_crun[col];
+          double r = v / run_max[col];
           r = r < 0 ? 0 : (r > 1 ? 1 : r);
           p = c->cat_min_p + r * (c->cstr_max_p[t] - c->cat_min_p);
         }
-        if (p > pt[t]) pt[t] = p;
+        if (p > pt) pt = p;
       }
-      if (pt[t] > pmax) pmax = pt[t];
+      if (pterm) pterm[(size_t)t * n + i] = pt;
+      if (pt > pm) pm = pt;
     }
-    rew[i] = (float)(rew[i] * (1.0 - pmax));
-    int reset = terminated[i] || truncated[i];
-    if (cstr_prob) cstr_prob[i] = reset ? 1.0f : (float)pmax;
-    double len = cs[(size_t)CAT_ROW_EPLEN * n + i];
+    pmax[i] = pm;
+  }
+  free(list);
+  return 0;
+}
+
+/* ConstraintManager.compute + CaTEnv.step's use of it (constraint_manager.py:42-78, 222-237; cat_env.py:148-153,
+ * 164-166) over the whole batch: column maxima (no_move: env i takes the row of the (i mod m)-th still env),
+ * running maxima, probabilities, reward scaling, dones, episode statistics. */
+/* ConstraintManager statistics (constraint_manager.py:221-227) and their reset (:195-210): per term the episode
+ * sums of [p_term > 0] and of p_term; at a reset the env adds sum / episode_length to the log accumulator
+ * (log_acc[H12_NREW + 4 + t]: violations, [H12_NREW + 4 + H12_NCSTR + t]: probabilities; the host divides by
+ * the number of reset envs, x 100 for violations) and its sums restart.  sum_v / sum_p are [H12_NCSTR][n]. */
+void orc_cat_stats(const h12env_config* c, int n, const double* pterm, const double* eplen, const uint8_t* reset,
+                   float* sum_v, float* sum_p, float* log_acc) {
+  for (int i = 0; i < n; ++i)
     for (int t = 0; t < H12_NCSTR; ++t) {
       if (!((c->cstr_mask >> t) & 1u)) continue;
-      float* fs = &F[(size_t)(H12_F_CSTR_SUM + t) * n + i];
-      float* fp = &F[(size_t)(H12_F_CSTR_P + t) * n + i];
-      double vs = *fs + (pt[t] > 0 ? 1.0 : 0.0), vp = *fp + pt[t];
-      if (reset) {
+      double pt = pterm[(size_t)t * n + i];
+      float* fs = &sum_v[(size_t)t * n + i];
+      float* fp = &sum_p[(size_t)t * n + i];
+      double vs = *fs + (pt > 0 ? 1.0 : 0.0), vp = *fp + pt;
+      if (reset[i]) {
         if (log_acc) {
-          log_acc[H12_NREW + 4 + t] += (float)(vs / len);
-          log_acc[H12_NREW + 4 + H12_NCSTR + t] += (float)(vp / len);
+          log_acc[H12_NREW + 4 + t] += (float)(vs / eplen[i]);
+          log_acc[H12_NREW + 4 + H12_NCSTR + t] += (float)(vp / eplen[i]);
         }
         vs = vp = 0;
       }
       *fs = (float)vs;
       *fp = (float)vp;
     }
+}
+
+static void cat_pass(const h12env_config* c, int n, float* F, const double* cs, float* rew, const uint8_t* terminated,
+                     const uint8_t* truncated, float* cstr_prob, float* log_acc) {
+  const size_t nn = (size_t)(n > 0 ? n : 1);
+  double* pmax = (double*)malloc(sizeof(double) * nn);
+  double* pterm = (double*)malloc(sizeof(double) * (size_t)H12_NCSTR * nn);
+  uint8_t* reset = (uint8_t*)malloc(nn);
+  orc_cat_probs(c, n, cs, g_crun, &g_crun_init, pmax, pterm, NULL);
+  for (int i = 0; i < n; ++i) {
+    rew[i] = (float)(rew[i] * (1.0 - pmax[i]));
+    reset[i] = terminated[i] || truncated[i];
+    if (cstr_prob) cstr_prob[i] = reset[i] ? 1.0f : (float)pmax[i];
   }
-  free(list);
+  /* the workspace keeps the sums field-major: [H12_NCSTR][n] from H12_F_CSTR_SUM / H12_F_CSTR_P */
+  orc_cat_stats(c, n, pterm, cs + (size_t)CAT_ROW_EPLEN * n, reset, F + (size_t)H12_F_CSTR_SUM * n,
+                F + (size_t)H12_F_CSTR_P * n, log_acc);
+  free(pmax);
+  free(pterm);
+  free(reset);
 }
 
 int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t env_offset, float* F, int32_t* I,
@@ -1330,104 +1539,22 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       }
     }
     e.eplen += 1;
-    /* terminations: time_out, illegal_contact (velocity_env_cfg.py:264-268) */
-    int tout = e.eplen >= c->max_episode_length;
-    int term = 0;
-    if (c->illegal_contact_knees && (fmax_knee[0] > c->contact_threshold || fmax_knee[1] > c->contact_threshold)) term = 1;
-    if (c->illegal_contact_torso && fmax_torso > c->contact_threshold) term = 1;
-    /* rewards (pre-reset state) */
-    m3 R;
-    quat_to_R(e.p.quat, R);
-    double wb[3] = {e.p.wang[0], e.p.wang[1], e.p.wang[2]}, ww[3];
-    m3v(R, wb, ww);
-    double gw[3] = {0, 0, -1}, gb[3];
-    m3tv(R, gw, gb);
-    double vcom[3];
-    base_com_vel(m, &e.p, R, vcom);
-    double yaw = atan2(R[1][0], R[0][0]);
-    double cy = cos(yaw), sy = sin(yaw);
-    double vy0 = cy * vcom[0] + sy * vcom[1], vy1 = -sy * vcom[0] + cy * vcom[1];
+    orc_term_in ti;
+    ti.p = e.p;
+    memcpy(ti.act, e.act, sizeof ti.act);
+    memcpy(ti.act_prev, e.act_prev, sizeof ti.act_prev);
+    memcpy(ti.cmd, e.cmd, sizeof ti.cmd);
+    memcpy(ti.air, e.air, sizeof ti.air);
+    memcpy(ti.con, e.con, sizeof ti.con);
+    memcpy(ti.tau, tau_applied, sizeof ti.tau);
+    memcpy(ti.jacc, jacc, sizeof ti.jacc);
+    memcpy(ti.fmax_foot, fmax_foot, sizeof ti.fmax_foot);
+    memcpy(ti.fmax_knee, fmax_knee, sizeof ti.fmax_knee);
+    ti.fmax_torso = fmax_torso;
+    ti.eplen = e.eplen;
     double terms[H12_NREW];
-    double std2 = c->track_std * c->track_std;
-    terms[H12_R_TRACK_LIN_VEL_XY] = exp(-(sq(e.cmd[0] - vy0) + sq(e.cmd[1] - vy1)) / std2);
-    terms[H12_R_TRACK_ANG_VEL_Z] = exp(-sq(e.cmd[2] - ww[2]) / std2);
-    terms[H12_R_ANG_VEL_XY_L2] = sq(wb[0]) + sq(wb[1]);
-    double s_t = 0, s_a = 0, s_r = 0, s_lim = 0, s_dev = 0;
-    for (int j = 0; j < NJ; ++j) {
-      s_t += sq(tau_applied[j]);
-      s_a += sq(jacc[j]);
-      s_r += sq(e.act[j] - e.act_prev[j]);
-    }
-    terms[H12_R_DOF_TORQUES_L2] = s_t;
-    terms[H12_R_DOF_ACC_L2] = s_a;
-    terms[H12_R_ACTION_RATE_L2] = s_r;
-    /* feet_air_time_positive_biped (mdp/rewards.py:38-62) */
-    {
-      int inc[2] = {e.con[0] > 0, e.con[1] > 0};
-      double mode_t[2] = {inc[0] ? e.con[0] : e.air[0], inc[1] ? e.con[1] : e.air[1]};
-      int single = (inc[0] + inc[1]) == 1;
-      double r = single ? (mode_t[0] < mode_t[1] ? mode_t[0] : mode_t[1]) : 0.0;
-      if (r > c->air_time_threshold) r = c->air_time_threshold;
-      double cn = sqrt(sq(e.cmd[0]) + sq(e.cmd[1]));
-      terms[H12_R_FEET_AIR_TIME] = cn > 0.1 ? r : 0.0;
-    }
-    terms[H12_R_FLAT_ORIENTATION_L2] = sq(gb[0]) + sq(gb[1]);
-    for (int f = 0; f < 2; ++f)
-      for (int k = 4; k < 6; ++k) { /* ankle pitch, ankle roll */
-        int j = 6 * f + k;
-        double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
-        double lo_s = mid - half, hi_s = mid + half, q = e.p.q[j];
-        s_lim += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
-      }
-    terms[H12_R_DOF_POS_LIMITS] = s_lim;
-    terms[H12_R_TERMINATION] = term ? 1.0 : 0.0;
-    {
-      /* feet_slide: |v_xy| of the ankle-roll link COM where max_h |F| > 1 */
-      kin_t k;
-      kinematics(m, &e.p, &k);
-      double fs = 0;
-      for (int f = 0; f < 2; ++f) {
-        int b = 6 * f + 6;
-        if (!(fmax_foot[f] > 1.0)) continue;
-        double cl[3] = {m->link_com[b - 1][0], m->link_com[b - 1][1], m->link_com[b - 1][2]}, vl[3], vw[3];
-        cross3(k.v[b], cl, vl);
-        for (int a = 0; a < 3; ++a) vl[a] += k.v[b][3 + a];
-        m3v(k.R[b], vl, vw);
-        fs += sqrt(sq(vw[0]) + sq(vw[1]));
-      }
-      terms[H12_R_FEET_SLIDE] = fs;
-    }
-    for (int f = 0; f < 2; ++f) {
-      int j0 = 6 * f + 0, j2 = 6 * f + 2; /* hip yaw, hip roll */
-      s_dev += fabs(e.p.q[j0] - m->q_default[j0]) + fabs(e.p.q[j2] - m->q_default[j2]);
-    }
-    terms[H12_R_JOINT_DEV_HIP] = s_dev;
-    /* Rsl table (rsl_env_cfg.py:279-407) */
-    {
-      double vb[3];
-      m3tv(R, vcom, vb); /* root_lin_vel_b */
-      terms[H12_R_TRACK_LIN_VEL_XY_BASE] = exp(-(sq(e.cmd[0] - vb[0]) + sq(e.cmd[1] - vb[1])) / std2);
-      terms[H12_R_TRACK_ANG_VEL_Z_BASE] = exp(-sq(e.cmd[2] - wb[2]) / std2);
-      terms[H12_R_BASE_HEIGHT_L2] = sq(e.p.pos[2] - c->base_height_target);
-      double s_v = 0, s_da = 0, s_lh = 0, s_cf = 0;
-      for (int j = 0; j < NJ; ++j) s_v += sq(e.p.qd[j]);
-      for (int f = 0; f < 2; ++f) {
-        for (int k = 4; k < 6; ++k) s_da += fabs(e.p.q[6 * f + k] - m->q_default[6 * f + k]);
-        for (int k = 0; k < 3; k += 2) { /* hip yaw, hip roll soft limits */
-          int j = 6 * f + k;
-          double mid = 0.5 * (m->q_lower[j] + m->q_upper[j]), half = 0.5 * (m->q_upper[j] - m->q_lower[j]) * c->soft_limit_factor;
-          double lo_s = mid - half, hi_s = mid + half, q = e.p.q[j];
-          s_lh += (q < lo_s ? lo_s - q : 0.0) + (q > hi_s ? q - hi_s : 0.0);
-        }
-        double viol = fmax_foot[f] - c->contact_force_threshold;
-        s_cf += viol > 0 ? viol : 0.0;
-      }
-      terms[H12_R_JOINT_VEL_L2] = s_v;
-      terms[H12_R_JOINT_DEV_ANKLE] = s_da;
-      terms[H12_R_DOF_POS_LIMITS_HIP] = s_lh;
-      terms[H12_R_CONTACT_FORCES] = s_cf;
-      terms[H12_R_LIN_VEL_Z_L2] = sq(vb[2]);
-    }
+    int term, tout;
+    orc_mdp_terms(m, c, &ti, terms, &term, &tout);
     double r = 0;
     for (int t = 0; t < H12_NREW; ++t) {
       double v = terms[t] * c->rew_w[t] * step_dt;
@@ -1435,7 +1562,12 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
       e.epsum[t] += v;
     }
     rew[i] = (float)r;
-    if (cs) cat_constraints(m, c, &e, tau_applied, fmax_foot, term, gb, n, i, F, step_dt, cs);
+    if (cs) {
+      double sw[2] = {F[(size_t)H12_F_SWING_H * n + i], F[(size_t)(H12_F_SWING_H + 1) * n + i]};
+      orc_cat_row(m, c, &ti, term, sw, cs + i, (size_t)n);
+      F[(size_t)H12_F_SWING_H * n + i] = (float)sw[0];
+      F[(size_t)(H12_F_SWING_H + 1) * n + i] = (float)sw[1];
+    }
     terminated[i] = (uint8_t)term;
     truncated[i] = (uint8_t)tout;
     if (applied_torque) for (int j = 0; j < NJ; ++j) applied_torque[(size_t)i * NJ + j] = (float)tau_applied[j];

@@ -82,6 +82,45 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
                  int32_t* istate, const float* actions, const float* obs_prev, float* obs, float* rew,
                  uint8_t* terminated, uint8_t* truncated, float* log_acc, float* applied_torque,
                  float* foot_force, float* cstr_prob, int64_t step_index, int n_threads);
+/* ---- MDP terms on a post-physics snapshot (the code orc_env_step runs; fixture-pinned in tests/) ---- */
+typedef struct orc_term_in {
+  orc_phys p;                      /* post-physics state of the env step */
+  double act[H12_NJ], act_prev[H12_NJ]; /* ActionManager action / prev_action */
+  double cmd[3];                   /* base_velocity command (pre-reset) */
+  double air[2], con[2];           /* ContactSensor current_air_time / current_contact_time of the feet */
+  double tau[H12_NJ];              /* applied_torque */
+  double jacc[H12_NJ];             /* joint_acc */
+  double fmax_foot[2], fmax_knee[2], fmax_torso; /* max over net_forces_w_history (3) of |F| */
+  int eplen;                       /* episode_length_buf after this step's increment */
+} orc_term_in;
+/* terminations + the H12_NREW unweighted reward terms */
+int orc_mdp_terms(const h12env_model* m, const h12env_config* c, const orc_term_in* in, double terms[H12_NREW],
+                  int* terminated, int* time_out);
+/* CaT constraint values of one env (+ still flag, episode length): out[col * stride], col < H12_NCSTR_COLS + 2;
+ * swing_h = foot_clearance's swing_max_height (in / out) */
+int orc_cat_row(const h12env_model* m, const h12env_config* c, const orc_term_in* in, int terminated,
+                double swing_h[2], double* out, size_t stride);
+/* CaT.add / get_probs over a batch of rows [H12_NCSTR_COLS + 2][n] (no_move remap included); run_max / run_init
+ * carry the running maxima; pmax [n], pterm [H12_NCSTR][n] and ceff [H12_NCSTR_COLS][n] (may be NULL) out */
+int orc_cat_probs(const h12env_config* c, int n, const double* cs, double run_max[H12_NCSTR_COLS], int* run_init,
+                  double* pmax, double* pterm, double* ceff);
+
+/* ConstraintManager episode statistics + their reset into the log accumulator; sum_v / sum_p [H12_NCSTR][n] */
+void orc_cat_stats(const h12env_config* c, int n, const double* pterm, const double* eplen, const uint8_t* reset,
+                   float* sum_v, float* sum_p, float* log_acc);
+/* commands: the update given its decisions (returns 1 = resample this env); terrain curriculum decision */
+int orc_cmd_update_decided(const h12env_config* c, double cmd[3], double heading_target, const double quat[4],
+                           int is_heading, int is_standing, int deactivate, int activate, int flip);
+void orc_terrain_move(const h12env_config* c, const double pos[3], const double origin[3], const double cmd[3], int* up,
+                      int* down);
+/* observations from explicit noise draws: the 45-float frame (noise + scale), the rough row (noise + clip),
+ * and one history update with nh frames per term */
+void orc_obs_frame_from(const h12env_config* c, const double raw[H12_OBS_FRAME], const double u[30],
+                        double fr[H12_OBS_FRAME]);
+void orc_rough_row_from(const h12env_config* c, const double raw[H12_NOBS_ROUGH], const double u[H12_NOBS_ROUGH - 15],
+                        float* out);
+void orc_history_write_n(const double frame[H12_OBS_FRAME], const float* prev_row, float* out_row, int fill, int nh);
+
 /* CaT running maxima carried between steps (process-global): forget them / read them. */
 void orc_cat_reset(void);
 void orc_cat_running_max(double out[H12_NCSTR_COLS]);

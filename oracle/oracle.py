@@ -48,6 +48,14 @@ class Phys(C.Structure):
         return p
 
 
+class TermIn(C.Structure):
+    """orc_term_in: the post-physics snapshot the MDP terms / CaT constraints are evaluated on."""
+    _fields_ = [("p", Phys), ("act", C.c_double * NJ), ("act_prev", C.c_double * NJ), ("cmd", C.c_double * 3),
+                ("air", C.c_double * 2), ("con", C.c_double * 2), ("tau", C.c_double * NJ), ("jacc", C.c_double * NJ),
+                ("fmax_foot", C.c_double * 2), ("fmax_knee", C.c_double * 2), ("fmax_torso", C.c_double),
+                ("eplen", C.c_int)]
+
+
 class Report(C.Structure):
     _fields_ = [("foot_force", (C.c_double * 3) * 2), ("knee_force", (C.c_double * 3) * 2),
                 ("torso_force", C.c_double * 3)]
@@ -101,6 +109,25 @@ def lib():
         L.orc_set_dz_count.restype = None
         L.orc_dz_count.argtypes = []
         L.orc_dz_count.restype = C.c_int
+        Tp = C.POINTER(TermIn)
+        L.orc_mdp_terms.argtypes = [M, Cf, Tp, dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.orc_mdp_terms.restype = C.c_int
+        L.orc_cat_row.argtypes = [M, Cf, Tp, C.c_int, dp, dp, C.c_size_t]
+        L.orc_cat_row.restype = C.c_int
+        L.orc_cat_probs.argtypes = [Cf, C.c_int, dp, dp, C.POINTER(C.c_int), dp, dp, dp]
+        L.orc_cat_probs.restype = C.c_int
+        L.orc_cat_stats.argtypes = [Cf, C.c_int, dp, dp, vp, vp, vp, vp]
+        L.orc_cat_stats.restype = None
+        L.orc_cmd_update_decided.argtypes = [Cf, dp, C.c_double, dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_cmd_update_decided.restype = C.c_int
+        L.orc_terrain_move.argtypes = [Cf, dp, dp, dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.orc_terrain_move.restype = None
+        L.orc_obs_frame_from.argtypes = [Cf, dp, dp, dp]
+        L.orc_obs_frame_from.restype = None
+        L.orc_rough_row_from.argtypes = [Cf, dp, dp, vp]
+        L.orc_rough_row_from.restype = None
+        L.orc_history_write_n.argtypes = [dp, vp, vp, C.c_int, C.c_int]
+        L.orc_history_write_n.restype = None
         _lib = L
     return _lib
 
@@ -122,6 +149,107 @@ def history_write(frame, prev_row, fill):
     prev = np.ascontiguousarray(prev_row, dtype=np.float32)
     out = np.empty(NOBS, dtype=np.float32)
     lib().orc_history_write(_d(frame), _p(prev), _p(out), int(fill))
+    return out
+
+
+def term_in(state, act, act_prev, cmd, air, con, tau, jacc, fmax_foot, fmax_knee, fmax_torso, eplen) -> TermIn:
+    """orc_term_in from numpy pieces; state = 37 physics coordinates (pos, quat wxyz, v_world, w_body, q, qd)."""
+    t = TermIn()
+    t.p = Phys.from_numpy(state)
+    t.act[:] = np.asarray(act, np.float64)
+    t.act_prev[:] = np.asarray(act_prev, np.float64)
+    t.cmd[:] = np.asarray(cmd, np.float64)
+    t.air[:] = np.asarray(air, np.float64)
+    t.con[:] = np.asarray(con, np.float64)
+    t.tau[:] = np.asarray(tau, np.float64)
+    t.jacc[:] = np.asarray(jacc, np.float64)
+    t.fmax_foot[:] = np.asarray(fmax_foot, np.float64)
+    t.fmax_knee[:] = np.asarray(fmax_knee, np.float64)
+    t.fmax_torso = float(fmax_torso)
+    t.eplen = int(eplen)
+    return t
+
+
+def mdp_terms(model, cfg, ti: TermIn):
+    """(20 unweighted reward terms, terminated, time_out) of one env snapshot."""
+    out = np.zeros(20)
+    term, tout = C.c_int(), C.c_int()
+    lib().orc_mdp_terms(C.byref(model), C.byref(cfg), C.byref(ti), _d(out), C.byref(term), C.byref(tout))
+    return out, bool(term.value), bool(tout.value)
+
+
+def cat_row(model, cfg, ti: TermIn, terminated: bool, swing_h):
+    """(58,) constraint values (+ still flag, episode length) of one env; swing_h (2,) updated in place."""
+    out = np.zeros(58)
+    sw = np.ascontiguousarray(swing_h, dtype=np.float64)
+    lib().orc_cat_row(C.byref(model), C.byref(cfg), C.byref(ti), int(terminated), _d(sw), _d(out), 1)
+    swing_h[:] = sw
+    return out
+
+
+class CaTProbs:
+    """orc_cat_probs with its running maxima carried between calls (a fresh CaT object)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.run_max = np.zeros(56)
+        self.init = C.c_int(0)
+
+    def __call__(self, cs):
+        cs = np.ascontiguousarray(cs, dtype=np.float64)
+        n = cs.shape[1]
+        pmax, pterm, ceff = np.zeros(n), np.zeros((10, n)), np.zeros((56, n))
+        lib().orc_cat_probs(C.byref(self.cfg), n, _d(cs), _d(self.run_max), C.byref(self.init), _d(pmax), _d(pterm),
+                            _d(ceff))
+        return pmax, pterm, ceff
+
+
+def cat_stats(cfg, pterm, eplen, reset, sum_v, sum_p, log_acc):
+    """orc_cat_stats on (10, n) episode sums (float32, updated in place) and a log accumulator (NLOG float32)."""
+    pterm = np.ascontiguousarray(pterm, dtype=np.float64)
+    eplen = np.ascontiguousarray(eplen, dtype=np.float64)
+    reset = np.ascontiguousarray(reset, dtype=np.uint8)
+    lib().orc_cat_stats(C.byref(cfg), pterm.shape[1], _d(pterm), _d(eplen), _p(reset), _p(sum_v), _p(sum_p),
+                        _p(log_acc))
+
+
+def cmd_update_decided(cfg, cmd, heading_target, quat, is_heading, is_standing, deactivate, activate, flip):
+    c = np.ascontiguousarray(cmd, dtype=np.float64).copy()
+    q = np.ascontiguousarray(quat, dtype=np.float64)
+    r = lib().orc_cmd_update_decided(C.byref(cfg), _d(c), float(heading_target), _d(q), int(is_heading),
+                                     int(is_standing), int(deactivate), int(activate), int(flip))
+    return c, bool(r)
+
+
+def terrain_move(cfg, pos, origin, cmd):
+    up, down = C.c_int(), C.c_int()
+    lib().orc_terrain_move(C.byref(cfg), _d(np.ascontiguousarray(pos, np.float64)),
+                           _d(np.ascontiguousarray(origin, np.float64)), _d(np.ascontiguousarray(cmd, np.float64)),
+                           C.byref(up), C.byref(down))
+    return bool(up.value), bool(down.value)
+
+
+def obs_frame_from(cfg, raw, u):
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    fr = np.zeros(45)
+    lib().orc_obs_frame_from(C.byref(cfg), _d(raw), _d(u), _d(fr))
+    return fr
+
+
+def rough_row_from(cfg, raw, u):
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    out = np.zeros(235, dtype=np.float32)
+    lib().orc_rough_row_from(C.byref(cfg), _d(raw), _d(u), _p(out))
+    return out
+
+
+def history_write_n(frame, prev_row, fill, nh):
+    frame = np.ascontiguousarray(frame, dtype=np.float64)
+    prev = np.ascontiguousarray(prev_row, dtype=np.float32)
+    out = np.empty(45 * nh, dtype=np.float32)
+    lib().orc_history_write_n(_d(frame), _p(prev), _p(out), int(fill), int(nh))
     return out
 
 
