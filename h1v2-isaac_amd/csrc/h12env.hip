@@ -191,6 +191,33 @@ H12_DEV float ground(const KParams& P, float x, float y, float& gx, float& gy) {
   return h00 + fu * a + fv * b;
 }
 
+// The same ground at the env-local point (xl, yl) (real axes) of an env whose origin is org: the contact
+// geometry runs in env-local coordinates (|x| of a few m) and only the per-env cell base (org - x0) / hs is
+// formed at the terrain's magnitude -- its rounding is one rigid shift shared by every contact point of the
+// env, where world coordinates (up to ~100 m on the C5 terrain, fp32 ulp 8e-6 m) would round each point
+// independently (independent sub-10-micron errors on stiff contacts).  Returns the height relative to org.z.
+H12_DEV float ground_local(const KParams& P, const float* org, float xl, float yl, float& gx, float& gy) {
+  const float cu = (org[0] - P.t_x0) * P.t_inv_hs, cv = (org[1] - P.t_y0) * P.t_inv_hs;
+  const float iu0 = floorf(cu), iv0 = floorf(cv);
+  const float u = (cu - iu0) + xl * P.t_inv_hs, v = (cv - iv0) + yl * P.t_inv_hs;
+  const float fu0 = floorf(u), fv0 = floorf(v);
+  int ix = (int)iu0 + (int)fu0, iy = (int)iv0 + (int)fv0;
+  float fu = u - fu0, fv = v - fv0;
+  // clamp to [0, n - 1 - 1e-3] in cell units as ground() does (flat border outside the grid)
+  if (ix < 0) { ix = 0; fu = 0.f; }
+  if (ix > P.t_nx - 2) { ix = P.t_nx - 2; fu = 1.f - 1e-3f; }
+  if (iy < 0) { iy = 0; fv = 0.f; }
+  if (iy > P.t_ny - 2) { iy = P.t_ny - 2; fv = 1.f - 1e-3f; }
+  const float* hp = P.t_h + (size_t)ix * P.t_ny + iy;
+  float h00 = hp[0], h01 = hp[1], h10 = hp[P.t_ny], h11 = hp[P.t_ny + 1];
+  float a, b;
+  if (fv >= fu) { a = h11 - h01; b = h01 - h00; }  // triangle (00, 11, 01)
+  else { a = h10 - h00; b = h11 - h10; }           // triangle (00, 10, 11)
+  gx = a * P.t_inv_hs;
+  gy = b * P.t_inv_hs;
+  return (h00 - org[2]) + fu * a + fv * b;
+}
+
 // ------------------------------------------------------------------ per-lane simulation state
 struct Base {               // shared floating base, REAL coordinates (identical in both lanes)
   float pos[3], quat[4], vlin[3], wang[3];
@@ -248,14 +275,15 @@ H12_DEV void impl_force(const float* a, const float* p, const float* u, float be
 
 // one penalty contact (sphere centre pl in body coords, body world pose Rb/pb, body spatial velocity
 // vb in body coords); adds the body-frame spatial force into f[6]; anchored stiction for sole spheres
-// sg: the lane's mirror sign (the heightfield is looked up at the real y = sg * y); mus / mud: Coulomb
+// sg: the lane's mirror sign (the heightfield is looked up at the real y = sg * y); org: the env origin (real
+// axes; positions are env-local on terrain, see ground_local); mus / mud: Coulomb
 // coefficients of this contact (per-env sole friction or the config's).  With P.impl, ic receives the
 // added point inertia of the contact (oracle contact_point) and f the force that cancels its weight
 // under the gravity-as-base-acceleration formulation.
 template <bool ANCHOR, bool TERRAIN>
 H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
                             const float* pl, float rad, float* f, float* fw, float* anc, bool was_in, float sg,
-                            float mus, float mud, ImplC& ic) {
+                            const float* org, float mus, float mud, ImplC& ic) {
   ic.beta = 0.f;
   ic.gamma = 0.f;
   float xw[3];
@@ -264,7 +292,7 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   float nrm[3] = {0.f, 0.f, 1.f}, depth;
   if constexpr (TERRAIN) {  // unit normal (-h_x, -h_y, 1)/|.| of the ground triangle
     float gx, gy;
-    float hg = ground(P, xw[0], sg * xw[1], gx, gy);
+    float hg = ground_local(P, org, xw[0], sg * xw[1], gx, gy);
     float in = __builtin_amdgcn_rsqf(1.f + gx * gx + gy * gy);
     nrm[0] = -gx * in; nrm[1] = -sg * gy * in; nrm[2] = in;
     depth = rad - (xw[2] - hg) * in;
@@ -662,7 +690,8 @@ H12_DEV void sole_impl_force_flat(const float* a, const float R[3][3], const Sol
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
 // lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
 template <int K>
-H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr) {
+H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
+                        const float* org) {
   const float sg = leg ? -1.f : 1.f;
   float R0[3][3];
   quat_R(b.quat, R0);
@@ -676,7 +705,10 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
   float vl0[6];
   for (int i = 0; i < 6; ++i) vl0[i] = s6(i, sg) * v0[i];
-  float p[3] = {b.pos[0], sg * b.pos[1], b.pos[2]};
+  // base position: env-local on terrain (contact geometry relative to the env origin, ground_local)
+  float pb0[3] = {b.pos[0], b.pos[1], b.pos[2]};
+  if constexpr (Feat<K>::terrain) { pb0[0] -= org[0]; pb0[1] -= org[1]; pb0[2] -= org[2]; }
+  float p[3] = {pb0[0], sg * pb0[1], pb0[2]};
   float cs[NL][2], v[NL][6];
   float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   ImplC ick;     // knee contact linearisation (added to link 3 in pass 2)
@@ -694,7 +726,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     const float* pl = lo0 ? h12m::KNEE0 : h12m::KNEE1;
     knee_pz = lo0 ? h12m::KNEE0[2] : h12m::KNEE1[2];
     float dummy[2];
-    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, P.mus, P.mud, ick);
+    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, org, P.mus, P.mud, ick);
   }
   link_pass1<4>(lg, cs, v[3], v, R, p);
   link_pass1<5>(lg, cs, v[4], v, R, p);
@@ -715,7 +747,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     for (int q = 0; q < H12_NFOOT_PTS; ++q) {
       bool was = (lg.cmask >> q) & 1;
       ImplC ic;
-      if (contact_sphere<true, Feat<K>::terrain>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was, sg, lg.mus,
+      if (contact_sphere<true, Feat<K>::terrain>(P, R, p, v[5], h12m::FOOT[q], h12m::FOOT_R, fext, fr.foot, lg.anc[q], was, sg, org, lg.mus,
                                lg.mud, ic)) {
         nmask |= 1 << q;
         if (P.impl) {
@@ -786,7 +818,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dummy[2];
-    if (contact_sphere<false, Feat<K>::terrain>(P, R0, b.pos, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, P.mus, P.mud,
+    if (contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org, P.mus, P.mud,
                                                 ict) &&
         P.impl)
       ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
@@ -1746,7 +1778,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
-      for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr);
+      for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
       // ContactSensor: net force = mean over the inner steps of the physics step
@@ -2073,7 +2105,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr);
+    for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
   }
   store_env<K>(P, W, e, leg, s);
 }

@@ -255,7 +255,7 @@ enum {
   H12_F_LAST_AIR = 70,  /* 2  last_air_time */
   H12_F_LAST_CONTACT = 72, /* 2 last_contact_time */
   H12_F_EPSUM = 74,     /* 12 episode reward sums */
-  H12_F_ANCHOR = 86,    /* 16 sole-sphere stiction anchors: [foot][pt][x,y] world (env-local) */
+  H12_F_ANCHOR = 86,    /* 16 sole-sphere stiction anchors: [foot][pt][x,y] world axes, relative to the env origin */
   H12_F_ORIGIN = 102,   /* 3  env origin (terrain origin of the env's level / type; 0 on the plane) */
   H12_F_MU = 105,       /* 4  static, dynamic friction of the left / right sole (per_env_friction) */
   H12_F_DMASS = 109,    /* 1  mass added at the torso COM (per_env_mass) */

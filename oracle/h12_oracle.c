@@ -780,9 +780,17 @@ static void env_load_extra(const h12env_config* c, const float* F, const int32_t
   e->p.dmass = c->per_env_mass ? F[(size_t)H12_F_DMASS * n + i] : 0.0;
   for (int a = 0; a < 3; ++a) e->origin[a] = c->terrain ? F[(size_t)(H12_F_ORIGIN + a) * n + i] : 0.0;
   e->tcell = (c->terrain && I) ? I[(size_t)H12_I_TERRAIN * n + i] : 0;
+  /* stiction anchors are stored relative to the env origin (the kernel's env-local contact geometry) */
+  for (int f = 0; f < 2; ++f)
+    for (int q = 0; q < H12_NFOOT_PTS; ++q)
+      for (int a = 0; a < 2; ++a) e->p.anchor[f][q][a] += e->origin[a];
 }
 static void env_store_extra(const h12env_config* c, float* F, int32_t* I, int n, int i, const orc_env* e) {
   if (!c->terrain) return;
+  for (int f = 0; f < 2; ++f)
+    for (int q = 0; q < H12_NFOOT_PTS; ++q)
+      for (int a = 0; a < 2; ++a)
+        F[(size_t)(H12_F_ANCHOR + 2 * H12_NFOOT_PTS * f + 2 * q + a) * n + i] = (float)(e->p.anchor[f][q][a] - e->origin[a]);
   for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_ORIGIN + a) * n + i] = (float)e->origin[a];
   I[(size_t)H12_I_TERRAIN * n + i] = e->tcell;
 }
@@ -958,6 +966,10 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   e->p.env_params = ep;
   memcpy(e->p.mu, mu, sizeof mu);
   e->p.dmass = dm;
+  /* cleared stiction anchors: 0 in the stored (origin-relative) frame */
+  for (int f = 0; f < 2; ++f)
+    for (int q = 0; q < H12_NFOOT_PTS; ++q)
+      for (int a = 0; a < 2; ++a) e->p.anchor[f][q][a] = e->origin[a];
   e->p.pos[0] = e->origin[0] + (double)(float)uab(r0[0], c->reset_x[0], c->reset_x[1]);
   e->p.pos[1] = e->origin[1] + (double)(float)uab(r0[1], c->reset_y[0], c->reset_y[1]);
   e->p.pos[2] = e->origin[2] + m->root_height;
@@ -1654,7 +1666,10 @@ int orc_env_step_physics(const h12env_model* m, const h12env_config* c, int n, f
     for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_VLIN + a) * n + i] = (float)e.p.vlin[a];
     for (int a = 0; a < 3; ++a) F[(size_t)(H12_F_WANG + a) * n + i] = (float)e.p.wang[a];
     for (int j = 0; j < NJ; ++j) { F[(size_t)(H12_F_Q + j) * n + i] = (float)e.p.q[j]; F[(size_t)(H12_F_QD + j) * n + i] = (float)e.p.qd[j]; }
-    for (int a = 0; a < 16; ++a) F[(size_t)(H12_F_ANCHOR + a) * n + i] = (float)(&e.p.anchor[0][0][0])[a];
+    for (int f = 0; f < 2; ++f)
+      for (int q = 0; q < H12_NFOOT_PTS; ++q)
+        for (int a = 0; a < 2; ++a)
+          F[(size_t)(H12_F_ANCHOR + 2 * H12_NFOOT_PTS * f + 2 * q + a) * n + i] = (float)(e.p.anchor[f][q][a] - e.origin[a]);
     if (I) I[(size_t)H12_I_PACK * n + i] = (pk & ~(0xFF << 13)) | ((e.p.cmask & 0xFF) << 13);
   }
   return 0;

@@ -8,6 +8,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests" / "helpers"))
 
 
 def pytest_configure(config):

@@ -1,0 +1,245 @@
+"""Teacher-forced (state-resynced) parity between the HIP env and the CPU oracle (test infrastructure).
+
+Every step the GPU workspace (float + int state) and the GPU's previous observation buffer are copied into
+the oracle, both take the same step with the same actions and step index, and each env is checked against
+per-criterion tolerances:
+
+  phys   base pose / velocity and joint state after the step   |g - o| <= TOL_PHYS * max(1, |o|)
+  flags  terminated, truncated                                   exact
+  ints   episode length, lags, steps-since-reset, command / contact flags (I state)   exact
+  rew    reward                                                  |g - o| <= TOL_REW_R * |o| + TOL_REW_A
+  terms  every reward term's weighted contribution (episode-sum deltas, envs that did not reset)
+                                                                 |g - o| <= TOL_TERM_R * |o| + TOL_TERM_A
+  obs    the observation row (history from the forced previous row; the new frame with its noise)
+                                                                 |g - o| <= TOL_OBS * max(1, |o|)
+
+The dynamics are piecewise (contact on/off, stick/slip, joint-limit and 1 N sensor thresholds), so an env
+whose state sits within fp32 rounding of a switching surface may legitimately flip.  Such envs are not
+waved through by a percentage alone: an env that fails a criterion must be shown to be threshold-sensitive by
+the oracle ITSELF -- some oracle re-run of that env from its pre-step state perturbed by PERTURBS relative
+(escalating from the GPU's fp32 error scale) must either reproduce the GPU's result (a flipped switch:
+integer and flag outputs identical and every other output within half the GPU-oracle distance) or, for a
+perturbation of at most AMPLIFY_EPS (~30x the fp32 error), move at least half as far from the unperturbed
+oracle as the GPU is (an ill-conditioned state).  Anything else is a kernel bug.  On
+top, at most 1 % of env-steps may fail.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+import oracle as O
+from h12env._abi import F as FIELDS
+from h12env._abi import I as IFIELDS
+
+TOL_PHYS = 1e-3
+TOL_REW_R, TOL_REW_A = 1e-3, 1e-5
+TOL_TERM_R, TOL_TERM_A = 1e-3, 1e-6
+TOL_OBS = 1e-3
+# escalating relative perturbations of the physics state for the sensitivity re-runs (first hit wins).
+# Calibration (oracle against itself, 4096 envs, one step): a 1e-7 perturbation keeps all but ~0.1 % of envs
+# inside the tolerances above, 1e-6 all but ~1 %; the GPU's fp32 error is of the order of 1e-7.  An env
+# off the oracle counts as threshold-sensitive when a perturbed oracle run REPRODUCES the GPU's result (lands
+# within half the GPU-oracle distance), or is ill-conditioned at the fp32 scale (AMPLIFY_EPS).  Round-2
+# 4096 x 1100 run: ~3.9k of 4.5M env-steps off tolerance; all but one explained within 112 draws, the last
+# one (a flip reached by ~1 in 400 draws at 1e-5) within 240.
+AMPLIFY_EPS = 3e-6
+PERTURBS = (1e-7,) * 16 + (1e-6,) * 32 + (3e-6,) * 64 + (1e-5,) * 128
+PHYS = ("POS", "QUAT", "VLIN", "WANG", "Q", "QD")
+TERMS = ("EPSUM", "EPSUM2")  # episode sums of the 20 kernel reward terms (12 Flat + 8 Rsl)
+CRITERIA = ("phys", "flags", "ints", "rew", "terms", "obs")
+
+
+def n_threads() -> int:
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _rows(Fm, names):
+    return np.concatenate([Fm[FIELDS[k][0]:FIELDS[k][0] + FIELDS[k][1]] for k in names], axis=0)
+
+
+def phys_err(Fa, Fb):
+    """Per-env max relative error of the physics state, |a - b| / max(1, |b|)."""
+    pa, pb = _rows(Fa, PHYS), _rows(Fb, PHYS)
+    return (np.abs(pa - pb) / np.maximum(1.0, np.abs(pb))).max(axis=0)
+
+
+def unexplained_envs(F0, gerr, tol, rerun, err_fn, base, gout, seed=0):
+    """Envs whose GPU error gerr = err_fn(gout, base) (per env) exceeds tol and that the oracle does not show
+    to be threshold-sensitive: rerun(F) re-runs the oracle (whole batch) from physics state F perturbed by
+    PERTURBS; an env is explained once some re-run reproduces the GPU's output, err_fn(run, gout) <= gerr / 2,
+    or a re-run with eps <= AMPLIFY_EPS moves at least gerr / 2 from the unperturbed oracle."""
+    rng = np.random.default_rng(seed)
+    bad = np.nonzero(gerr > tol)[0]
+    got = np.zeros(bad.size, bool)
+    for eps in PERTURBS:
+        if got.all():
+            break
+        run = rerun(perturbed(rng, F0, eps))
+        got |= err_fn(run, gout)[bad] <= 0.5 * gerr[bad]
+        if eps <= AMPLIFY_EPS:
+            got |= err_fn(run, base)[bad] >= 0.5 * gerr[bad]
+    return bad[~got]
+
+
+def compare(F0, Fa, Ia, obs_a, rew_a, term_a, trunc_a, Fb, Ib, obs_b, rew_b, term_b, trunc_b):
+    """Per-env bool masks (criterion -> ok) of run a against run b (b is the reference side), plus the
+    normalised error (error / tolerance) of each continuous criterion per env."""
+    ok, worst = {}, {}
+    e = phys_err(Fa, Fb) / TOL_PHYS
+    ok["phys"] = e <= 1.0
+    worst["phys"] = e
+    ok["flags"] = (term_a == term_b) & (trunc_a == trunc_b)
+    ok["ints"] = (Ia == Ib).all(axis=0)
+    e = np.abs(rew_a - rew_b) / (TOL_REW_R * np.abs(rew_b) + TOL_REW_A)
+    ok["rew"] = e <= 1.0
+    worst["rew"] = e
+    da = _rows(Fa, TERMS) - _rows(F0, TERMS)
+    db = _rows(Fb, TERMS) - _rows(F0, TERMS)
+    done = term_b | trunc_b | term_a | trunc_a
+    e = np.abs(da - db) / (TOL_TERM_R * np.abs(db) + TOL_TERM_A)
+    e[:, done] = 0.0
+    ok["terms"] = (e <= 1.0).all(axis=0)
+    worst["terms"] = e.max(axis=0)
+    e = np.abs(obs_a - obs_b) / (TOL_OBS * np.maximum(1.0, np.abs(obs_b)))
+    ok["obs"] = (e <= 1.0).all(axis=1)
+    worst["obs"] = e.max(axis=1)
+    return ok, worst
+
+
+def perturbed(rng, F0, eps):
+    Fp = F0.copy()
+    for k in PHYS:
+        o, c = FIELDS[k]
+        x = Fp[o:o + c].astype(np.float64)
+        x += eps * np.maximum(1.0, np.abs(x)) * rng.choice([-1.0, 1.0], size=x.shape)
+        if k == "QUAT":
+            x /= np.linalg.norm(x, axis=0, keepdims=True)
+        Fp[o:o + c] = x.astype(np.float32)
+    return Fp
+
+
+def _distance(F0, a, b, scale_from=None, exact=True):
+    """Tolerance-normalised max distance between two single-env step outputs (F, I, obs, rew, term, trunc);
+    scales from scale_from (default b).  With exact, integer / flag mismatches count as infinitely far."""
+    s = scale_from if scale_from is not None else b
+    if exact and not ((a[1] == b[1]).all() and (a[4] == b[4]).all() and (a[5] == b[5]).all()):
+        return np.inf
+    ps = _rows(s[0], PHYS)
+    d = (np.abs(_rows(a[0], PHYS) - _rows(b[0], PHYS)) / (TOL_PHYS * np.maximum(1.0, np.abs(ps)))).max()
+    d = max(d, float((np.abs(a[3] - b[3]) / (TOL_REW_R * np.abs(s[3]) + TOL_REW_A)).max()))
+    d = max(d, float((np.abs(_rows(a[0], TERMS) - _rows(b[0], TERMS)) /
+                      (TOL_TERM_R * np.abs(_rows(s[0], TERMS) - _rows(F0, TERMS)) + TOL_TERM_A)).max()))
+    d = max(d, float((np.abs(a[2] - b[2]) / (TOL_OBS * np.maximum(1.0, np.abs(s[2])))).max()))
+    return d
+
+
+class ForcedParity:
+    """Drive one H12VelocityEnv and an OracleEnv of the same config teacher-forced (see module doc)."""
+
+    def __init__(self, env, seed=0):
+        self.env = env
+        self.ref = O.OracleEnv(env._model, env._ccfg, env.num_envs, env.env_offset)
+        self.rng = np.random.default_rng(seed)
+        self.threads = n_threads()
+        self.bad_counts = {c: 0 for c in CRITERIA}
+        self.unexplained = []
+        self.explained = 0
+        self.dump = [] if os.environ.get("H12_FORCED_DUMP") else None
+        self.worst = {c: 0.0 for c in ("phys", "rew", "terms", "obs")}
+        self.steps = 0
+        self.env_steps = 0
+
+    def _oracle_step(self, F0, I0, obs0, a, t):
+        O.set_dz_count(self._dz0)  # the oracle's deadzone-command carry (Rsl) as it was before this step
+        self.ref.F[:] = F0
+        self.ref.I[:] = I0
+        self.ref.obs[:] = obs0
+        obs, rew, term, trunc, info = self.ref.step(a, t, n_threads=self.threads)
+        return self.ref.F.copy(), self.ref.I.copy(), obs, rew, term, trunc, info
+
+    def step(self, a_np):
+        """One forced step; returns (gpu outputs, oracle outputs, per-env ok mask)."""
+        import torch
+
+        env = self.env
+        F0 = env._fstate.cpu().numpy().copy()
+        I0 = env._istate.cpu().numpy().copy()
+        obs0 = env._obs[env._k].cpu().numpy().copy()
+        self.last_F0 = F0
+        obs, rew, term, trunc, ex = env.step(torch.from_numpy(a_np).to(env.device))
+        t = env.common_step_counter
+        g = (env._fstate.cpu().numpy().copy(), env._istate.cpu().numpy().copy(), obs["policy"].cpu().numpy(),
+             rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy())
+        self._dz0 = O.dz_count()
+        o = self._oracle_step(F0, I0, obs0, a_np, t)
+        dz1 = O.dz_count()
+        ok, worst = compare(F0, *g, *o[:6])
+        allok = np.ones(env.num_envs, bool)
+        for c in CRITERIA:
+            self.bad_counts[c] += int((~ok[c]).sum())
+            allok &= ok[c]
+        for c in self.worst:
+            w = worst[c][ok[c]]
+            if w.size:
+                self.worst[c] = max(self.worst[c], float(w.max()))
+        if not allok.all():
+            for e in np.nonzero(~allok)[0]:
+                if self._reproduced(e, F0, I0, obs0, a_np, t, g, o):
+                    self.explained += 1
+                    continue
+                self.unexplained.append((t, int(e), [c for c in CRITERIA if not ok[c][e]],
+                                         {c: round(float(worst[c][e]), 3) for c in worst}))
+                if self.dump is not None:  # the env's inputs and both outputs, for offline diagnosis
+                    self.dump.append(dict(t=t, e=int(e), F0=F0[:, e], I0=I0[:, e], obs0=obs0[e], a=a_np[e],
+                                          Fg=g[0][:, e], Ig=g[1][:, e], Fo=o[0][:, e], Io=o[1][:, e]))
+        O.set_dz_count(dz1)
+        self.steps += 1
+        self.env_steps += env.num_envs
+        return g, o, allok, ex
+
+    def _reproduced(self, e, F0, I0, obs0, a_np, t, g, o):
+        """True when the oracle, re-run for env e alone from its pre-step state perturbed by PERTURBS,
+        lands within half the GPU-oracle distance of the GPU's result (composite, tolerance-normalised
+        distance over every criterion; integer / flag outputs must match the GPU's exactly)."""
+        ref = O.OracleEnv(self.env._model, self.env._ccfg, 1, self.env.env_offset + int(e))
+        o_e = tuple(x[:, e:e + 1] if x.ndim == 2 and x.shape[-1] == self.env.num_envs else x[e:e + 1] for x in o[:6])
+        g_e = tuple(x[:, e:e + 1] if x.ndim == 2 and x.shape[-1] == self.env.num_envs else x[e:e + 1] for x in g[:6])
+        f0 = F0[:, e:e + 1]
+        d_og = _distance(f0, g_e, o_e, exact=False)
+        for eps in PERTURBS:
+            O.set_dz_count(self._dz0)
+            ref.F[:], ref.I[:], ref.obs[:] = perturbed(self.rng, f0, eps), I0[:, e:e + 1], obs0[e:e + 1]
+            po, pr, pt, ptr, _ = ref.step(a_np[e:e + 1], t)
+            p_e = (ref.F.copy(), ref.I.copy(), po, pr, pt, ptr)
+            d_pg = _distance(f0, g_e, p_e, o_e)
+            if d_pg <= 0.5 * d_og or (d_og == 0.0 and d_pg == 0.0):
+                return True  # the perturbed oracle reproduces the GPU's result (a flipped switch)
+            if eps <= AMPLIFY_EPS and _distance(f0, p_e, o_e, exact=False) >= 0.5 * d_og:
+                return True  # ill-conditioned: the oracle itself moves as far under an fp32-scale perturbation
+        return False
+
+    def report(self) -> str:
+        frac = {c: self.bad_counts[c] / max(1, self.env_steps) for c in CRITERIA}
+        return (f"steps {self.steps} x {self.env.num_envs} envs; failing env-steps per criterion {frac}; worst "
+                f"passing error / tolerance {self.worst}; threshold-sensitive (explained) env-steps {self.explained}; unexplained (not threshold-sensitive) "
+                f"{len(self.unexplained)}: {self.unexplained[:8]}")
+
+    def save_dump(self, tag):
+        if self.dump:
+            path = os.path.join(os.environ["H12_FORCED_DUMP"], f"{tag}.npz")
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            np.savez(path, **{f"{k}_{i}": v for i, d in enumerate(self.dump) for k, v in d.items()})
+
+    def check(self, max_bad_frac=0.01):
+        if self.dump:
+            self.save_dump(os.environ.get("PYTEST_CURRENT_TEST", "forced").split(" ")[0].replace("/", "_").replace(":", "_"))
+        assert not self.unexplained, self.report()
+        for c in CRITERIA:
+            assert self.bad_counts[c] <= max_bad_frac * self.env_steps, self.report()
+
+
+def int_field(I, name):
+    o, _ = IFIELDS[name]
+    return I[o]

@@ -7,8 +7,9 @@ Tolerances (fp32 kernel vs fp64 oracle):
     (the BASELINE.json north_star criterion, contact-free segment)
   * integer / boolean outputs (terminated, truncated, episode counters, lags): bit-exact
 Contact and stiction make the dynamics piecewise: states whose contact/slip decision sits within fp32
-rounding of a threshold can legitimately flip; the contact-state tests therefore check >= 99 % of envs
-at the tight tolerance and all envs finite, and say so.
+rounding of a threshold can legitimately flip.  The contact-state tests therefore require every env at the
+tight tolerance OR shown threshold-sensitive by the oracle itself (re-run from a slightly perturbed state,
+tests/helpers/forced.py), with at most 1 % such envs and all envs finite.
 """
 import numpy as np
 import pytest
@@ -18,6 +19,7 @@ import oracle as O
 from h12env import H12FlatEnvCfg, mujoco_cfg
 from h12env._abi import F as FIELDS
 from h12env.env import H12VelocityEnv
+from forced import ForcedParity, phys_err, unexplained_envs
 
 pytestmark = pytest.mark.gpu
 
@@ -124,41 +126,41 @@ def test_physics_step_parity_contact(gpu, integrator):
     rng = np.random.default_rng(2)
     scatter_states(env, ref, rng, height=(0.95, 1.06))
     q_ref = (np.asarray(env._model.q_default)[None] + rng.normal(size=(n, 12)) * 0.3).astype(np.float32)
+    F0, I0 = ref.F.copy(), ref.I.copy()
+
+    def rerun(Fs):
+        ref.F[:], ref.I[:] = Fs, I0
+        for _ in range(4):
+            ref.step_physics(q_ref, 1)
+        return ref.F.copy()
+
     for _ in range(4):
         env.step_physics(torch.from_numpy(q_ref).cuda(), 1)
-        ref.step_physics(q_ref, 1)
-    g = phys_fields(env._fstate.cpu().numpy())
-    o = phys_fields(ref.F)
-    ok = np.ones(n, bool)
-    for k in g:
-        assert np.isfinite(g[k]).all()
-        ok &= (rel_err(g[k], o[k], axis=0) < 2e-3).all(axis=0)
-    assert ok.mean() >= 0.99, f"only {ok.mean():.4f} of envs within tolerance"
+    g = env._fstate.cpu().numpy()
+    base = rerun(F0)
+    assert np.isfinite(g).all()
+    gerr = phys_err(g, base)
+    bad = unexplained_envs(F0, gerr, 2e-3, rerun, phys_err, base, g)
+    assert bad.size == 0, f"{bad.size} envs off the oracle and not threshold-sensitive: {bad[:10]} {gerr[bad[:10]]}"
+    assert (gerr > 2e-3).mean() <= 0.01, (gerr > 2e-3).mean()
     env.close()
 
 
 @pytest.mark.parametrize("integrator", list(INTEGRATORS))
 def test_env_step_parity(gpu, integrator):
-    """Full MDP step (delayed PD, physics, sensor, terminations, rewards, resets, commands, obs)."""
+    """Full MDP step (delayed PD, physics, sensor, terminations, rewards per term, resets, commands, obs),
+    60 teacher-forced steps from reset: every env matches the oracle on every criterion of
+    tests/helpers/forced.py or is shown threshold-sensitive by the oracle itself."""
     n = 512
     env = make(n, integrator_cfg(integrator))
-    obs, _ = env.reset()
-    ref = O.OracleEnv(env._model, env._ccfg, n)
-    ref.reset()
+    env.reset()
+    fp = ForcedParity(env, seed=3)
     rng = np.random.default_rng(3)
-    for t in range(1, 4):
+    for t in range(60):
         a = rng.normal(size=(n, 12)).astype(np.float32)
-        obs, rew, term, trunc, ex = env.step(torch.from_numpy(a).cuda())
-        r_obs, r_rew, r_term, r_trunc, r_ex = ref.step(a, t)
-        torch.cuda.synchronize()
-        go = obs["policy"].cpu().numpy()
-        ok = (np.abs(go - r_obs) <= 2e-3 * np.maximum(1, np.abs(r_obs))).all(axis=1)
-        assert ok.mean() >= 0.99, (t, ok.mean())
-        assert (term.cpu().numpy() == r_term).mean() >= 0.99
-        assert (trunc.cpu().numpy() == r_trunc).all()
-        assert np.isfinite(rew.cpu().numpy()).all()
-        okr = np.abs(rew.cpu().numpy() - r_rew) <= 1e-3 * np.maximum(1, np.abs(r_rew))
-        assert okr.mean() >= 0.99, (t, okr.mean())
+        (_, _, _, rew, _, _), _, _, _ = fp.step(a)
+        assert np.isfinite(rew).all()
+    fp.check(max_bad_frac=0.01)
     env.close()
 
 
@@ -166,7 +168,8 @@ def test_env_step_parity(gpu, integrator):
 def test_contact_force_and_torque_parity(gpu, integrator):
     """One MDP step from identical generated near-ground states: the feet's reported net contact force (with the
     implicit part -M a_p of the implicit integrator, added after the solve) and the applied joint torques agree
-    with the oracle (>= 99 % of envs; contact / slip decisions can flip within fp32 rounding)."""
+    with the oracle; an env off the oracle must be threshold-sensitive in the oracle itself (contact / slip
+    decisions can flip within fp32 rounding), and at most 1 % may be."""
     n = 1024
     env = make(n, integrator_cfg(integrator))
     env.reset()
@@ -175,17 +178,27 @@ def test_contact_force_and_torque_parity(gpu, integrator):
     rng = np.random.default_rng(7)
     scatter_states(env, ref, rng, height=(0.95, 1.04))
     a = rng.normal(size=(n, 12)).astype(np.float32) * 0.5
+    F0, I0, obs0 = ref.F.copy(), ref.I.copy(), ref.obs.copy()
+
+    def rerun(Fs):
+        ref.F[:], ref.I[:], ref.obs[:] = Fs, I0, obs0
+        _, _, _, _, info = ref.step(a, 1)
+        return np.concatenate([info["foot_force"], info["applied_torque"]], axis=1)
+
+    def err(x, b):  # feet: 1e-2 of max(10 N, |F|); torques: 2e-3 of max(1, |tau|) -> normalised to tol 1
+        ef = np.abs(x[:, :2] - b[:, :2]) / (1e-2 * np.maximum(10.0, np.abs(b[:, :2])))
+        et = np.abs(x[:, 2:] - b[:, 2:]) / (2e-3 * np.maximum(1.0, np.abs(b[:, 2:])))
+        return np.maximum(ef.max(axis=1), et.max(axis=1))
+
     env.step(torch.from_numpy(a).cuda())
-    _, _, _, _, info = ref.step(a, 1)
+    base = rerun(F0)
     torch.cuda.synchronize()
-    gf = env.foot_contact_force.cpu().numpy()
-    of = info["foot_force"]
-    assert (of > 1.0).mean() > 0.3  # most envs have a foot on the ground
-    okf = (np.abs(gf - of) <= 1e-2 * np.maximum(10.0, np.abs(of))).all(axis=1)
-    assert okf.mean() >= 0.99, okf.mean()
-    gt = env._applied_torque.cpu().numpy()
-    okt = (np.abs(gt - info["applied_torque"]) <= 2e-3 * np.maximum(1.0, np.abs(info["applied_torque"]))).all(axis=1)
-    assert okt.mean() >= 0.99, okt.mean()
+    g = np.concatenate([env.foot_contact_force.cpu().numpy(), env._applied_torque.cpu().numpy()], axis=1)
+    assert (base[:, :2] > 1.0).mean() > 0.3  # most envs have a foot on the ground
+    gerr = err(g, base)
+    bad = unexplained_envs(F0, gerr, 1.0, rerun, err, base, g)
+    assert bad.size == 0, f"{bad.size} envs off the oracle and not threshold-sensitive: {bad[:10]} {gerr[bad[:10]]}"
+    assert (gerr > 1.0).mean() <= 0.01, (gerr > 1.0).mean()
     env.close()
 
 
