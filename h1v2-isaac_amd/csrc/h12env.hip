@@ -99,6 +99,8 @@ struct KParams {
   // below the drag cap) of every active contact to its body in the dynamics solve
   int impl;
   float fc_v;             // viscous tangential coefficient of the knee / torso contacts
+  int self_coll;          // self-collision between the legs (h12env_config.self_collision)
+  float sk, sc, sct, smu; // its normal stiffness / damping, tangential damping, Coulomb cap
   float dl;               // implicit joint-limit inertia h (lc + h lk) (lc already includes h lk)
   float cmd_T, cmd_x0, cmd_x1, cmd_y0, cmd_y1, cmd_w0, cmd_w1, cmd_h0, cmd_h1;
   float rel_stand, rel_head, head_k;
@@ -687,6 +689,190 @@ H12_DEV void sole_impl_force_flat(const float* a, const float R[3][3], const Sol
   f[2] -= xb[2] + ss.sb * a[5] + gn * u[2];
 }
 
+// ---- self-collision between the legs (oracle self_contacts; h12env_config.self_collision).  Capsules: the knee
+// cylinder (KNEE0-KNEE1, KNEE_R) and the four sole rods (ROD, FOOT_R) of each leg; every left/right pair (25).
+//  * broad phase, every physics step, split over the lane pair: a knee segment and a foot bounding capsule
+//    (FB0-FB1, FB_R) per leg, four capsule tests (knee-knee, knee-foot x2, foot-foot), two per lane;
+//  * narrow phase only in waves where some env has a candidate group, and COMPACTED across the wave: the
+//    lanes stage their leg's capsules and body kinematics in LDS, then the 25 pair jobs of every candidate env
+//    are spread over all 64 lanes (one pass for up to 2 such envs), each job adding its pair force and moment
+//    to the two bodies' LDS accumulators with no-return LDS float atomics (one wave per block: order fixed
+//    by the single wave's instruction stream), and each lane reads back its own knee / foot wrench.
+// Real (un-mirrored) coordinates throughout; the pair force acts +F on the left body, -F on the right one.
+
+// closest points of segments p1-q1 and p2-q2 (the construction of the oracle's seg_closest)
+H12_DEV void seg_closest(const float* p1, const float* q1, const float* p2, const float* q2, float* c1, float* c2) {
+  float d1[3], d2[3], r[3];
+  for (int a = 0; a < 3; ++a) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
+  const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
+  const float den = A * E - B * B, iA = frcp(A);
+  float s;
+  if (den > 1e-3f * A * E) {
+    s = fminf(fmaxf((B * F - C * E) * frcp(den), 0.f), 1.f);
+  } else {  // nearly parallel (sin^2 < 1e-3): middle of the overlap along the first segment (oracle seg_closest)
+    const float t0 = -C * iA, t1 = (B - C) * iA;
+    const float lo = fmaxf(0.f, fminf(t0, t1)), hi = fminf(1.f, fmaxf(t0, t1));
+    s = fminf(fmaxf(0.5f * (lo + hi), 0.f), 1.f);
+  }
+  float t = (B * s + F) * frcp(E);
+  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-C * iA, 0.f), 1.f); }
+  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((B - C) * iA, 0.f), 1.f); }
+  for (int a = 0; a < 3; ++a) { c1[a] = p1[a] + d1[a] * s; c2[a] = p2[a] + d2[a] * t; }
+}
+H12_DEV bool capsules_near(const float* p1, const float* q1, const float* p2, const float* q2, float rr) {
+  float c1[3], c2[3];
+  seg_closest(p1, q1, p2, q2, c1, c2);
+  const float d[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
+  return dot3(d, d) < rr * rr;
+}
+// real-frame point of a lane-frame body point: M (Rb pl + pb), M = diag(1, sg, 1)
+H12_DEV void body_point_real(const float Rb[3][3], const float* pb, const float* pl, float sg, float* out) {
+  mv(Rb, pl, out);
+  out[0] += pb[0]; out[1] = sg * (out[1] + pb[1]); out[2] += pb[2];
+}
+H12_DEV void swap3(const float* a, float* b) { b[0] = pair_swap(a[0]); b[1] = pair_swap(a[1]); b[2] = pair_swap(a[2]); }
+
+// LDS staging of one wave (block = one wave): per env and leg 16 float4 -- knee segment (2), sole rods (8),
+// knee w / v / origin (3), foot w / v / origin (3), real frame -- and the per-body wrench accumulators
+// (F, moment about the world origin).
+constexpr int SG_KNEE = 0, SG_ROD = 2, SG_KKIN = 10, SG_FKIN = 13, SG_N = 16;
+struct SelfLds {
+  float4 geo[ENVS_PER_BLOCK][2][SG_N];
+  float acc[ENVS_PER_BLOCK][2][2][8];  // [env][leg][body: 0 knee, 1 foot][F xyz, pad, m xyz, pad]
+  int slot[ENVS_PER_BLOCK], flags[ENVS_PER_BLOCK];
+};
+
+// Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
+// added to the reported knee / foot contact forces.  Rk/pk, vk: knee pose (lane frame) and body velocity,
+// Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP swap; wave-uniform at every barrier.
+H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
+                           const float (&Rf)[3][3], const float* pf, const float* vf, float* wk, float* wf, Forces& fr) {
+  __shared__ SelfLds L;
+  const float sg = leg ? -1.f : 1.f;
+  for (int i = 0; i < 6; ++i) { wk[i] = 0.f; wf[i] = 0.f; }
+  // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
+  float k0[3], k1[3], b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
+  body_point_real(Rk, pk, h12m::KNEE0, sg, k0);
+  body_point_real(Rk, pk, h12m::KNEE1, sg, k1);
+  body_point_real(Rf, pf, h12m::FB0, sg, b0);
+  body_point_real(Rf, pf, h12m::FB1, sg, b1);
+  swap3(k0, ok0); swap3(k1, ok1); swap3(b0, ob0); swap3(b1, ob1);
+  // own left capsule (lane 0: its knee; lane 1: the partner's = left foot bound) vs the right leg's two
+  // value selects (a select between register arrays by pointer would go through scratch)
+  float La[3], Lb[3], Rk0[3], Rk1[3], Rb0[3], Rb1[3];
+  for (int a = 0; a < 3; ++a) {
+    La[a] = leg ? ob0[a] : k0[a]; Lb[a] = leg ? ob1[a] : k1[a];
+    Rk0[a] = leg ? k0[a] : ok0[a]; Rk1[a] = leg ? k1[a] : ok1[a];
+    Rb0[a] = leg ? b0[a] : ob0[a]; Rb1[a] = leg ? b1[a] : ob1[a];
+  }
+  const float rl = leg ? h12m::FB_R : h12m::KNEE_R;
+  const int f0 = capsules_near(La, Lb, Rk0, Rk1, rl + h12m::KNEE_R) ? 1 : 0;
+  const int f1 = capsules_near(La, Lb, Rb0, Rb1, rl + h12m::FB_R) ? 1 : 0;
+  const int mine = (f0 | f1 << 1) << (2 * leg);   // bits: 0 kk, 1 kf, 2 fk, 3 ff (left capsule major)
+  const int flags = mine | pair_swap_i(mine);
+  const uint64_t act = __ballot(flags != 0 && leg == 0);
+  if (act == 0) return;  // wave-uniform: no candidate pair anywhere in the wave
+  // ---- stage this leg's capsules and body kinematics (real frame)
+  const int el = threadIdx.x >> 1;
+  {
+    float4* g = L.geo[el][leg];
+    g[SG_KNEE] = make_float4(k0[0], k0[1], k0[2], 0.f);
+    g[SG_KNEE + 1] = make_float4(k1[0], k1[1], k1[2], 0.f);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a0[3], a1[3];
+      body_point_real(Rf, pf, h12m::ROD[r][0], sg, a0);
+      body_point_real(Rf, pf, h12m::ROD[r][1], sg, a1);
+      g[SG_ROD + 2 * r] = make_float4(a0[0], a0[1], a0[2], 0.f);
+      g[SG_ROD + 2 * r + 1] = make_float4(a1[0], a1[1], a1[2], 0.f);
+    }
+    // world angular velocity (a pseudo-vector: w_real = det(M) M w_lane, det M = sg), origin velocity, origin
+    float w[3], v[3];
+    mv(Rk, vk, w); mv(Rk, vk + 3, v);
+    g[SG_KKIN] = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+    g[SG_KKIN + 1] = make_float4(v[0], sg * v[1], v[2], 0.f);
+    g[SG_KKIN + 2] = make_float4(pk[0], sg * pk[1], pk[2], 0.f);
+    mv(Rf, vf, w); mv(Rf, vf + 3, v);
+    g[SG_FKIN] = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+    g[SG_FKIN + 1] = make_float4(v[0], sg * v[1], v[2], 0.f);
+    g[SG_FKIN + 2] = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
+    float* ac = L.acc[el][leg][0];
+    for (int i = 0; i < 16; ++i) ac[i] = 0.f;
+    if (leg == 0 && flags) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+      L.slot[rank] = el;
+      L.flags[rank] = flags;
+    }
+  }
+  __syncthreads();
+  // ---- pair jobs of the candidate envs over the wave's live lanes (a ragged last block has fewer):
+  // job = (env rank, left capsule i, right capsule j)
+  const uint64_t live = __ballot(1);
+  const int nlive = __popcll(live);
+  const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+  const int njobs = 25 * __popcll(act);
+  for (int jb = me; jb < njobs; jb += nlive) {
+    const int rank = jb / 25, k = jb - 25 * rank, i = k / 5, j = k - 5 * i;
+    const int e = L.slot[rank], fl = L.flags[rank];
+    if (!((fl >> (2 * (i > 0) + (j > 0))) & 1)) continue;
+    const float4* gl = L.geo[e][0];
+    const float4* gr = L.geo[e][1];
+    const float4 la = gl[i == 0 ? SG_KNEE : SG_ROD + 2 * (i - 1)], lb = gl[i == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (i - 1) + 1];
+    const float4 ra = gr[j == 0 ? SG_KNEE : SG_ROD + 2 * (j - 1)], rb = gr[j == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (j - 1) + 1];
+    const float pa[3] = {la.x, la.y, la.z}, pb[3] = {lb.x, lb.y, lb.z}, qa[3] = {ra.x, ra.y, ra.z}, qb[3] = {rb.x, rb.y, rb.z};
+    const float rs = (i == 0 ? h12m::KNEE_R : h12m::FOOT_R) + (j == 0 ? h12m::KNEE_R : h12m::FOOT_R);
+    float cA[3], cB[3];
+    seg_closest(pa, pb, qa, qb, cA, cB);
+    const float dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
+    const float d2 = dot3(dv, dv);
+    if (!(d2 < rs * rs) || !(d2 > 1e-18f)) continue;
+    const float d = fsqrt(d2), depth = rs - d, id = frcp(d);
+    const float n[3] = {dv[0] * id, dv[1] * id, dv[2] * id};
+    const float x[3] = {0.5f * (cA[0] + cB[0]), 0.5f * (cA[1] + cB[1]), 0.5f * (cA[2] + cB[2])};
+    const float4* kl = gl + (i == 0 ? SG_KKIN : SG_FKIN);
+    const float4* kr = gr + (j == 0 ? SG_KKIN : SG_FKIN);
+    const float4 wl = kl[0], vl = kl[1], ol = kl[2], wr = kr[0], vr_ = kr[1], orr = kr[2];
+    const float rl_[3] = {x[0] - ol.x, x[1] - ol.y, x[2] - ol.z}, rr_[3] = {x[0] - orr.x, x[1] - orr.y, x[2] - orr.z};
+    const float WL[3] = {wl.x, wl.y, wl.z}, WR[3] = {wr.x, wr.y, wr.z};
+    float ul[3], ur[3];
+    cross(WL, rl_, ul);
+    cross(WR, rr_, ur);
+    const float vrel[3] = {vl.x + ul[0] - vr_.x - ur[0], vl.y + ul[1] - vr_.y - ur[1], vl.z + ul[2] - vr_.z - ur[2]};
+    const float vn = dot3(vrel, n), fn = P.sk * depth - P.sc * vn;
+    if (!(fn > 0.f)) continue;
+    float F[3];
+    for (int a = 0; a < 3; ++a) F[a] = -P.sct * (vrel[a] - vn * n[a]);
+    const float ftn2 = dot3(F, F), cap = P.smu * fn;
+    if (ftn2 > cap * cap) { const float sc = cap * __builtin_amdgcn_rsqf(ftn2); F[0] *= sc; F[1] *= sc; F[2] *= sc; }
+    for (int a = 0; a < 3; ++a) F[a] += fn * n[a];
+    float m[3];
+    cross(x, F, m);
+    float* al = L.acc[e][0][i > 0];
+    float* ar = L.acc[e][1][j > 0];
+    for (int a = 0; a < 3; ++a) {
+      atomicAdd(&al[a], F[a]); atomicAdd(&al[4 + a], m[a]);
+      atomicAdd(&ar[a], -F[a]); atomicAdd(&ar[4 + a], -m[a]);
+    }
+  }
+  __syncthreads();
+  // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
+  const float ms[3] = {1.f, sg, 1.f};
+  auto own_body = [&](const float* ac, const float* po, const float (&Rb)[3][3], float* w, float* rep) {
+    const float Fr[3] = {ac[0], ac[1], ac[2]};
+    const float por[3] = {po[0], sg * po[1], po[2]};
+    float pxF[3];
+    cross(por, Fr, pxF);
+    float Fl[3], Tl[3], fb[3], tb[3];
+    for (int a = 0; a < 3; ++a) { Fl[a] = ms[a] * Fr[a]; Tl[a] = sg * ms[a] * (ac[4 + a] - pxF[a]); }
+    mtv(Rb, Fl, fb);
+    mtv(Rb, Tl, tb);
+    for (int a = 0; a < 3; ++a) { w[a] = tb[a]; w[3 + a] = fb[a]; rep[a] += fb[a]; }
+  };
+  own_body(L.acc[el][leg][0], pk, Rk, wk, fr.knee);
+  own_body(L.acc[el][leg][1], pf, Rf, wf, fr.foot);
+  __syncthreads();  // the staging area is rewritten by the next physics step
+}
+
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
 // lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
 template <int K>
@@ -717,6 +903,11 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   link_pass1<1>(lg, cs, v[0], v, R, p);
   link_pass1<2>(lg, cs, v[1], v, R, p);
   link_pass1<3>(lg, cs, v[2], v, R, p);
+  float Rk[3][3], pk[3];  // knee pose, kept for the self-collision pass
+  for (int i = 0; i < 3; ++i) {
+    pk[i] = p[i];
+    for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j];
+  }
   {
     // knee capsule: lower end point, contact evaluated at the knee link pose
     float w0[3], w1[3];
@@ -730,6 +921,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   }
   link_pass1<4>(lg, cs, v[3], v, R, p);
   link_pass1<5>(lg, cs, v[4], v, R, p);
+  // self-contacts between the legs: explicit wrenches on the knee (-> fext_knee) and the foot (-> pAcc below)
+  float wsf[6];
+  if (P.self_coll) {
+    float wsk[6];
+    self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wsk, wsf, fr);
+    for (int i = 0; i < 6; ++i) fext_knee[i] += wsk[i];
+  }
   // ---- foot: 4 anchored sole spheres on the ankle-roll link; starts pass 2 of link 5
   int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
   float fu[H12_NFOOT_PTS][3];         // implicit: ground normal at each sole sphere, foot coords
@@ -738,6 +936,8 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float pAcc[6];
   bias<5>(v[5], pAcc);
   SoleSums ss;
+  if (P.self_coll)
+    for (int i = 0; i < 6; ++i) pAcc[i] -= wsf[i];
   if constexpr (!Feat<K>::terrain) {
     sole_contacts_flat(P, R, p, v[5], lg, IA, pAcc, fr.foot, ss);
   } else {
@@ -1863,6 +2063,50 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
   }
 }
 
+// Self-contact hook (h12env_eval_self_contacts, parity tests only): the self-contact wrenches step_kernel's
+// physics applies on the workspace state as it stands, per env [leg][knee, foot][moment xyz, force xyz] in
+// REAL body coordinates (the oracle's fext layout).
+template <int K>
+__global__ void __launch_bounds__(BLOCK) selfc_kernel(KParams P, Workspace W, float* out) {
+  const int leg = threadIdx.x & 1;
+  const float sg = leg ? -1.f : 1.f;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);
+  if (e >= W.n) return;
+  EnvSt s;
+  load_phys<K>(P, W, e, leg, s);
+  float R0[3][3];
+  quat_R(s.b.quat, R0);
+  float vb[3];
+  mtv(R0, s.b.vlin, vb);
+  const float mm[3] = {1.f, sg, 1.f};
+  float R[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[i][j] = mm[i] * mm[j] * R0[i][j];
+  float v0[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
+  for (int i = 0; i < 6; ++i) v0[i] *= s6(i, sg);
+  float p[3] = {s.b.pos[0], sg * s.b.pos[1], s.b.pos[2]};
+  float cs[NL][2], v[NL][6];
+  link_pass1<0>(s.lg, cs, v0, v, R, p);
+  link_pass1<1>(s.lg, cs, v[0], v, R, p);
+  link_pass1<2>(s.lg, cs, v[1], v, R, p);
+  link_pass1<3>(s.lg, cs, v[2], v, R, p);
+  float Rk[3][3], pk[3];
+  for (int i = 0; i < 3; ++i) {
+    pk[i] = p[i];
+    for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j];
+  }
+  link_pass1<4>(s.lg, cs, v[3], v, R, p);
+  link_pass1<5>(s.lg, cs, v[4], v, R, p);
+  float wk[6], wf[6];
+  Forces fr = {};
+  self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wk, wf, fr);
+  float* o = out + ((size_t)e * 2 + leg) * 12;
+  for (int a = 0; a < 3; ++a) {  // lane body frame -> real body frame (force M f, moment sg M m)
+    o[a] = sg * mm[a] * wk[a]; o[3 + a] = mm[a] * wk[3 + a];
+    o[6 + a] = sg * mm[a] * wf[a]; o[9 + a] = mm[a] * wf[3 + a];
+  }
+}
+
 // Term-evaluation hook (h12env_eval_terms, parity tests only): the reward terms, terminations and CaT constraint
 // values of step_kernel's code on a state written into the workspace (post-physics, pre-reset; EPLEN already
 // counted) plus injected per-step quantities: applied torques, joint accelerations, and the per-body maxima over
@@ -2176,6 +2420,11 @@ int check_model(const h12env_model* m) {
       !close(m->knee_radius, h12m::KNEE_R) || !close(m->torso_com[0], h12m::TORSO_COM[0]) ||
       !close(m->torso_com[1], h12m::TORSO_COM[1]) || !close(m->torso_com[2], h12m::TORSO_COM[2]))
     return set_err(H12_E_ARG, "base / contact geometry differs from the compiled H1-2 model");
+  for (int r = 0; r < 4; ++r)
+    for (int e = 0; e < 2; ++e)
+      for (int a = 0; a < 3; ++a)
+        if (!close(m->foot_rods[r][e][a], h12m::ROD[r][e][a]))
+          return set_err(H12_E_ARG, "sole rod geometry differs from the compiled H1-2 model");
   return 0;
 }
 
@@ -2226,6 +2475,8 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.mus = c->mu_static; P.mud = c->mu_dynamic; P.lk = c->limit_k; P.lc = c->limit_c;
   P.fc_v = c->friction_c;
   P.impl = c->implicit_penalty != 0;
+  P.self_coll = c->self_collision != 0;
+  P.sk = c->self_k; P.sc = c->self_c; P.sct = c->self_ct; P.smu = c->self_mu;
   P.dl = 0.f;
   if (P.impl) {  // the springs act at the end of the substep: extra damping h k (oracle contact_point)
     P.cc = c->contact_c + P.h * c->contact_k;
@@ -2441,6 +2692,7 @@ int h12env_config_default(h12env_config* c) {
   const float vmax[6] = {23, 23, 23, 14, 9, 9};  // URDF velocity limits as the USD / PhysX hold them
   for (int j = 0; j < H12_NJ; ++j) c->max_joint_vel[j] = vmax[j % 6];
   c->max_joint_vel_damping = 1.0e3f;
+  c->self_collision = 1; c->self_k = 3e4f; c->self_c = 50.f; c->self_ct = 50.f; c->self_mu = 0.36f;
   c->contact_k = 3e4f; c->contact_c = 100.f; c->friction_k = 3e4f; c->friction_c = 100.f;
   c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1000.f; c->limit_c = 2.f; c->contact_threshold = 1.f;
   c->cmd_resample_time = 10.f;
@@ -2729,6 +2981,16 @@ int h12env_eval_terms(h12env* hh, const float* tau, const float* jacc, const flo
   if (P.cat) P.cscr = cstr;  // the constraint rows go to the caller's buffer, not the step's scratch
   TermArgs T = {tau, jacc, fmax, terms, terminated, truncated};
   LAUNCH_K(terms_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, P, h->W, T);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_eval_self_contacts(h12env* hh, float* out, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  if (!out) return set_err(H12_E_ARG, "out is required");
+  if (!h->P.self_coll) return set_err(H12_E_STATE, "self_collision is off in this env's config");
+  LAUNCH_K(selfc_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, out);
   HIP_TRY(hipGetLastError());
   return 0;
 }

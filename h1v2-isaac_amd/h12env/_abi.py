@@ -20,7 +20,7 @@ NCSTR = 10       # CaT constraint terms (CONSTRAINT_TERMS)
 NCSTR_COLS = 56
 NLOG = 44        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare,
                  # then per constraint term the summed violation rates (10) and mean probabilities (10)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -95,6 +95,7 @@ class H12Model(C.Structure):
         ("torso_half", f32 * 3),
         ("gravity", f32),
         ("torso_com", f32 * 3),
+        ("foot_rods", f32 * 3 * 2 * 4),
     ]
 
 
@@ -188,6 +189,11 @@ class H12Config(C.Structure):
         ("implicit_penalty", i32),
         ("max_joint_vel", f32 * NJ),
         ("max_joint_vel_damping", f32),
+        ("self_collision", i32),
+        ("self_k", f32),
+        ("self_c", f32),
+        ("self_ct", f32),
+        ("self_mu", f32),
     ]
 
 
@@ -254,6 +260,8 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_field_ptr.restype = vp
     lib.h12env_eval_terms.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.h12env_eval_terms.restype = C.c_int
+    lib.h12env_eval_self_contacts.argtypes = [vp, vp, vp]
+    lib.h12env_eval_self_contacts.restype = C.c_int
     lib.h12env_num_envs.argtypes = [vp]
     lib.h12env_num_envs.restype = C.c_int
     lib.h12env_obs_dim.argtypes = [vp]
@@ -297,5 +305,5 @@ EXPORTED_SYMBOLS = [
     "h12env_step", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
-    "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms",
+    "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms", "h12env_eval_self_contacts",
 ]

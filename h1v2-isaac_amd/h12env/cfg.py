@@ -38,6 +38,14 @@ class SimCfg:
     # here: a stiff joint damper above the limit, integrated implicitly
     joint_velocity_limit: bool = True
     joint_velocity_limit_damping: float = 1.0e3
+    # self-collision between the legs (h12.py:32 enabled_self_collisions=True): knee and sole-rod capsules,
+    # explicit penalty: the ground contact's stiffness, damping below the explicit
+    # stability bound c h / m_eff < 2 of the lightest contact DOF (toe about the ankle pitch, ~0.35 kg)
+    self_collision: bool = True
+    self_k: float = 3.0e4
+    self_c: float = 50.0
+    self_ct: float = 50.0
+    self_mu: float = 0.36
     contact_k: float = 3.0e4
     contact_c: float = 100.0
     friction_k: float = 3.0e4
@@ -499,6 +507,9 @@ class H12FlatEnvCfg:
         if self.mode == MODE_ISAACLAB and self.sim.joint_velocity_limit:
             c.max_joint_vel[:] = self.robot.joint_vel_limits
             c.max_joint_vel_damping = self.sim.joint_velocity_limit_damping
+        c.self_collision = int(self.sim.self_collision and self.mode == MODE_ISAACLAB)
+        c.self_k, c.self_c = self.sim.self_k, self.sim.self_c
+        c.self_ct, c.self_mu = self.sim.self_ct, self.sim.self_mu
         c.max_episode_length = self.max_episode_length
         c.action_scale = self.actions.joint_pos.scale
         import re

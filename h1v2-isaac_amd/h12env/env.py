@@ -530,6 +530,14 @@ class H12VelocityEnv:
             None if cstr is None else C.c_void_p(cstr.data_ptr()), self._stream()), "h12env_eval_terms")
         return terms, term.bool(), trunc.bool(), cstr
 
+    def eval_self_contacts(self) -> torch.Tensor:
+        """Parity hook (h12env_eval_self_contacts): the self-contact wrenches between the legs on the workspace
+        state as it stands, (N, 2 legs, 2 bodies [knee, foot], 6 [moment, force]) in body coordinates."""
+        out = torch.zeros(self.num_envs, 2, 2, 6, device=self.device)
+        check(self._lib, self._lib.h12env_eval_self_contacts(self._h, C.c_void_p(out.data_ptr()), self._stream()),
+              "h12env_eval_self_contacts")
+        return out
+
     def observe(self, fill_mask: torch.Tensor | None = None):
         """ObservationManager.compute(): append a frame of the current state to the history."""
         prev = self._obs[self._k]

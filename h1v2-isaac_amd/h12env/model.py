@@ -63,6 +63,10 @@ def build_model() -> H12Model:
         m.torso_half[a] = d["torso_box"]["half"][a]
         m.torso_com[a] = d["torso_link"]["com"][a]
     m.knee_radius = d["knee"]["radius"]
+    for r, seg in enumerate(d["foot"]["rods"]):
+        for e in range(2):
+            for a in range(3):
+                m.foot_rods[r][e][a] = seg[e][a]
     m.gravity = d["gravity"]
     assert len(d["joints"]) == NJ
     return m

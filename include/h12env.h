@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 5
+#define H12ENV_ABI_VERSION 6
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -147,6 +147,9 @@ typedef struct h12env_model {
   float gravity;                 /* 9.81 */
   float torso_com[3];            /* torso_link COM in base frame (h12_12dof.xml:144): where the
                                     randomize_rigid_body_mass event adds mass (cat_env_cfg.py:240-249) */
+  /* ABI 6: the four sole rods (URDF cylinders r = foot_radius, h12_12dof.urdf:168-191) as segments in the
+   * ankle-roll frame: heel, toe, two side rods (self-collision capsules) */
+  float foot_rods[4][2][3];
 } h12env_model;
 
 /* Task / simulation configuration. h12env_config_default() fills the Flat-H12_12dof values. */
@@ -235,6 +238,15 @@ typedef struct h12env_config {
    * -max_joint_vel_damping (|qd| - max) sign(qd), integrated implicitly; 0 = no limit (MuJoCo mode) */
   float max_joint_vel[H12_NJ];
   float max_joint_vel_damping; /* [N m s / rad]; C1 ramp-in over the first H12_VLIM_RAMP of excess (see below) */
+  /* ABI 6: self-collision between the two legs (ArticulationCfg enabled_self_collisions=True, h12.py:32):
+   * capsules of the knee cylinders (knee_p0/p1, knee_radius) and the four sole rods of each foot (foot_rods,
+   * foot_radius), every left/right pair.  Penalty law, explicit: f_n = max(0, k d - c v_n) along the
+   * closest-point normal, viscous friction -c_t v_t capped at mu f_n, applied equal and opposite at the
+   * midpoint of the closest points; reported into the bodies' net contact forces (ContactSensor: foot timers,
+   * illegal knee contact). */
+  int32_t self_collision;
+  float self_k, self_c;        /* normal stiffness [N/m], damping [N s/m] */
+  float self_ct, self_mu;      /* tangential damping [N s/m], Coulomb cap (0.6 x 0.6, material multiply) */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */
@@ -326,6 +338,12 @@ int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* str
  * (velocity/mdp/rewards.py, utils/cat/constraints.py) for the reference-fixture tests. */
 int h12env_eval_terms(h12env* h, const float* tau, const float* jacc, const float* fmax, float* terms,
                       uint8_t* terminated, uint8_t* truncated, float* cstr, void* stream);
+
+/* Parity hook (tests only): the self-contact wrenches between the legs (h12env_config.self_collision) that the
+ * physics step applies on the workspace state as it stands; out (device, n x 2 x 2 x 6): per env, leg (left,
+ * right), body (knee, foot): moment xyz, force xyz in body coordinates.  Replaces nothing in the reference (its
+ * self-collisions live inside PhysX, ArticulationCfg enabled_self_collisions, A/robots/h12.py:32). */
+int h12env_eval_self_contacts(h12env* env, float* out, void* stream);
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);

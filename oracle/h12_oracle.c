@@ -89,6 +89,8 @@ int orc_dz_count(void) { return g_dz_count; }
 
 /* ------------------------------------------------------------------ small linear algebra */
 typedef double m3[3][3];
+static double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 static void cross3(const double a[3], const double b[3], double o[3]) {
   double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
   o[0] = t0; o[1] = t1; o[2] = t2;
@@ -365,6 +367,116 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   return 1;
 }
 
+/* ---- self-collision between the legs (ArticulationCfg enabled_self_collisions=True, A/robots/h12.py:32).
+ * Colliders of the URDF the IsaacLab USD was converted from: the knee cylinders (h12_12dof.urdf:116,286) and
+ * the four sole rods of each foot (:168-191, :338-361), as capsules (segment + radius).  PhysX filters
+ * jointed parent/child pairs; within one leg no knee/foot pair can touch (shank 0.4 m), so every left/right
+ * pair is tested.  Generic restatement (world frame, every pair, fp64); the kernel mirrors it per lane pair. */
+
+/* closest points of segments p1-q1 and p2-q2 (the standard clamped-parameter construction); nearly parallel
+ * segments (sin^2 of the angle < 1e-3, ~1.8 deg) take the middle of their overlap along the first segment: a line
+ * contact's centre, and well-conditioned in fp32 (den = |d1|^2 |d2|^2 sin^2 loses ~log10(1/sin^2) digits
+ * to cancellation; the parallel side rods of two feet side by side sit right there) */
+static void seg_closest(const double p1[3], const double q1[3], const double p2[3], const double q2[3], double c1[3],
+                        double c2[3]) {
+  double d1[3], d2[3], r[3];
+  for (int a = 0; a < 3; ++a) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
+  const double A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
+  const double den = A * E - B * B;
+  double s;
+  if (den > 1e-3 * A * E) {
+    s = clampd((B * F - C * E) / den, 0.0, 1.0);
+  } else {
+    const double t0 = -C / A, t1 = (B - C) / A;
+    const double lo = fmax(0.0, fmin(t0, t1)), hi = fmin(1.0, fmax(t0, t1));
+    s = clampd(0.5 * (lo + hi), 0.0, 1.0);
+  }
+  double t = (B * s + F) / E;
+  if (t < 0.0) { t = 0.0; s = clampd(-C / A, 0.0, 1.0); }
+  else if (t > 1.0) { t = 1.0; s = clampd((B - C) / A, 0.0, 1.0); }
+  for (int a = 0; a < 3; ++a) { c1[a] = p1[a] + d1[a] * s; c2[a] = p2[a] + d2[a] * t; }
+}
+
+typedef struct capsule_w {
+  int b;               /* body */
+  double p0[3], p1[3]; /* world segment */
+  double r;
+} capsule_w;
+
+static void capsule_world(const kin_t* k, int b, const float* p0, const float* p1, double r, capsule_w* out) {
+  double a0[3] = {p0[0], p0[1], p0[2]}, a1[3] = {p1[0], p1[1], p1[2]};
+  out->b = b;
+  out->r = r;
+  m3v(k->R[b], a0, out->p0);
+  m3v(k->R[b], a1, out->p1);
+  for (int a = 0; a < 3; ++a) { out->p0[a] += k->p[b][a]; out->p1[a] += k->p[b][a]; }
+}
+
+/* world velocity of the body-b material point at world x */
+static void point_vel(const kin_t* k, int b, const double x[3], double v[3]) {
+  double w[3], vo[3], rx[3], wr[3];
+  m3v(k->R[b], k->v[b], w);
+  m3v(k->R[b], k->v[b] + 3, vo);
+  for (int a = 0; a < 3; ++a) rx[a] = x[a] - k->p[b][a];
+  cross3(w, rx, wr);
+  for (int a = 0; a < 3; ++a) v[a] = vo[a] + wr[a];
+}
+
+/* world force F at world point x on body b -> body-coordinate spatial force */
+static void apply_world_force(const kin_t* k, int b, const double x[3], const double F[3], double fext[NB][6]) {
+  double rx[3], xb[3], fb[3], nb[3];
+  for (int a = 0; a < 3; ++a) rx[a] = x[a] - k->p[b][a];
+  m3tv(k->R[b], rx, xb);
+  m3tv(k->R[b], F, fb);
+  cross3(xb, fb, nb);
+  for (int a = 0; a < 3; ++a) { fext[b][a] += nb[a]; fext[b][3 + a] += fb[a]; }
+}
+
+static void self_contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, double fext[NB][6],
+                          orc_contact_report* rr) {
+  capsule_w cap[2][5]; /* per leg: knee, then the four sole rods */
+  for (int f = 0; f < 2; ++f) {
+    capsule_world(k, 6 * f + 4, m->knee_p0, m->knee_p1, m->knee_radius, &cap[f][0]);
+    for (int r = 0; r < 4; ++r) {
+      float p0[3], p1[3];
+      for (int a = 0; a < 3; ++a) {
+        /* the right foot's rods are the mirror images (y -> -y) of the left foot's */
+        const double sy = (f == 1 && a == 1) ? -1.0 : 1.0;
+        p0[a] = (float)(sy * m->foot_rods[r][0][a]);
+        p1[a] = (float)(sy * m->foot_rods[r][1][a]);
+      }
+      capsule_world(k, 6 * f + 6, p0, p1, m->foot_radius, &cap[f][1 + r]);
+    }
+  }
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) {
+      const capsule_w *A = &cap[0][i], *Bc = &cap[1][j];
+      double cA[3], cB[3];
+      seg_closest(A->p0, A->p1, Bc->p0, Bc->p1, cA, cB);
+      double dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
+      const double d = sqrt(dot3(dv, dv)), depth = A->r + Bc->r - d;
+      if (!(depth > 0.0) || d < 1e-9) continue;
+      double n[3], x[3], va[3], vb[3], vr[3];
+      for (int a = 0; a < 3; ++a) { n[a] = dv[a] / d; x[a] = 0.5 * (cA[a] + cB[a]); }
+      point_vel(k, A->b, x, va);
+      point_vel(k, Bc->b, x, vb);
+      for (int a = 0; a < 3; ++a) vr[a] = va[a] - vb[a];
+      const double vn = dot3(vr, n), fn = c->self_k * depth - c->self_c * vn;
+      if (!(fn > 0.0)) continue;
+      double ft[3];
+      for (int a = 0; a < 3; ++a) ft[a] = -c->self_ct * (vr[a] - vn * n[a]);
+      const double ftn = sqrt(dot3(ft, ft)), cap_t = c->self_mu * fn;
+      if (ftn > cap_t) for (int a = 0; a < 3; ++a) ft[a] *= cap_t / ftn;
+      double F[3], Fm[3];
+      for (int a = 0; a < 3; ++a) { F[a] = fn * n[a] + ft[a]; Fm[a] = -F[a]; }
+      apply_world_force(k, A->b, x, F, fext);
+      apply_world_force(k, Bc->b, x, Fm, fext);
+      double* ra = i == 0 ? rr->knee_force[0] : rr->foot_force[0];
+      double* rb = j == 0 ? rr->knee_force[1] : rr->foot_force[1];
+      for (int a = 0; a < 3; ++a) { ra[a] += F[a]; rb[a] -= F[a]; }
+    }
+}
+
 /* evaluates every contact primitive; s->anchor/cmask are read, next_anchor/next_mask written */
 static void contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
                      double fext[NB][6], orc_contact_report* rep, double next_anchor[2][H12_NFOOT_PTS][2],
@@ -402,6 +514,7 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
   }
   contact_point(c, k, 0, corner, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic, hi, Madd,
                 m->gravity, rec);
+  if (c->self_collision) self_contacts(m, c, k, fext, rr);
   if (next_mask) *next_mask = mask;
 }
 
@@ -657,6 +770,30 @@ static int forward_dynamics(const h12env_model* m, const h12env_config* c, const
 int orc_forward_dynamics(const h12env_model* m, const h12env_config* c, const orc_phys* s, const double tau[NJ],
                          int algo, double dt_impl, int with_contact, double nudot[18], orc_contact_report* rep) {
   return forward_dynamics(m, c, s, tau, algo, dt_impl, NULL, with_contact, nudot, rep, 0, 0);
+}
+
+/* the self-contact wrenches alone (body-coordinate spatial forces, NB x 6) and their report, for tests */
+int orc_self_contacts(const h12env_model* m, const h12env_config* c, const orc_phys* s, double* fext,
+                      orc_contact_report* rep) {
+  kin_t k;
+  kinematics(m, s, &k);
+  memset(fext, 0, sizeof(double) * NB * 6);
+  memset(rep, 0, sizeof *rep);
+  self_contacts(m, c, &k, (double(*)[6])fext, rep);
+  return 0;
+}
+
+/* world pose (R row-major, p) of every body, for tests */
+int orc_body_poses(const h12env_model* m, const orc_phys* s, double* R, double* p) {
+  kin_t k;
+  kinematics(m, s, &k);
+  for (int b = 0; b < NB; ++b) {
+    for (int i = 0; i < 3; ++i) {
+      p[3 * b + i] = k.p[b][i];
+      for (int j = 0; j < 3; ++j) R[9 * b + 3 * i + j] = k.R[b][i][j];
+    }
+  }
+  return 0;
 }
 
 int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy, double lin[3], double ang[3]) {

@@ -61,6 +61,9 @@ int orc_forward_dynamics(const h12env_model* m, const h12env_config* c, const or
 /* Joint-space mass matrix (18 x 18, row major, base coords (w_b, v_b)), armature included. */
 int orc_mass_matrix(const h12env_model* m, const orc_phys* s, double M[18 * 18]);
 /* Total mechanical energy (kinetic + potential), linear + angular momentum about the world origin. */
+int orc_self_contacts(const h12env_model* m, const h12env_config* c, const orc_phys* s, double* fext,
+                      orc_contact_report* rep);
+int orc_body_poses(const h12env_model* m, const orc_phys* s, double* R, double* p);
 int orc_energy_momentum(const h12env_model* m, const orc_phys* s, double* energy, double lin_mom[3],
                         double ang_mom[3]);
 /* One physics step of length c->physics_dt split into c->inner_steps, holding tau_pd;

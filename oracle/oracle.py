@@ -80,6 +80,8 @@ def lib():
         L.orc_forward_dynamics.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_double, C.c_int, dp, C.POINTER(Report)]
         L.orc_mass_matrix.argtypes = [M, C.POINTER(Phys), dp]
         L.orc_energy_momentum.argtypes = [M, C.POINTER(Phys), dp, dp, dp]
+        L.orc_self_contacts.argtypes = [M, Cf, C.POINTER(Phys), dp, C.POINTER(Report)]
+        L.orc_body_poses.argtypes = [M, C.POINTER(Phys), dp, dp]
         L.orc_physics_step.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.POINTER(Report)]
         L.orc_mujoco_rollout.argtypes = [M, Cf, C.POINTER(Phys), dp, C.c_int, C.c_int, C.c_int, dp]
         L.orc_env_reset.argtypes = [M, Cf, C.c_int, C.c_int64, vp, vp, vp, vp, C.c_uint64]
@@ -276,6 +278,24 @@ def mass_matrix(model, state):
     M = np.zeros((18, 18))
     lib().orc_mass_matrix(C.byref(model), C.byref(s), _d(M))
     return M
+
+
+def self_contacts(model, cfg, state):
+    """Self-contact wrenches between the legs (body-coordinate spatial forces, (13, 6)) and the report."""
+    s = Phys.from_numpy(state)
+    f = np.zeros(13 * 6)
+    rep = Report()
+    lib().orc_self_contacts(C.byref(model), C.byref(cfg), C.byref(s), _d(f), C.byref(rep))
+    return f.reshape(13, 6), rep
+
+
+def body_poses(model, state):
+    """World rotation (13, 3, 3) and origin (13, 3) of every body."""
+    s = Phys.from_numpy(state)
+    R = np.zeros(13 * 9)
+    p = np.zeros(13 * 3)
+    lib().orc_body_poses(C.byref(model), C.byref(s), _d(R), _d(p))
+    return R.reshape(13, 3, 3), p.reshape(13, 3)
 
 
 def energy_momentum(model, state):

@@ -167,6 +167,12 @@ def main():
     # transverse heel rod (x=-0.08, |y|<=0.038) and toe rod (x=0.17, |y|<=0.021)
     pts = sorted(pts, key=lambda p: (p[0], p[1]))
     assert len(pts) == 4
+    # every sole rod as a segment (self-collision capsules): rotated about x -> axis y, about y -> axis x
+    rod_segs = []
+    for xyz, rpy, tag, a in rods:
+        L = float(a["length"])
+        ax = np.array([0.0, 1.0, 0.0]) if abs(rpy[0]) > 1 else np.array([1.0, 0.0, 0.0])
+        rod_segs.append([(xyz - ax * L / 2).tolist(), (xyz + ax * L / 2).tolist()])
     knee = coll("left_knee_link")[0]
     knee_r = float(knee[3]["radius"])
     knee_L = float(knee[3]["length"])
@@ -189,7 +195,8 @@ def main():
         ],
         "joint_defaults": {"damping": damping, "armature": armature, "frictionloss": frictionloss},
         "keyframe_qpos": qpos0.tolist(),
-        "foot": {"body": ["left_ankle_roll_link", "right_ankle_roll_link"], "points": pts, "radius": r_foot},
+        "foot": {"body": ["left_ankle_roll_link", "right_ankle_roll_link"], "points": pts, "radius": r_foot,
+                 "rods": rod_segs},
         "knee": {"body": ["left_knee_link", "right_knee_link"],
                  "p0": (knee[0] + np.array([0, 0, knee_L / 2])).tolist(),
                  "p1": (knee[0] - np.array([0, 0, knee_L / 2])).tolist(), "radius": knee_r},
