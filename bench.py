@@ -187,7 +187,9 @@ def train_mode(args, world, rank, dev, torch, dist):
     dt = time.perf_counter() - t0
     t = torch.tensor([dt, coll, learn], device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        from h12env import distributed as D
+
+        D.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, coll, learn = (float(x) for x in t.tolist())
     steps = world * args.envs * agent.num_steps_per_env * args.iterations
     if rank == 0:
@@ -280,7 +282,9 @@ def main():
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        from h12env import distributed as D
+
+        D.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     if args.profile_only:
         if rank == 0:

@@ -48,13 +48,46 @@ def init(envs_per_rank: int, backend: str | None = None) -> Shard:
     return Shard(rank, world, local, envs_per_rank)
 
 
+def _staged() -> bool:
+    """gloo handles CPU tensors: under gloo (CPU tests, or several ranks sharing one GPU, where RCCL refuses
+    duplicate devices) device tensors go through host copies; RCCL works on the device tensors directly."""
+    return dist.get_backend() == "gloo"
+
+
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM) -> None:
+    if _staged() and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+
+
+def broadcast(t: torch.Tensor, src: int = 0) -> None:
+    if _staged() and t.is_cuda:
+        h = t.cpu()
+        dist.broadcast(h, src=src)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src=src)
+
+
+def all_gather_into_tensor(out: torch.Tensor, x: torch.Tensor) -> None:
+    if _staged() and x.is_cuda:
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, x.cpu())
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, x)
+
+
 def allgather_envs(x: torch.Tensor, shard: Shard, env_dim: int = 0) -> torch.Tensor:
     """All-gather a per-shard tensor along its env dimension (rank order = global env order)."""
     if shard.world == 1:
         return x
     xt = x.movedim(env_dim, 0).contiguous()
     out = torch.empty((shard.world * xt.shape[0], *xt.shape[1:]), dtype=xt.dtype, device=xt.device)
-    dist.all_gather_into_tensor(out, xt)
+    all_gather_into_tensor(out, xt)
     return out.movedim(0, env_dim)
 
 
@@ -72,7 +105,7 @@ def allgather_rollout(storage: dict[str, torch.Tensor], shard: Shard, env_dim: i
         parts = [storage[k].movedim(env_dim, 0).contiguous() for k in keys]
         flat = torch.cat([p.reshape(p.shape[0], -1) for p in parts], dim=1)  # (N_shard, sum features)
         g = torch.empty((shard.world * flat.shape[0], flat.shape[1]), dtype=dt, device=flat.device)
-        dist.all_gather_into_tensor(g, flat)
+        all_gather_into_tensor(g, flat)
         col = 0
         for k, p in zip(keys, parts):
             w = p[0].numel()
@@ -85,7 +118,7 @@ def max_over_ranks(value: float, device=None) -> float:
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 

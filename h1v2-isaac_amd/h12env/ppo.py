@@ -199,8 +199,8 @@ class EmpiricalNormalization(nn.Module):
                 and torch.distributed.get_world_size() > 1:
             s = torch.cat([mean_x, var_x + mean_x * mean_x]) * n   # per-rank sum and sum of squares
             cnt = torch.tensor([float(n)], device=x.device)
-            torch.distributed.all_reduce(s)
-            torch.distributed.all_reduce(cnt)
+            D.all_reduce(s)
+            D.all_reduce(cnt)
             n = int(cnt.item())
             mean_x = s[:1] / n
             var_x = s[1:] / n - mean_x * mean_x
@@ -352,6 +352,9 @@ class PPO:
         key = (tuple(obs.shape), tuple(critic_obs.shape), critic_obs is obs, obs.dtype)
         if getattr(self, "_ga", None) is None or self._ga_key != key:
             # normal (not inference) tensors throughout: the graph's RNG state is updated outside inference mode
+            # the warm-up and capture consume exploration-noise draws: the generator state is put back after
+            # them, so the replays draw the same noise sequence as the eager path (graph-safe philox offsets)
+            rng_state = torch.cuda.get_rng_state(obs.device)
             with torch.inference_mode(False), torch.no_grad():
                 self._ga_obs = torch.zeros(obs.shape, dtype=obs.dtype, device=obs.device)
                 self._ga_cobs = (self._ga_obs if critic_obs is obs else
@@ -365,6 +368,7 @@ class PPO:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._act_body()
+            torch.cuda.set_rng_state(rng_state, obs.device)
             self._ga, self._ga_key = g, key
         self._ga_obs.copy_(obs)
         if critic_obs is not obs:
@@ -408,7 +412,7 @@ class PPO:
             return
         grads = [p.grad for p in self.policy.parameters() if p.grad is not None]
         flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        D.all_reduce(flat, op=dist.ReduceOp.SUM)
         flat /= self.shard.world
         off = 0
         for g in grads:
@@ -446,7 +450,7 @@ class PPO:
                                + (old_sigma.square() + (old_mu - mu).square()) / (2.0 * sigma.square()) - 0.5, dim=-1)
                 kl_mean = kl.mean()
                 if world > 1:
-                    dist.all_reduce(kl_mean, op=dist.ReduceOp.SUM)
+                    D.all_reduce(kl_mean, op=dist.ReduceOp.SUM)
                     kl_mean /= world
                 if self._lr_t is not None:
                     # rsl_rl's schedule on the device tensor the fused optimizer reads
@@ -585,7 +589,7 @@ class PPO:
     def broadcast_parameters(self):
         if self.shard.world > 1:
             for p in self.policy.state_dict().values():
-                dist.broadcast(p, src=0)
+                D.broadcast(p, src=0)
 
 
 # ---------------------------------------------------------------------------------------------- runner

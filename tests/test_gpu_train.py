@@ -120,3 +120,40 @@ def test_graph_captured_update_equals_eager(gpu, monkeypatch):
     for p, q in zip(a.policy.parameters(), b.policy.parameters()):
         assert torch.equal(p, q), (p - q).abs().max()
     assert la == lb and a.learning_rate == b.learning_rate
+
+
+@pytest.mark.timeout(400)
+def test_c3_ppo_iteration_at_4096_envs_graph_equals_eager(gpu, monkeypatch):
+    """BASELINE config C3 at its size: one PPO iteration of the runner (24 steps x 4096 envs, 5 epochs x 4
+    minibatches) on the Flat task.  The HIP-graph collection (actor / critic forward, Gaussian sample and
+    log-probability in one replay) and the graph-captured update must give the eager path's rollout and
+    parameters, and everything must stay finite."""
+    from biped_tasks.tasks.agents import H12_12dof_FlatPPORunnerCfg
+    from h12env import H12FlatEnvCfg
+    from h12env.env import H12VelocityEnv
+    from h12env.ppo import OnPolicyRunner
+    from isaaclab_rl.rsl_rl import RslRlVecEnvWrapper
+
+    def run(graph: bool):
+        monkeypatch.setenv("H12_PPO_GRAPH", "1" if graph else "0")
+        cfg = H12FlatEnvCfg()
+        cfg.scene.num_envs = 4096
+        cfg.sim.device = "cuda:0"
+        env = H12VelocityEnv(cfg)
+        agent = H12_12dof_FlatPPORunnerCfg()
+        runner = OnPolicyRunner(RslRlVecEnvWrapper(env), agent.to_dict(), log_dir=None, device="cuda:0")
+        runner.learn(1, init_at_random_ep_len=True)
+        st = {k: v.clone() for k, v in runner.alg.storage.t.items()}
+        params = torch.cat([p.detach().reshape(-1) for p in runner.alg.policy.parameters()])
+        env.close()
+        return st, params
+
+    sg, pg = run(True)
+    se, pe = run(False)
+    for k in ("observations", "actions", "rewards", "dones", "values", "actions_log_prob", "mu", "sigma"):
+        if k in sg:
+            assert torch.isfinite(sg[k].float()).all(), k
+            assert torch.equal(sg[k], se[k]), (k, (sg[k].float() - se[k].float()).abs().max())
+    assert sg["dones"].any()
+    assert torch.isfinite(pg).all()
+    assert torch.equal(pg, pe), (pg - pe).abs().max()
