@@ -67,6 +67,7 @@ def parse():
     p.add_argument("--inner-steps", type=int, default=None, help="experiment override (not the metric config)")
     p.add_argument("--explicit-penalty", action="store_true",
                    help="experiment: round-1 explicit penalty contact (use with --inner-steps 2)")
+    p.add_argument("--no-self-collision", action="store_true", help="experiment: legs do not collide (not the metric)")
     return p.parse_args()
 
 
@@ -256,6 +257,8 @@ def main():
         cfg.sim.inner_steps = args.inner_steps
     if args.explicit_penalty:
         cfg.sim.implicit_penalty = False
+    if args.no_self_collision:
+        cfg.sim.self_collision = False
     env = H12VelocityEnv(cfg, env_offset=rank * n)
     env.reset()
     g = torch.Generator(device=dev).manual_seed(1234 + rank)

@@ -772,6 +772,12 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
   const int flags = mine | pair_swap_i(mine);
   const uint64_t act = __ballot(flags != 0 && leg == 0);
   if (act == 0) return;  // wave-uniform: no candidate pair anywhere in the wave
+#ifdef H12_SELF_BROAD_ONLY  // experiment builds only: price the broad phase alone
+  if (act != 0) return;
+#endif
+#ifdef H12_SELF_NARROW_DEAD  // experiment builds only: narrow phase compiled in but never run (register cost)
+  if (P.mode != 12345) return;
+#endif
   // ---- stage this leg's capsules and body kinematics (real frame)
   const int el = threadIdx.x >> 1;
   {
