@@ -1559,6 +1559,16 @@ H12_DEV float noise_of(const KParams& P, int t, uint32_t r) {
 // stored with one float4 store.  All global reads precede the first barrier, so obs may alias obs_prev.
 // Reset mode: rows with sel[e] (all if sel is NULL) are filled, the others are rewritten unchanged
 // from obs itself.  Otherwise fill[e] = fill_a[e] | fill_b[e].
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (blocks b and b + 8 share one
+// XCD and its L2; MI355X_MICROARCH.md, workgroup dispatch), so consecutive logical blocks -- which share cache
+// lines of the [45][n] frame scratch (a 128-B line holds 32 envs' component = 8 blocks of 4 rows) and the row
+// boundaries -- are mapped to one XCD: logical block = (b % 8) * q + min(b % 8, r) + b / 8 with nb = 8 q + r.
+// Affinity only (placement is not a contract); a bijection on [0, nb).
+H12_DEV int xcd_block(int b, int nb) {
+  const int x = b & 7, k = b >> 3, q = nb >> 3, r = nb & 7;
+  return x * q + min(x, r) + k;
+}
+
 struct AsmArgs {
   const float* obs_prev;
   float* obs;
@@ -1628,7 +1638,7 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
   __shared__ int s_write[ASM_ROWS], s_fill[ASM_ROWS];
   const int n = A.n;
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * ASM_ROWS;
+  const int r0 = xcd_block(blockIdx.x, gridDim.x) * ASM_ROWS;
   const int rows = min(ASM_ROWS, n - r0);
   const bool full = A.vec && rows == ASM_ROWS;
   const size_t base = (size_t)r0 * ROW;
