@@ -742,6 +742,15 @@ struct SelfLds {
   int slot[ENVS_PER_BLOCK], flags[ENVS_PER_BLOCK];
 };
 
+// LDS hand-off among the lanes of ONE wave (the compiler's lowering of a one-wave block's __syncthreads without
+// the s_barrier): self_contacts runs inside a wave that may share its block with another wave (step_kernel's
+// helper wave), so it must not wait at a workgroup barrier.
+H12_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
 // added to the reported knee / foot contact forces.  Rk/pk, vk: knee pose (lane frame) and body velocity,
 // Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP swap; wave-uniform at every barrier.
@@ -779,7 +788,7 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
   if (P.mode != 12345) return;
 #endif
   // ---- stage this leg's capsules and body kinematics (real frame)
-  const int el = threadIdx.x >> 1;
+  const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
   {
     float4* g = L.geo[el][leg];
     g[SG_KNEE] = make_float4(k0[0], k0[1], k0[2], 0.f);
@@ -810,7 +819,7 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
       L.flags[rank] = flags;
     }
   }
-  __syncthreads();
+  wave_sync();
   // ---- pair jobs of the candidate envs over the wave's live lanes (a ragged last block has fewer):
   // job = (env rank, left capsule i, right capsule j)
   const uint64_t live = __ballot(1);
@@ -860,7 +869,7 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
       atomicAdd(&ar[a], -F[a]); atomicAdd(&ar[4 + a], -m[a]);
     }
   }
-  __syncthreads();
+  wave_sync();
   // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
   const float ms[3] = {1.f, sg, 1.f};
   auto own_body = [&](const float* ac, const float* po, const float (&Rb)[3][3], float* w, float* rep) {
@@ -876,12 +885,66 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
   };
   own_body(L.acc[el][leg][0], pk, Rk, wk, fr.knee);
   own_body(L.acc[el][leg][1], pf, Rf, wf, fr.foot);
-  __syncthreads();  // the staging area is rewritten by the next physics step
+  wave_sync();  // the staging area is rewritten by the next physics step
+}
+
+// ---- self-contact helper wave (step_kernel with self-collision: a second wave per block).  The self-contact
+// wrenches are explicit and enter the ABA only at pass 2, so the block's second wave computes them
+// (self_contacts, the same code as the in-wave path) while the physics wave evaluates the sole contacts and the
+// joint torques.  Per inner step: the physics wave writes its knee / foot kinematics, barrier, the helper computes
+// and writes the two wrenches, barrier, the physics wave reads them.
+struct SelfHand {
+  float4 kin[9][BLOCK];  // per physics lane: knee R (9), p (3), v (6); foot R (9), p (3), v (6)
+  float4 res[3][BLOCK];  // per physics lane: knee wrench (6), foot wrench (6)
+};
+H12_DEV SelfHand& self_hand() {
+  __shared__ SelfHand H;
+  return H;
+}
+H12_DEV void hand_put(int l, const float (&Rk)[3][3], const float* pk, const float* vk, const float (&Rf)[3][3],
+                      const float* pf, const float* vf) {
+  float k[36];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) { k[3 * i + j] = Rk[i][j]; k[18 + 3 * i + j] = Rf[i][j]; }
+  for (int i = 0; i < 3; ++i) { k[9 + i] = pk[i]; k[27 + i] = pf[i]; }
+  for (int i = 0; i < 6; ++i) { k[12 + i] = vk[i]; k[30 + i] = vf[i]; }
+  SelfHand& H = self_hand();
+#pragma unroll
+  for (int c = 0; c < 9; ++c) H.kin[c][l] = make_float4(k[4 * c], k[4 * c + 1], k[4 * c + 2], k[4 * c + 3]);
+}
+template <int K>
+H12_DEV void self_helper(const KParams& P, int n, int n_steps) {
+  const int l = threadIdx.x - BLOCK;
+  const int leg = l & 1;
+  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
+  SelfHand& H = self_hand();
+  for (int it = 0; it < n_steps; ++it) {
+    __syncthreads();  // kinematics written
+    if (active) {
+      float k[36];
+#pragma unroll
+      for (int c = 0; c < 9; ++c) {
+        const float4 x = H.kin[c][l];
+        k[4 * c] = x.x; k[4 * c + 1] = x.y; k[4 * c + 2] = x.z; k[4 * c + 3] = x.w;
+      }
+      float Rk[3][3], Rf[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { Rk[i][j] = k[3 * i + j]; Rf[i][j] = k[18 + 3 * i + j]; }
+      float wk[6], wf[6];
+      Forces fr = {};
+      self_contacts(P, leg, Rk, k + 9, k + 12, Rf, k + 27, k + 30, wk, wf, fr);
+      H.res[0][l] = make_float4(wk[0], wk[1], wk[2], wk[3]);
+      H.res[1][l] = make_float4(wk[4], wk[5], wf[0], wf[1]);
+      H.res[2][l] = make_float4(wf[2], wf[3], wf[4], wf[5]);
+    }
+    __syncthreads();  // wrenches written
+  }
 }
 
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
-// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.
-template <int K>
+// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.  HW: the block has a self-contact
+// helper wave (step_kernel; used when P.self_coll), else the self-contacts are evaluated in this wave.
+template <int K, bool HW>
 H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
                         const float* org) {
   const float sg = leg ? -1.f : 1.f;
@@ -930,9 +993,14 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   // self-contacts between the legs: explicit wrenches on the knee (-> fext_knee) and the foot (-> pAcc below)
   float wsf[6];
   if (P.self_coll) {
-    float wsk[6];
-    self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wsk, wsf, fr);
-    for (int i = 0; i < 6; ++i) fext_knee[i] += wsk[i];
+    if constexpr (HW) {
+      hand_put(threadIdx.x, Rk, pk, v[3], R, p, v[5]);
+      __syncthreads();  // the helper wave computes the wrenches while this wave continues
+    } else {
+      float wsk[6];
+      self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wsk, wsf, fr);
+      for (int i = 0; i < 6; ++i) fext_knee[i] += wsk[i];
+    }
   }
   // ---- foot: 4 anchored sole spheres on the ankle-roll link; starts pass 2 of link 5
   int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
@@ -942,7 +1010,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float pAcc[6];
   bias<5>(v[5], pAcc);
   SoleSums ss;
-  if (P.self_coll)
+  if (!HW && P.self_coll)
     for (int i = 0; i < 6; ++i) pAcc[i] -= wsf[i];
   if constexpr (!Feat<K>::terrain) {
     sole_contacts_flat(P, R, p, v[5], lg, IA, pAcc, fr.foot, ss);
@@ -988,6 +1056,14 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     t -= P.dimpl[k] * qd;
     if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
     tau[k] = t;
+  }
+  if (HW && P.self_coll) {
+    __syncthreads();  // the helper's wrenches are in LDS
+    const SelfHand& H = self_hand();
+    const float4 r0 = H.res[0][threadIdx.x], r1 = H.res[1][threadIdx.x], r2 = H.res[2][threadIdx.x];
+    const float wk[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wf[6] = {r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
+    for (int i = 0; i < 6; ++i) { fext_knee[i] += wk[i]; pAcc[i] -= wf[i]; }
+    for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
   }
   // ---- pass 2 (leaf -> root)
   float U[NL][6], Dinv[NL], u[NL];
@@ -1940,7 +2016,11 @@ struct StepArgs {
 };
 
 template <int K>
-__global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+__global__ void __launch_bounds__(2 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  if (threadIdx.x >= BLOCK) {  // the self-contact helper wave (launched only with P.self_coll)
+    if (P.self_coll) self_helper<K>(P, W.n, P.decimation * P.inner);
+    return;
+  }
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
@@ -1994,7 +2074,7 @@ __global__ void __launch_bounds__(BLOCK) step_kernel(KParams P, Workspace W, Ste
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
-      for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
+      for (int it = 0; it < P.inner; ++it) inner_step<K, true>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
       // ContactSensor: net force = mean over the inner steps of the physics step
@@ -2365,7 +2445,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step<K>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
+    for (int it = 0; it < P.inner; ++it) inner_step<K, false>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
   }
   store_env<K>(P, W, e, leg, s);
 }
@@ -2936,7 +3016,9 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.dz_slot = (int)(h->dz_step++ % 3);
   hipEvent_t t0, t1;
   timing_events(h, 0, &t0, &t1);
-  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
+  // with self-collision each block carries a second (helper) wave, see self_helper
+  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3(h->P.self_coll ? 2 * BLOCK : BLOCK), 0, (hipStream_t)stream,
+            h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (h->P.cat) {
     const dim3 cg((h->W.n + CAT_CHUNK - 1) / CAT_CHUNK, H12_NCSTR_COLS);

@@ -403,6 +403,24 @@ typedef struct capsule_w {
   double r;
 } capsule_w;
 
+/* Test hook (tests/helpers/forced.py only): jitter every capsule end point of the self-contacts by an independent
+ * uniform +-eps (m) per coordinate -- the GPU rounds each rod end it computes independently (fp32, ~1e-7 m at
+ * the env's ~1 m scale), a perturbation that no perturbation of the joint state reproduces.  eps = 0 (the
+ * default) is the exact model.  Single-env re-runs only (the draw sequence is global, not thread-safe). */
+static double g_sj_eps = 0.0;
+static uint64_t g_sj_state = 0;
+void orc_set_self_jitter(double eps, uint64_t seed) {
+  g_sj_eps = eps;
+  g_sj_state = seed;
+}
+static double sj_draw(void) { /* splitmix64 -> uniform [-1, 1) */
+  uint64_t z = (g_sj_state += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
 static void capsule_world(const kin_t* k, int b, const float* p0, const float* p1, double r, capsule_w* out) {
   double a0[3] = {p0[0], p0[1], p0[2]}, a1[3] = {p1[0], p1[1], p1[2]};
   out->b = b;
@@ -410,6 +428,8 @@ static void capsule_world(const kin_t* k, int b, const float* p0, const float* p
   m3v(k->R[b], a0, out->p0);
   m3v(k->R[b], a1, out->p1);
   for (int a = 0; a < 3; ++a) { out->p0[a] += k->p[b][a]; out->p1[a] += k->p[b][a]; }
+  if (g_sj_eps > 0.0)
+    for (int a = 0; a < 3; ++a) { out->p0[a] += g_sj_eps * sj_draw(); out->p1[a] += g_sj_eps * sj_draw(); }
 }
 
 /* world velocity of the body-b material point at world x */

@@ -153,6 +153,8 @@ int orc_obs_dim(const h12env_config* c);
 /* Deadzone command count carried from one orc_env_step to the next (the kernel's rotating counter);
  * process-global like the terrain. */
 void orc_set_dz_count(int v);
+/* test hook: jitter of the self-contact capsule end points (m), see h12_oracle.c capsule_world */
+void orc_set_self_jitter(double eps, uint64_t seed);
 int orc_dz_count(void);
 
 /* RNG shared by both sides (Philox4x32-10). */

@@ -111,6 +111,8 @@ def lib():
         L.orc_set_dz_count.restype = None
         L.orc_dz_count.argtypes = []
         L.orc_dz_count.restype = C.c_int
+        L.orc_set_self_jitter.argtypes = [C.c_double, C.c_uint64]
+        L.orc_set_self_jitter.restype = None
         Tp = C.POINTER(TermIn)
         L.orc_mdp_terms.argtypes = [M, Cf, Tp, dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_mdp_terms.restype = C.c_int
@@ -365,6 +367,11 @@ def cat_last_constraints(n: int) -> np.ndarray:
 
 def dz_count() -> int:
     return int(lib().orc_dz_count())
+
+
+def set_self_jitter(eps: float, seed: int = 0):
+    """Test hook: jitter every self-contact capsule end point by uniform +-eps m per coordinate (0 = exact)."""
+    lib().orc_set_self_jitter(float(eps), int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
 def ground(cfg, x, y):

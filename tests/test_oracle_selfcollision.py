@@ -135,3 +135,23 @@ def test_random_action_rollout_finite_and_knee_contacts_terminate(model):
         out[sc] = term
     # knee self-contacts are illegal contacts: more falls are declared with the model
     assert out[True] > out[False]
+
+
+def test_self_jitter_hook(model):
+    """The forced-parity harness's capsule jitter (oracle set_self_jitter): off by default and after reset to 0
+    (bit-identical wrenches), and a 1e-6 m jitter moves a penetrating pair's force by about k * 1e-6 m."""
+    c = H12FlatEnvCfg().to_c()
+    s = crossed_state(model, -0.25)
+    # a generic crossing (the symmetric state itself has exactly intersecting rod axes: no contact normal)
+    s[13:25] += np.random.default_rng(3).normal(size=12) * 0.05
+    f0, _ = O.self_contacts(model, c, s)
+    assert np.abs(f0).max() > 0
+    try:
+        O.set_self_jitter(1e-6, 7)
+        f1, _ = O.self_contacts(model, c, s)
+    finally:
+        O.set_self_jitter(0.0)
+    f2, _ = O.self_contacts(model, c, s)
+    np.testing.assert_array_equal(f2, f0)
+    d = np.abs(f1 - f0).max()
+    assert 0.0 < d < 10 * c.self_k * 1e-6
