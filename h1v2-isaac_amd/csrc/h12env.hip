@@ -63,9 +63,19 @@ __device__ unsigned long long g_phase[16];
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _ph_t);                \
     _ph_t = _t;                                                                     \
   } while (0)
+// inside inner_step (its own clock mark): slots 10.. split the inner step around the helper hand-off
+#define PHX_INIT() unsigned long long _phx_t = __builtin_readcyclecounter()
+#define PHX(i)                                                                      \
+  do {                                                                              \
+    unsigned long long _t = __builtin_readcyclecounter();                           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _phx_t);               \
+    _phx_t = _t;                                                                    \
+  } while (0)
 #else
 #define PH_INIT() (void)0
 #define PH(i) (void)0
+#define PHX_INIT() (void)0
+#define PHX(i) (void)0
 #endif
 
 thread_local char g_err[512] = "";
@@ -469,23 +479,26 @@ H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, floa
   rmul_axis<A>(R, c, s);
 }
 
-// ---- ABA pass 2 for leg link LINK (leaf -> root).  On entry IA / pAcc are the articulated inertia /
-// bias force of LINK in its own frame; on exit those of the parent (rigid part and bias included;
-// for LINK == 0 the leg's contribution to the base, at the base origin).
+// ---- ABA pass 2 for leg link LINK (leaf -> root), split in two chains: the articulated-inertia chain
+// (link_ia: depends on the joint angles, the link velocities and the implicit contact / limit inertias only) and
+// the bias-force chain (link_p: linear in the applied forces).  The split lets the forces of the step --
+// actuator + limit torques, rigid-body bias forces, self-contact wrenches -- arrive after the inertia chain
+// (step_kernel computes them in the block's helper wave meanwhile).
+// link_ia: on entry IA is the articulated inertia of LINK in its own frame; on exit that of the parent (rigid part
+// included; for LINK == 0 the leg's contribution to the base, at the base origin).  Keeps U, 1/D and
+// Ic = Ia c (c = the velocity-product acceleration) for link_p and pass 3.
 template <int LINK>
-H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
-                        const float* fext_knee, const ImplC& ick, float knee_pz, const float* tau, const float* dl,
-                        AInertia& IA, float* pAcc, float (&U)[NL][6], float (&Dinv)[NL], float (&u)[NL], float h) {
+H12_DEV void link_ia(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
+                     const ImplC& ick, float knee_pz, const float* dl, AInertia& IA, float (&U)[NL][6],
+                     float (&Dinv)[NL], float (&Ic)[NL][6], float h) {
   constexpr int A = AX[LINK];
   float Ua[3] = {sget(IA.A, 0, A), sget(IA.A, 1, A), sget(IA.A, 2, A)};
   float Ul[3] = {IA.B[A][0], IA.B[A][1], IA.B[A][2]};
   float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK] + dl[LINK];
   float di = frcp(D);
-  float uu = tau[LINK] - pAcc[A];
   U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
   U[LINK][3] = Ul[0]; U[LINK][4] = Ul[1]; U[LINK][5] = Ul[2];
   Dinv[LINK] = di;
-  u[LINK] = uu;
   // Ia = IA - U U^T / D
   float Uad[3] = {Ua[0] * di, Ua[1] * di, Ua[2] * di};
   float Uld[3] = {Ul[0] * di, Ul[1] * di, Ul[2] * di};
@@ -495,21 +508,37 @@ H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2
   IA.C[3] -= Ul[0] * Uld[1]; IA.C[4] -= Ul[0] * Uld[2]; IA.C[5] -= Ul[1] * Uld[2];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * Uld[j];
-  // pa = pA + Ia c + U u / D
-  float cb[6], Ic[6];
+  float cb[6];
   vprod<A>(v[LINK], lg.qd[LINK], cb);
-  ai_mul(IA, cb, Ic);
-  float ud = uu * di;
-  float pa[6];
-  for (int i = 0; i < 3; ++i) {
-    pa[i] = pAcc[i] + Ic[i] + Ua[i] * ud;
-    pa[3 + i] = pAcc[3 + i] + Ic[3 + i] + Ul[i] * ud;
-  }
+  ai_mul(IA, cb, Ic[LINK]);
   // to the parent: rotate into parent axes, then shift the reference point by r
-  float c = cs[LINK][0], s = cs[LINK][1];
+  ai_rotate<A>(IA, cs[LINK][0], cs[LINK][1]);
+  ai_shift(IA, h12m::R[LINK]);
+  if constexpr (LINK > 0) {
+    AInertia Rg;
+    ai_rigid(Rg, h12m::IBAR[LINK - 1], h12m::MC[LINK - 1], h12m::M[LINK - 1]);
+    ai_add(IA, Rg);
+    if constexpr (LINK - 1 == 3) {
+      if (P.impl && ick.gamma + ick.beta > 0.f) {
+        const float pk[3] = {0.f, 0.f, knee_pz};
+        ai_add_contact(IA, pk, ick.u, ick.beta, ick.gamma);
+      }
+    }
+  }
+}
+// link_p: on entry pAcc is the bias force of LINK (own frame, applied forces subtracted); on exit the parent's
+// (its rigid-body bias force pbias[LINK - 1] included, the knee's external wrench subtracted), u[LINK] set.
+template <int LINK>
+H12_DEV void link_p(const float (&cs)[NL][2], const float (&U)[NL][6], const float (&Dinv)[NL], const float (&Ic)[NL][6],
+                    const float* tau, const float (&pbias)[NL][6], const float* fext_knee, float* pAcc, float (&u)[NL]) {
+  constexpr int A = AX[LINK];
+  const float uu = tau[LINK] - pAcc[A];
+  u[LINK] = uu;
+  const float ud = uu * Dinv[LINK];
+  float pa[6];
+  for (int i = 0; i < 6; ++i) pa[i] = pAcc[i] + Ic[LINK][i] + U[LINK][i] * ud;
+  const float c = cs[LINK][0], s = cs[LINK][1];
   const float* r = h12m::R[LINK];
-  ai_rotate<A>(IA, c, s);
-  ai_shift(IA, r);
   float nr[3], fr[3], rf[3];
   rot<A>(c, s, pa, nr);
   rot<A>(c, s, pa + 3, fr);
@@ -517,19 +546,9 @@ H12_DEV void link_pass2(const KParams& P, const Leg& lg, const float (&cs)[NL][2
   pAcc[0] = nr[0] + rf[0]; pAcc[1] = nr[1] + rf[1]; pAcc[2] = nr[2] + rf[2];
   pAcc[3] = fr[0]; pAcc[4] = fr[1]; pAcc[5] = fr[2];
   if constexpr (LINK > 0) {
-    AInertia Rg;
-    ai_rigid(Rg, h12m::IBAR[LINK - 1], h12m::MC[LINK - 1], h12m::M[LINK - 1]);
-    ai_add(IA, Rg);
-    float pb[6];
-    bias<LINK - 1>(v[LINK - 1], pb);
-    for (int i = 0; i < 6; ++i) pAcc[i] += pb[i];
-    if constexpr (LINK - 1 == 3) {
+    for (int i = 0; i < 6; ++i) pAcc[i] += pbias[LINK - 1][i];
+    if constexpr (LINK - 1 == 3)
       for (int i = 0; i < 6; ++i) pAcc[i] -= fext_knee[i];
-      if (P.impl && ick.gamma + ick.beta > 0.f) {
-        const float pk[3] = {0.f, 0.f, knee_pz};
-        ai_add_contact(IA, pk, ick.u, ick.beta, ick.gamma);
-      }
-    }
   }
 }
 
@@ -751,14 +770,20 @@ H12_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
-// added to the reported knee / foot contact forces.  Rk/pk, vk: knee pose (lane frame) and body velocity,
-// Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP swap; wave-uniform at every barrier.
-H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
-                           const float (&Rf)[3][3], const float* pf, const float* vf, float* wk, float* wf, Forces& fr) {
+H12_DEV SelfLds& self_lds() {
   __shared__ SelfLds L;
+  return L;
+}
+
+// Self-contacts, phase 1 (self_stage): broad phase and, when some env of the wave has a candidate pair, the LDS
+// staging of the wave's capsules and body kinematics; returns the wave's candidate mask (0: nothing staged, no
+// self-contact anywhere in the wave).  Phase 2 (self_finish): the pair jobs and each lane's wrenches.  Rk/pk, vk:
+// knee pose (lane frame) and body velocity, Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP
+// swap; wave-uniform at every wave_sync.
+H12_DEV uint64_t self_stage(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
+                            const float (&Rf)[3][3], const float* pf, const float* vf) {
+  SelfLds& L = self_lds();
   const float sg = leg ? -1.f : 1.f;
-  for (int i = 0; i < 6; ++i) { wk[i] = 0.f; wf[i] = 0.f; }
   // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
   float k0[3], k1[3], b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
   body_point_real(Rk, pk, h12m::KNEE0, sg, k0);
@@ -780,13 +805,7 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
   const int mine = (f0 | f1 << 1) << (2 * leg);   // bits: 0 kk, 1 kf, 2 fk, 3 ff (left capsule major)
   const int flags = mine | pair_swap_i(mine);
   const uint64_t act = __ballot(flags != 0 && leg == 0);
-  if (act == 0) return;  // wave-uniform: no candidate pair anywhere in the wave
-#ifdef H12_SELF_BROAD_ONLY  // experiment builds only: price the broad phase alone
-  if (act != 0) return;
-#endif
-#ifdef H12_SELF_NARROW_DEAD  // experiment builds only: narrow phase compiled in but never run (register cost)
-  if (P.mode != 12345) return;
-#endif
+  if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
   // ---- stage this leg's capsules and body kinematics (real frame)
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
   {
@@ -820,6 +839,18 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
     }
   }
   wave_sync();
+  return act;
+}
+
+// Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
+// added to the reported knee / foot contact forces (fr).  act: self_stage's result.
+H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&Rk)[3][3], const float* pk,
+                         const float (&Rf)[3][3], const float* pf, float* wk, float* wf, Forces& fr) {
+  for (int i = 0; i < 6; ++i) { wk[i] = 0.f; wf[i] = 0.f; }
+  if (act == 0) return;
+  SelfLds& L = self_lds();
+  const float sg = leg ? -1.f : 1.f;
+  const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
   // ---- pair jobs of the candidate envs over the wave's live lanes (a ragged last block has fewer):
   // job = (env rank, left capsule i, right capsule j)
   const uint64_t live = __ballot(1);
@@ -888,132 +919,222 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
   wave_sync();  // the staging area is rewritten by the next physics step
 }
 
-// ---- self-contact helper wave (step_kernel with self-collision: a second wave per block).  The self-contact
-// wrenches are explicit and enter the ABA only at pass 2, so the block's second wave computes them
-// (self_contacts, the same code as the in-wave path) while the physics wave evaluates the sole contacts and the
-// joint torques.  Per inner step: the physics wave writes its knee / foot kinematics, barrier, the helper computes
-// and writes the two wrenches, barrier, the physics wave reads them.
-struct SelfHand {
-  float4 kin[9][BLOCK];  // per physics lane: knee R (9), p (3), v (6); foot R (9), p (3), v (6)
-  float4 res[3][BLOCK];  // per physics lane: knee wrench (6), foot wrench (6)
+H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
+                           const float (&Rf)[3][3], const float* pf, const float* vf, float* wk, float* wf, Forces& fr) {
+  const uint64_t act = self_stage(P, leg, Rk, pk, vk, Rf, pf, vf);
+  self_finish(P, leg, act, Rk, pk, Rf, pf, wk, wf, fr);
+}
+
+// ---- the helper waves (step_kernel: two more waves per block, on other SIMDs of the CU).  The forces of an inner
+// step that do not depend on its ground contacts -- the joint torques beyond the PD term (limit penalty,
+// max-velocity damper, damping, friction loss) with their implicit inertias, the rigid-body bias forces of the 6
+// links, and the leg-leg self-contact wrenches -- are computed from the state at the start of the inner step by
+// helper waves while the physics wave runs pass 1, the ground contacts and the articulated-inertia chain of
+// pass 2.  Per inner step (workgroup barriers S, R1, R2):
+//   physics wave: pass 1, knee / sole contacts | R1 | inertia chain | R2 | bias-force chain, base solve, pass 3,
+//                 integration, next state to LDS | S
+//   helper wave:  S | joint terms | R1 | pass 1, bias forces | R2
+//   self wave:    S | pass 1, self-contact broad phase + staging | R1 | pair jobs, wrenches | R2
+// (the self wave is launched only with self-collision).
+struct HelpLds {
+  float4 st[7][BLOCK];    // state: base pos (3), quat (4), v (3), w (3); leg q (6), qd (6) (lane frame); env origin (3)
+  float4 jt[3][BLOCK];    // joint terms: tq (6), dl (6)
+  float4 bias[9][BLOCK];  // bias forces of the 6 links (6 x 6)
+  float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
 };
-H12_DEV SelfHand& self_hand() {
-  __shared__ SelfHand H;
+// value barrier: x is computed before this point (an empty volatile asm that reads and rewrites it)
+H12_DEV void pin(float& x) { asm volatile("" : "+v"(x)); }
+H12_DEV HelpLds& help_lds() {
+  __shared__ HelpLds H;
   return H;
 }
-H12_DEV void hand_put(int l, const float (&Rk)[3][3], const float* pk, const float* vk, const float (&Rf)[3][3],
-                      const float* pf, const float* vf) {
-  float k[36];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) { k[3 * i + j] = Rk[i][j]; k[18 + 3 * i + j] = Rf[i][j]; }
-  for (int i = 0; i < 3; ++i) { k[9 + i] = pk[i]; k[27 + i] = pf[i]; }
-  for (int i = 0; i < 6; ++i) { k[12 + i] = vk[i]; k[30 + i] = vf[i]; }
-  SelfHand& H = self_hand();
-#pragma unroll
-  for (int c = 0; c < 9; ++c) H.kin[c][l] = make_float4(k[4 * c], k[4 * c + 1], k[4 * c + 2], k[4 * c + 3]);
+H12_DEV void put4(float4 (*dst)[BLOCK], int l, const float* x, int n4) {
+  for (int c = 0; c < n4; ++c) dst[c][l] = make_float4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
 }
-template <int K>
-H12_DEV void self_helper(const KParams& P, int n, int n_steps) {
-  const int l = threadIdx.x - BLOCK;
-  const int leg = l & 1;
-  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
-  SelfHand& H = self_hand();
-  for (int it = 0; it < n_steps; ++it) {
-    __syncthreads();  // kinematics written
-    if (active) {
-      float k[36];
+H12_DEV void get4(const float4 (*src)[BLOCK], int l, float* x, int n4) {
+  for (int c = 0; c < n4; ++c) {
+    const float4 y = src[c][l];
+    x[4 * c] = y.x; x[4 * c + 1] = y.y; x[4 * c + 2] = y.z; x[4 * c + 3] = y.w;
+  }
+}
+H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
+  float x[28] = {b.pos[0], b.pos[1], b.pos[2], b.quat[0], b.quat[1], b.quat[2], b.quat[3],
+                 b.vlin[0], b.vlin[1], b.vlin[2], b.wang[0], b.wang[1], b.wang[2]};
+  for (int k = 0; k < NL; ++k) { x[13 + k] = lg.q[k]; x[19 + k] = lg.qd[k]; }
+  x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
+  put4(help_lds().st, l, x, 7);
+}
+
+// joint torques beyond the PD term (tq) and the implicit joint inertia of the active limits (dl), from q / qd
+H12_DEV void joint_terms(const KParams& P, const Leg& lg, float h, float* tq, float* dl) {
 #pragma unroll
-      for (int c = 0; c < 9; ++c) {
-        const float4 x = H.kin[c][l];
-        k[4 * c] = x.x; k[4 * c + 1] = x.y; k[4 * c + 2] = x.z; k[4 * c + 3] = x.w;
-      }
-      float Rk[3][3], Rf[3][3];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) { Rk[i][j] = k[3 * i + j]; Rf[i][j] = k[18 + 3 * i + j]; }
-      float wk[6], wf[6];
-      Forces fr = {};
-      self_contacts(P, leg, Rk, k + 9, k + 12, Rf, k + 27, k + 30, wk, wf, fr);
-      H.res[0][l] = make_float4(wk[0], wk[1], wk[2], wk[3]);
-      H.res[1][l] = make_float4(wk[4], wk[5], wf[0], wf[1]);
-      H.res[2][l] = make_float4(wf[2], wf[3], wf[4], wf[5]);
-    }
-    __syncthreads();  // wrenches written
+  for (int k = 0; k < NL; ++k) {
+    const float q = lg.q[k], qd = lg.qd[k];
+    // joint-limit penalty, branch-free (selects instead of divergent branches); dl: h (lc + h lk) of an active
+    // limit (oracle joint_limit_torque)
+    const float dhi = q - h12m::QHI[k], dlo = q - h12m::QLO[k];
+    const float thi = fminf(0.f, -P.lk * dhi - P.lc * qd), tlo = fmaxf(0.f, -P.lk * dlo - P.lc * qd);
+    const float tl = dhi > 0.f ? thi : (dlo < 0.f ? tlo : 0.f);
+    float t = tl;
+    dl[k] = tl != 0.f ? P.dl : 0.f;
+    // PhysX max joint velocity: implicit stiff damper on the excess with a C1 ramp-in over H12_VLIM_RAMP
+    // (h12env.h; oracle joint_limit_torque); zero below the limit
+    const float ex = fmaxf(fabsf(qd) - P.vmax[k], 0.f);
+    const float r = fminf(ex * (1.f / H12_VLIM_RAMP), 1.f);
+    const float mag = ex < H12_VLIM_RAMP ? 0.5f * P.cv * ex * r : P.cv * (ex - 0.5f * H12_VLIM_RAMP);
+    t -= copysignf(mag, qd);
+    dl[k] += h * P.cv * r;
+    t -= P.dimpl[k] * qd;
+    if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
+    tq[k] = t;
   }
 }
 
-// One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
-// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.  HW: the block has a self-contact
-// helper wave (step_kernel; used when P.self_coll), else the self-contacts are evaluated in this wave.
-template <int K, bool HW>
-H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
-                        const float* org) {
+// pass 1 from the state: lane-frame base pose / velocity, then the 6 links' joint sin / cos, spatial velocities
+// and world poses; Rk / pk: the knee's pose, R / p on exit: the foot's.
+template <int K>
+H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, float (&R0)[3][3], float* vb,
+                       float* pb0, float (&cs)[NL][2], float (&v)[NL][6], float (&Rk)[3][3], float* pk,
+                       float (&R)[3][3], float* p) {
   const float sg = leg ? -1.f : 1.f;
-  float R0[3][3];
   quat_R(b.quat, R0);
-  float vb[3];
   mtv(R0, b.vlin, vb);
   // base quantities in the lane frame: R' = M R M, v' = s6 * v, p' = M p
   const float mm[3] = {1.f, sg, 1.f};
-  float R[3][3];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) R[i][j] = mm[i] * mm[j] * R0[i][j];
-  float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
-  float vl0[6];
-  for (int i = 0; i < 6; ++i) vl0[i] = s6(i, sg) * v0[i];
+  float vl0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+  for (int i = 0; i < 6; ++i) vl0[i] *= s6(i, sg);
   // base position: env-local on terrain (contact geometry relative to the env origin, ground_local)
-  float pb0[3] = {b.pos[0], b.pos[1], b.pos[2]};
+  pb0[0] = b.pos[0]; pb0[1] = b.pos[1]; pb0[2] = b.pos[2];
   if constexpr (Feat<K>::terrain) { pb0[0] -= org[0]; pb0[1] -= org[1]; pb0[2] -= org[2]; }
-  float p[3] = {pb0[0], sg * pb0[1], pb0[2]};
-  float cs[NL][2], v[NL][6];
-  float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  ImplC ick;     // knee contact linearisation (added to link 3 in pass 2)
-  float knee_pz;  // z of the knee contact point (KNEE0 or KNEE1; x = y = 0)
+  p[0] = pb0[0]; p[1] = sg * pb0[1]; p[2] = pb0[2];
   link_pass1<0>(lg, cs, vl0, v, R, p);
   link_pass1<1>(lg, cs, v[0], v, R, p);
   link_pass1<2>(lg, cs, v[1], v, R, p);
   link_pass1<3>(lg, cs, v[2], v, R, p);
-  float Rk[3][3], pk[3];  // knee pose, kept for the self-collision pass
   for (int i = 0; i < 3; ++i) {
     pk[i] = p[i];
     for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j];
   }
+  link_pass1<4>(lg, cs, v[3], v, R, p);
+  link_pass1<5>(lg, cs, v[4], v, R, p);
+}
+
+// rigid-body bias forces of the 6 links (link coords, lane frame)
+H12_DEV void leg_bias(const float (&v)[NL][6], float (&pbias)[NL][6]) {
+  bias<0>(v[0], pbias[0]);
+  bias<1>(v[1], pbias[1]);
+  bias<2>(v[2], pbias[2]);
+  bias<3>(v[3], pbias[3]);
+  bias<4>(v[4], pbias[4]);
+  bias<5>(v[5], pbias[5]);
+}
+
+H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
+  float x[28];
+  get4(help_lds().st, l, x, 7);
+  for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; org[i] = x[25 + i]; }
+  for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
+  for (int k = 0; k < NL; ++k) { lg.q[k] = x[13 + k]; lg.qd[k] = x[19 + k]; }
+}
+
+template <int K>
+H12_DEV void helper_wave(const KParams& P, int n, int n_steps) {
+  const int l = threadIdx.x - BLOCK;
+  const int leg = l & 1;
+  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
+  HelpLds& H = help_lds();
+  for (int it = 0; it < n_steps; ++it) {
+    __syncthreads();  // S: the state of this inner step
+    Base b;
+    Leg lg;
+    float org[3];
+    if (active) {
+      get_state(l, b, lg, org);
+      float jt[12];
+      joint_terms(P, lg, P.h, jt, jt + 6);
+      put4(H.jt, l, jt, 3);
+    }
+    __syncthreads();  // R1: joint terms
+    if (active) {
+      float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
+      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
+      float pb[NL][6], o[36];
+      leg_bias(v, pb);
+      for (int k = 0; k < NL; ++k)
+        for (int i = 0; i < 6; ++i) o[6 * k + i] = pb[k][i];
+      put4(H.bias, l, o, 9);
+    }
+    __syncthreads();  // R2: bias forces
+  }
+}
+
+template <int K>
+H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
+  const int l = threadIdx.x - 2 * BLOCK;
+  const int leg = l & 1;
+  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
+  HelpLds& H = help_lds();
+  for (int it = 0; it < n_steps; ++it) {
+    __syncthreads();  // S: the state of this inner step
+    float Rk[3][3], pk[3], R[3][3], p[3];
+    uint64_t act = 0;
+    if (active) {
+      Base b;
+      Leg lg;
+      float org[3];
+      get_state(l, b, lg, org);
+      float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
+      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
+      act = self_stage(P, leg, Rk, pk, v[3], R, p, v[5]);
+    }
+    __syncthreads();  // R1
+    if (active) {
+      float w[12];
+      Forces fr = {};
+      self_finish(P, leg, act, Rk, pk, R, p, w, w + 6, fr);
+      put4(H.selfw, l, w, 3);
+    }
+    __syncthreads();  // R2: self-contact wrenches
+  }
+}
+
+// One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
+// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.  HW: the block has a helper wave
+// (step_kernel; the state of this step is in LDS and, with more, the next one is put there), else the
+// contact-independent forces are evaluated in this wave.
+template <int K, bool HW>
+H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
+                        const float* org, bool more) {
+  PHX_INIT();
+  const float sg = leg ? -1.f : 1.f;
+  float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
+  leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
+  const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+  float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ImplC ick;      // knee contact linearisation (added to link 3 in pass 2)
+  float knee_pz;  // z of the knee contact point (KNEE0 or KNEE1; x = y = 0)
   {
     // knee capsule: lower end point, contact evaluated at the knee link pose
     float w0[3], w1[3];
-    mv(R, h12m::KNEE0, w0);
-    mv(R, h12m::KNEE1, w1);
+    mv(Rk, h12m::KNEE0, w0);
+    mv(Rk, h12m::KNEE1, w1);
     const bool lo0 = w0[2] <= w1[2];
     const float* pl = lo0 ? h12m::KNEE0 : h12m::KNEE1;
     knee_pz = lo0 ? h12m::KNEE0[2] : h12m::KNEE1[2];
     float dummy[2];
-    contact_sphere<false, Feat<K>::terrain>(P, R, p, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, org, P.mus, P.mud, ick);
+    contact_sphere<false, Feat<K>::terrain>(P, Rk, pk, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, org, P.mus, P.mud, ick);
   }
-  link_pass1<4>(lg, cs, v[3], v, R, p);
-  link_pass1<5>(lg, cs, v[4], v, R, p);
-  // self-contacts between the legs: explicit wrenches on the knee (-> fext_knee) and the foot (-> pAcc below)
-  float wsf[6];
-  if (P.self_coll) {
-    if constexpr (HW) {
-      hand_put(threadIdx.x, Rk, pk, v[3], R, p, v[5]);
-      __syncthreads();  // the helper wave computes the wrenches while this wave continues
-    } else {
-      float wsk[6];
-      self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wsk, wsf, fr);
-      for (int i = 0; i < 6; ++i) fext_knee[i] += wsk[i];
-    }
-  }
-  // ---- foot: 4 anchored sole spheres on the ankle-roll link; starts pass 2 of link 5
+  // ---- foot: 4 anchored sole spheres on the ankle-roll link; the inertia chain of pass 2 starts at link 5
   int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
   float fu[H12_NFOOT_PTS][3];         // implicit: ground normal at each sole sphere, foot coords
   AInertia IA;
   ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
-  float pAcc[6];
-  bias<5>(v[5], pAcc);
+  float pc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // minus the sole contact wrench (foot coords)
   SoleSums ss;
-  if (!HW && P.self_coll)
-    for (int i = 0; i < 6; ++i) pAcc[i] -= wsf[i];
   if constexpr (!Feat<K>::terrain) {
-    sole_contacts_flat(P, R, p, v[5], lg, IA, pAcc, fr.foot, ss);
+    sole_contacts_flat(P, R, p, v[5], lg, IA, pc, fr.foot, ss);
   } else {
     float fext[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int nmask = 0;
@@ -1032,47 +1153,70 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
       }
     }
     lg.cmask = nmask;
-    for (int i = 0; i < 6; ++i) pAcc[i] -= fext[i];
+    for (int i = 0; i < 6; ++i) pc[i] = -fext[i];
   }
-  // ---- joint torques for this inner step: actuator + limit penalty (+ MuJoCo passive)
-  float tau[NL], dl[NL];  // dl: implicit joint-limit inertia h (lc + h lk) of an active limit (oracle joint_limit_torque)
-#pragma unroll
-  for (int k = 0; k < NL; ++k) {
-    float q = lg.q[k], qd = lg.qd[k];
-    float t = tau_pd[k];
-    // joint-limit penalty, branch-free (selects instead of divergent branches)
-    const float dhi = q - h12m::QHI[k], dlo = q - h12m::QLO[k];
-    const float thi = fminf(0.f, -P.lk * dhi - P.lc * qd), tlo = fmaxf(0.f, -P.lk * dlo - P.lc * qd);
-    const float tl = dhi > 0.f ? thi : (dlo < 0.f ? tlo : 0.f);
-    t += tl;
-    dl[k] = tl != 0.f ? P.dl : 0.f;
-    // PhysX max joint velocity: implicit stiff damper on the excess with a C1 ramp-in over H12_VLIM_RAMP
-    // (h12env.h; oracle joint_limit_torque); zero below the limit
-    const float ex = fmaxf(fabsf(qd) - P.vmax[k], 0.f);
-    const float r = fminf(ex * (1.f / H12_VLIM_RAMP), 1.f);
-    const float mag = ex < H12_VLIM_RAMP ? 0.5f * P.cv * ex * r : P.cv * (ex - 0.5f * H12_VLIM_RAMP);
-    t -= copysignf(mag, qd);
-    dl[k] += h * P.cv * r;
-    t -= P.dimpl[k] * qd;
-    if (P.use_fl) t -= h12m::FRICTIONLOSS[k] * tanhf(qd * 100.f);
-    tau[k] = t;
+  // ---- joint torques beyond PD, implicit limit inertias (helper wave: from the state of this step)
+  float tau[NL], dl[NL];
+  PHX(10);
+  if constexpr (HW) {
+    __syncthreads();  // R1
+    float jt[12];
+    get4(help_lds().jt, threadIdx.x, jt, 3);
+    for (int k = 0; k < NL; ++k) { tau[k] = tau_pd[k] + jt[k]; dl[k] = jt[6 + k]; }
+  } else {
+    float tq[NL];
+    joint_terms(P, lg, h, tq, dl);
+    for (int k = 0; k < NL; ++k) tau[k] = tau_pd[k] + tq[k];
   }
-  if (HW && P.self_coll) {
-    __syncthreads();  // the helper's wrenches are in LDS
-    const SelfHand& H = self_hand();
-    const float4 r0 = H.res[0][threadIdx.x], r1 = H.res[1][threadIdx.x], r2 = H.res[2][threadIdx.x];
-    const float wk[6] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, wf[6] = {r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
-    for (int i = 0; i < 6; ++i) { fext_knee[i] += wk[i]; pAcc[i] -= wf[i]; }
-    for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
+  PHX(11);
+  // ---- pass 2, articulated-inertia chain (leaf -> root)
+  float U[NL][6], Dinv[NL], u[NL], Ic[NL][6];
+  link_ia<5>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<4>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<3>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<2>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<1>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<0>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  PHX(12);
+  // ---- the contact-independent forces: bias forces, self-contact wrenches (helper wave)
+  if constexpr (HW) {  // the inertia chain stays ahead of R2 (else the compiler sinks most of it past the barrier)
+    for (int i = 0; i < 6; ++i) { pin(IA.A[i]); pin(IA.C[i]); }
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) pin(IA.B[i][j]);
+    for (int k = 0; k < NL; ++k)
+      for (int i = 0; i < 6; ++i) pin(Ic[k][i]);
   }
-  // ---- pass 2 (leaf -> root)
-  float U[NL][6], Dinv[NL], u[NL];
-  link_pass2<5>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
-  link_pass2<4>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
-  link_pass2<3>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
-  link_pass2<2>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
-  link_pass2<1>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
-  link_pass2<0>(P, lg, cs, v, fext_knee, ick, knee_pz, tau, dl, IA, pAcc, U, Dinv, u, h);
+  float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (HW) {
+    __syncthreads();  // R2
+    float o[36];
+    get4(help_lds().bias, threadIdx.x, o, 9);
+    for (int k = 0; k < NL; ++k)
+      for (int i = 0; i < 6; ++i) pbias[k][i] = o[6 * k + i];
+    if (P.self_coll) {
+      float w[12];
+      get4(help_lds().selfw, threadIdx.x, w, 3);
+      for (int i = 0; i < 6; ++i) { wk[i] = w[i]; wf[i] = w[6 + i]; }
+    }
+  } else {
+    leg_bias(v, pbias);
+    if (P.self_coll) {
+      Forces fs = {};
+      self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wk, wf, fs);
+    }
+  }
+  PHX(13);
+  for (int i = 0; i < 6; ++i) fext_knee[i] += wk[i];
+  for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
+  // ---- pass 2, bias-force chain (leaf -> root)
+  float pAcc[6];
+  for (int i = 0; i < 6; ++i) pAcc[i] = pbias[5][i] + pc[i] - wf[i];
+  link_p<5>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<4>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<3>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<2>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<1>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<0>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
   // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
@@ -1168,6 +1312,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     lg.qd[k] += h * qdd[k];
     lg.q[k] += h * lg.qd[k];
   }
+  if constexpr (HW) {
+    if (more) {
+      put_state(threadIdx.x, b, lg, org);
+      __syncthreads();  // S: the next inner step's state
+    }
+  }
+  PHX(14);
 }
 
 // ------------------------------------------------------------------ state load / store
@@ -2016,9 +2167,10 @@ struct StepArgs {
 };
 
 template <int K>
-__global__ void __launch_bounds__(2 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
-  if (threadIdx.x >= BLOCK) {  // the self-contact helper wave (launched only with P.self_coll)
-    if (P.self_coll) self_helper<K>(P, W.n, P.decimation * P.inner);
+__global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
+    if (threadIdx.x < 2 * BLOCK) helper_wave<K>(P, W.n, P.decimation * P.inner);
+    else self_wave<K>(P, W.n, P.decimation * P.inner);
     return;
   }
   const int lane_pair = threadIdx.x >> 1;
@@ -2049,6 +2201,8 @@ __global__ void __launch_bounds__(2 * BLOCK) step_kernel(KParams P, Workspace W,
     float fmax_knee = 0.f, fmax_torso = 0.f, fmax_foot = 0.f, flast_foot = 0.f;
     uint32_t cflags = 0;  // foot contact flag of every physics step (ContactSensor replay)
     const float wgt = frcp((float)P.inner);
+    put_state(threadIdx.x, s.b, s.lg, s.origin);
+    __syncthreads();  // S: the first inner step's state for the helper wave
     for (int st = 0; st < dec; ++st) {
       if (P.mode == H12_MODE_ISAACLAB) {
         // DelayedPDActuator: delayed target = CircularBuffer[lag] with lag clamped to pushes-1
@@ -2074,7 +2228,8 @@ __global__ void __launch_bounds__(2 * BLOCK) step_kernel(KParams P, Workspace W,
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
-      for (int it = 0; it < P.inner; ++it) inner_step<K, true>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
+      for (int it = 0; it < P.inner; ++it)
+        inner_step<K, true>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin, !last || it < P.inner - 1);
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
       // ContactSensor: net force = mean over the inner steps of the physics step
@@ -2445,7 +2600,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step<K, false>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
+    for (int it = 0; it < P.inner; ++it) inner_step<K, false>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin, false);
   }
   store_env<K>(P, W, e, leg, s);
 }
@@ -3016,8 +3171,8 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.dz_slot = (int)(h->dz_step++ % 3);
   hipEvent_t t0, t1;
   timing_events(h, 0, &t0, &t1);
-  // with self-collision each block carries a second (helper) wave, see self_helper
-  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3(h->P.self_coll ? 2 * BLOCK : BLOCK), 0, (hipStream_t)stream,
+  // every block carries a helper wave and, with self-collision, a self-contact wave (helper_wave, self_wave)
+  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 3 : 2) * BLOCK), 0, (hipStream_t)stream,
             h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (h->P.cat) {

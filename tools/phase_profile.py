@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Per-phase shader-clock profile of step_kernel (experiment build, -DH12_PHASE_PROFILE).
+
+    python tools/phase_profile.py --build [--tag NAME] [-D FLAG ...]   # here: compile tools/_variants/lib_NAME.so
+    python tools/phase_profile.py [--tag NAME] [--steps K]            # GPU box: run the bench workload, print
+
+The variant library records, per main (physics) wave and lane 0, the cycles between the PH / PHX marks of
+csrc/h12env.hip into 16 global counters (h12env_phase_profile); printed here as cycles per wave and env
+step.  Slots: 0 state loads, 1 physics loop, 2 contact-sensor replay, 3 rewards / terminations, 4 outputs +
+episode log, 5 reset + commands + events, 6 observation frame, 7 state stores; inside each inner step
+(summed over the step's inner steps): 10 pass 1 and the ground contacts, 11 the wait for the helper wave's
+joint terms, 12 the articulated-inertia chain, 13 the wait for its bias forces / self-contact wrenches, 14 the
+rest (bias-force chain, base solve, pass 3, integration, next state to the helper).  The marks' own atomics add a few hundred cycles per step.  Not the product
+library: the variant is loaded through H12ENV_LIB and never built by __graft_entry__.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
+VARIANTS = ROOT / "tools" / "_variants"
+SLOTS = {0: "loads", 1: "physics", 2: "sensor", 3: "rewards", 4: "outputs+log", 5: "reset+cmd", 6: "frame",
+         7: "stores", 10: "inner: pass 1 + ground contacts", 11: "inner: wait R1 (joint terms)",
+         12: "inner: inertia chain", 13: "inner: wait R2 (bias, self-contacts)", 14: "inner: bias chain .. integration + S"}
+
+
+def build(tag: str, flags: list[str]) -> Path:
+    from h12env.build import ARCH, CSRC, hipcc
+
+    VARIANTS.mkdir(parents=True, exist_ok=True)
+    out = VARIANTS / f"lib_{tag}.so"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
+           "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros", "-fPIC", "-shared", "-Wno-unused-function",
+           "-DH12_PHASE_PROFILE", *[f"-D{f}" for f in flags], "-o", str(out), str(CSRC / "h12env.hip")]
+    print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
+    os.environ["H12ENV_LIB"] = str(VARIANTS / f"lib_{tag}.so")
+    import torch
+
+    from h12env import H12FlatEnvCfg
+    from h12env._abi import load_library
+    from h12env.env import H12VelocityEnv
+
+    lib = load_library()
+    lib.h12env_phase_profile.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    lib.h12env_phase_profile.restype = C.c_int
+    cfg = H12FlatEnvCfg()
+    cfg.scene.num_envs = envs
+    cfg.sim.device = "cuda:0"
+    cfg.sim.self_collision = self_coll
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    env.episode_length_buf = torch.randint(0, env.max_episode_length, (envs,), device="cuda:0", generator=g,
+                                           dtype=env.episode_length_buf.dtype)
+    acts = torch.randn(burn + steps, envs, 12, device="cuda:0", generator=g)
+    buf = (C.c_ulonglong * 16)()
+    for t in range(burn):
+        env.step(acts[t])
+    torch.cuda.synchronize()
+    lib.h12env_phase_profile(buf, 1)
+    for t in range(steps):
+        env.step(acts[burn + t])
+    torch.cuda.synchronize()
+    lib.h12env_phase_profile(buf, 1)
+    waves = (envs + 31) // 32
+    res = {SLOTS[i]: round(buf[i] / waves / steps, 1) for i in SLOTS}
+    env.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--tag", default="phase")
+    ap.add_argument("-D", dest="defs", action="append", default=[])
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--burn-in", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--no-self-collision", action="store_true")
+    a = ap.parse_args()
+    if a.build:
+        build(a.tag, a.defs)
+        return
+    res = run(a.tag, a.steps, a.burn_in, a.envs, not a.no_self_collision)
+    print(json.dumps({"tag": a.tag, "envs": a.envs, "cycles_per_wave_per_env_step": res}))
+
+
+if __name__ == "__main__":
+    main()
