@@ -937,9 +937,10 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
 //   self wave:    S | pass 1, self-contact broad phase + staging | R1 | pair jobs, wrenches | R2
 // (the self wave is launched only with self-collision).
 struct HelpLds {
-  float4 st[7][BLOCK];    // state: base pos (3), quat (4), v (3), w (3); leg q (6), qd (6) (lane frame); env origin (3)
-  float4 jt[3][BLOCK];    // joint terms: tq (6), dl (6)
-  float4 bias[9][BLOCK];  // bias forces of the 6 links (6 x 6)
+  float4 st[8][BLOCK];    // state: base pos (3), quat (4), v (3), w (3); leg q (6), qd (6) (lane frame); env origin (3);
+                          // added torso mass (1)
+  float4 jt[7][BLOCK];    // joint terms: tq (6), dl (6); knee contact: wrench (6), reported force (3), ImplC (5), z (1)
+  float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
 };
 // value barrier: x is computed before this point (an empty volatile asm that reads and rewrites it)
@@ -958,11 +959,12 @@ H12_DEV void get4(const float4 (*src)[BLOCK], int l, float* x, int n4) {
   }
 }
 H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
-  float x[28] = {b.pos[0], b.pos[1], b.pos[2], b.quat[0], b.quat[1], b.quat[2], b.quat[3],
+  float x[32] = {b.pos[0], b.pos[1], b.pos[2], b.quat[0], b.quat[1], b.quat[2], b.quat[3],
                  b.vlin[0], b.vlin[1], b.vlin[2], b.wang[0], b.wang[1], b.wang[2]};
   for (int k = 0; k < NL; ++k) { x[13 + k] = lg.q[k]; x[19 + k] = lg.qd[k]; }
   x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
-  put4(help_lds().st, l, x, 7);
+  x[28] = lg.dmass; x[29] = x[30] = x[31] = 0.f;
+  put4(help_lds().st, l, x, 8);
 }
 
 // joint torques beyond the PD term (tq) and the implicit joint inertia of the active limits (dl), from q / qd
@@ -1021,6 +1023,35 @@ H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, 
   link_pass1<5>(lg, cs, v[4], v, R, p);
 }
 
+// knee capsule contact with the ground: lower end point, evaluated at the knee link pose (Rk / pk / vk)
+template <int K>
+H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], const float* pk, const float* vk,
+                          const float* org, float* fext_knee, float* rep, ImplC& ick, float& knee_pz) {
+  float w0[3], w1[3];
+  mv(Rk, h12m::KNEE0, w0);
+  mv(Rk, h12m::KNEE1, w1);
+  const bool lo0 = w0[2] <= w1[2];
+  const float* pl = lo0 ? h12m::KNEE0 : h12m::KNEE1;
+  knee_pz = lo0 ? h12m::KNEE0[2] : h12m::KNEE1[2];
+  float dummy[2];
+  contact_sphere<false, Feat<K>::terrain>(P, Rk, pk, vk, pl, h12m::KNEE_R, fext_knee, rep, dummy, false, sg, org, P.mus,
+                                          P.mud, ick);
+}
+// rigid body of the base (with the added torso mass): inertia Rg and bias force v x* (Rg v) (pelvis coords)
+template <int K>
+H12_DEV void base_body(const KParams& P, const Leg& lg, const float* v0, AInertia& Rg, float* pb) {
+  ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
+  if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
+  float hb[6];
+  ai_mul(Rg, v0, hb);
+  float x1[3], x2[3], x3[3];
+  cross(v0, hb, x1);
+  cross(v0 + 3, hb + 3, x2);
+  cross(v0, hb + 3, x3);
+  pb[0] = x1[0] + x2[0]; pb[1] = x1[1] + x2[1]; pb[2] = x1[2] + x2[2];
+  pb[3] = x3[0]; pb[4] = x3[1]; pb[5] = x3[2];
+}
+
 // rigid-body bias forces of the 6 links (link coords, lane frame)
 H12_DEV void leg_bias(const float (&v)[NL][6], float (&pbias)[NL][6]) {
   bias<0>(v[0], pbias[0]);
@@ -1032,8 +1063,9 @@ H12_DEV void leg_bias(const float (&v)[NL][6], float (&pbias)[NL][6]) {
 }
 
 H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
-  float x[28];
-  get4(help_lds().st, l, x, 7);
+  float x[32];
+  get4(help_lds().st, l, x, 8);
+  lg.dmass = x[28];
   for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; org[i] = x[25 + i]; }
   for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
   for (int k = 0; k < NL; ++k) { lg.q[k] = x[13 + k]; lg.qd[k] = x[19 + k]; }
@@ -1050,21 +1082,30 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps) {
     Base b;
     Leg lg;
     float org[3];
+    float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
     if (active) {
       get_state(l, b, lg, org);
-      float jt[12];
+      float jt[28];
       joint_terms(P, lg, P.h, jt, jt + 6);
-      put4(H.jt, l, jt, 3);
-    }
-    __syncthreads();  // R1: joint terms
-    if (active) {
-      float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
-      float pb[NL][6], o[36];
+      ImplC ick;
+      for (int i = 12; i < 21; ++i) jt[i] = 0.f;
+      knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt + 12, jt + 18, ick, jt[26]);
+      jt[21] = ick.beta; jt[22] = ick.gamma; jt[23] = ick.u[0]; jt[24] = ick.u[1]; jt[25] = ick.u[2]; jt[27] = 0.f;
+      put4(H.jt, l, jt, 7);
+    }
+    __syncthreads();  // R1: joint terms, knee contact
+    if (active) {
+      float pb[NL][6], o[44];
       leg_bias(v, pb);
       for (int k = 0; k < NL; ++k)
         for (int i = 0; i < 6; ++i) o[6 * k + i] = pb[k][i];
-      put4(H.bias, l, o, 9);
+      const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+      AInertia Rg;
+      base_body<K>(P, lg, v0, Rg, o + 36);
+      if (leg) for (int i = 36; i < 42; ++i) o[i] = 0.f;
+      o[42] = o[43] = 0.f;
+      put4(H.bias, l, o, 11);
     }
     __syncthreads();  // R2: bias forces
   }
@@ -1115,17 +1156,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   ImplC ick;      // knee contact linearisation (added to link 3 in pass 2)
   float knee_pz;  // z of the knee contact point (KNEE0 or KNEE1; x = y = 0)
-  {
-    // knee capsule: lower end point, contact evaluated at the knee link pose
-    float w0[3], w1[3];
-    mv(Rk, h12m::KNEE0, w0);
-    mv(Rk, h12m::KNEE1, w1);
-    const bool lo0 = w0[2] <= w1[2];
-    const float* pl = lo0 ? h12m::KNEE0 : h12m::KNEE1;
-    knee_pz = lo0 ? h12m::KNEE0[2] : h12m::KNEE1[2];
-    float dummy[2];
-    contact_sphere<false, Feat<K>::terrain>(P, Rk, pk, v[3], pl, h12m::KNEE_R, fext_knee, fr.knee, dummy, false, sg, org, P.mus, P.mud, ick);
-  }
+  if constexpr (!HW) knee_contact<K>(P, sg, Rk, pk, v[3], org, fext_knee, fr.knee, ick, knee_pz);
   // ---- foot: 4 anchored sole spheres on the ankle-roll link; the inertia chain of pass 2 starts at link 5
   int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
   float fu[H12_NFOOT_PTS][3];         // implicit: ground normal at each sole sphere, foot coords
@@ -1160,9 +1191,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   PHX(10);
   if constexpr (HW) {
     __syncthreads();  // R1
-    float jt[12];
-    get4(help_lds().jt, threadIdx.x, jt, 3);
+    float jt[28];
+    get4(help_lds().jt, threadIdx.x, jt, 7);
     for (int k = 0; k < NL; ++k) { tau[k] = tau_pd[k] + jt[k]; dl[k] = jt[6 + k]; }
+    for (int i = 0; i < 6; ++i) fext_knee[i] = jt[12 + i];
+    for (int a = 0; a < 3; ++a) fr.knee[a] += jt[18 + a];
+    ick.beta = jt[21]; ick.gamma = jt[22]; ick.u[0] = jt[23]; ick.u[1] = jt[24]; ick.u[2] = jt[25];
+    knee_pz = jt[26];
   } else {
     float tq[NL];
     joint_terms(P, lg, h, tq, dl);
@@ -1187,12 +1222,17 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
       for (int i = 0; i < 6; ++i) pin(Ic[k][i]);
   }
   float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float pbase[6];  // base body bias force (lane 0; 0 on lane 1)
+  AInertia Rg;     // base body inertia (lane 0)
   if constexpr (HW) {
     __syncthreads();  // R2
-    float o[36];
-    get4(help_lds().bias, threadIdx.x, o, 9);
+    float o[44];
+    get4(help_lds().bias, threadIdx.x, o, 11);
     for (int k = 0; k < NL; ++k)
       for (int i = 0; i < 6; ++i) pbias[k][i] = o[6 * k + i];
+    for (int i = 0; i < 6; ++i) pbase[i] = o[36 + i];
+    ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
+    if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
     if (P.self_coll) {
       float w[12];
       get4(help_lds().selfw, threadIdx.x, w, 3);
@@ -1200,6 +1240,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
     }
   } else {
     leg_bias(v, pbias);
+    base_body<K>(P, lg, v0, Rg, pbase);
     if (P.self_coll) {
       Forces fs = {};
       self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wk, wf, fs);
@@ -1229,18 +1270,8 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   float corner[3];
   ict.beta = ict.gamma = 0.f;
   if (leg == 0) {
-    AInertia Rg;
-    ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
-    if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
     ai_add(IA, Rg);
-    float hb[6];
-    ai_mul(Rg, v0, hb);
-    float x1[3], x2[3], x3[3];
-    cross(v0, hb, x1);
-    cross(v0 + 3, hb + 3, x2);
-    cross(v0, hb + 3, x3);
-    pAcc[0] += x1[0] + x2[0]; pAcc[1] += x1[1] + x2[1]; pAcc[2] += x1[2] + x2[2];
-    pAcc[3] += x3[0]; pAcc[4] += x3[1]; pAcc[5] += x3[2];
+    for (int i = 0; i < 6; ++i) pAcc[i] += pbase[i];
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dummy[2];
