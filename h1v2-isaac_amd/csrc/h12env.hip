@@ -1384,6 +1384,7 @@ struct EnvSt {
   float cmd[3], heading, cmd_time, push_t;
   float air, con, last_air, last_con;  // this lane's foot
   float epsum[H12_NREW];
+  float metric[2];                // command metrics error_vel_xy, error_vel_yaw (episode accumulators)
   int eplen, lag[3], since_reset, is_heading, is_standing;
   float origin[3];                // env origin (terrain tasks)
   int tcell;                      // terrain level | type << 16
@@ -1439,6 +1440,8 @@ H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvS
   for (int t = H12_NREW_FLAT; t < H12_NREW; ++t)
     s.epsum[t] = (Feat<K>::ext && P.rsl) ? ldf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e) : 0.f;
   s.push_t = (Feat<K>::ext && P.push) ? ldf(W, H12_F_PUSH_TIME, e) : 0.f;
+  s.metric[0] = ldf(W, H12_F_METRIC, e);
+  s.metric[1] = ldf(W, H12_F_METRIC + 1, e);
   s.eplen = ldi(W, H12_I_EPLEN, e);
   if (Feat<K>::terrain) {
     for (int i = 0; i < 3; ++i) s.origin[i] = ldf(W, H12_F_ORIGIN + i, e);
@@ -1516,6 +1519,7 @@ H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, co
     stf(W, H12_F_ANCHOR + 2 * q + 1, e, sg * s.lg.anc[q][1], 8 * leg + 2 * (qr - q));
     cm_real |= ((s.lg.cmask >> q) & 1) << qr;
   }
+  stf(W, H12_F_METRIC, e, lsel(s.metric[0], s.metric[1]), leg);
   stf(W, H12_F_AIR, e, s.air, leg);
   stf(W, H12_F_CONTACT, e, s.con, leg);
   stf(W, H12_F_LAST_AIR, e, s.last_air, leg);
@@ -1726,6 +1730,7 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
   s.since_reset = 0;
   s.air = s.con = s.last_air = s.last_con = 0.f;
   for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = 0.f;
+  s.metric[0] = s.metric[1] = 0.f;  // CommandTerm.reset
   s.eplen = 0;
   if (Feat<K>::ext && P.push) {  // EventManager.reset: a new push interval for the reset envs
     uint32_t r3[4];
@@ -1748,6 +1753,21 @@ H12_DEV void base_com_vel(const KParams& P, const EnvSt& s, const float R[3][3],
   mv(R, c, cw);
   cross(ww, cw, wxc);
   for (int a = 0; a < 3; ++a) vcom[a] = s.b.vlin[a] + wxc[a];
+}
+
+// UniformVelocityCommand._update_metrics (IsaacLab 2.1): per step, |v*_xy - v_b,xy| and |w*_z - w_b,z| / (the
+// resampling time range's upper end in steps), v_b = root_lin_vel_b (COM velocity in the base frame), w_b the
+// base angular velocity; CommandTerm.reset logs their means over the reset envs and zeroes them (env_reset).
+template <int K>
+H12_DEV void cmd_metrics(const KParams& P, EnvSt& s) {
+  float R[3][3], vcom[3], vb[3];
+  quat_R(s.b.quat, R);
+  base_com_vel<K>(P, s, R, vcom);
+  mtv(R, vcom, vb);
+  const float ex = s.cmd[0] - vb[0], ey = s.cmd[1] - vb[1];
+  const float w = P.step_dt * frcp(P.cmd_T1);  // 1 / max_command_step
+  s.metric[0] += fsqrt(ex * ex + ey * ey) * w;
+  s.metric[1] += fabsf(s.cmd[2] - s.b.wang[2]) * w;
 }
 
 // this lane's part of the new (noise-free) observation frame, real coordinates, into the frame
@@ -2320,11 +2340,15 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       atomicAdd(&A.log_acc[H12_NREW], 1.f);
       if (tout) atomicAdd(&A.log_acc[H12_NREW + 1], 1.f);
       if (term) atomicAdd(&A.log_acc[H12_NREW + 2], 1.f);
+      atomicAdd(&A.log_acc[H12_LOG_METRIC], s.metric[0]);  // CommandTerm.reset: metrics of the ended episode
+      atomicAdd(&A.log_acc[H12_LOG_METRIC + 1], s.metric[1]);
     }
     PH(4);
     if (reset) env_reset<K>(P, s, leg, g, A.lo, A.hi);
     else s.since_reset = min(s.since_reset + 1, 2);
-    // ---- CommandTerm.compute(step_dt)
+    // ---- CommandTerm.compute(step_dt): UniformVelocityCommand._update_metrics on the post-reset state, then
+    // the resampling clock
+    cmd_metrics<K>(P, s);
     s.cmd_time -= P.step_dt;
     if (s.cmd_time <= 0.f) cmd_resample(P, s, g, A.lo, A.hi);
     if (Feat<K>::ext && P.dz) {

@@ -18,9 +18,11 @@ NREW = 20        # reward terms the kernel implements (REWARD_FUNCS)
 NREW_FLAT = 12   # terms 0-11: the Flat / Rough tables
 NCSTR = 10       # CaT constraint terms (CONSTRAINT_TERMS)
 NCSTR_COLS = 56
-NLOG = 44        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare,
-                 # then per constraint term the summed violation rates (10) and mean probabilities (10)
-ABI_VERSION = 6
+NLOG = 46        # log accumulator: NREW episode sums, count, time-out count, base-contact count, spare,
+                 # then per constraint term the summed violation rates (10) and mean probabilities (10),
+                 # then the summed command metrics error_vel_xy, error_vel_yaw (LOG_METRIC)
+LOG_METRIC = 44
+ABI_VERSION = 7
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -36,8 +38,8 @@ F = dict(POS=(0, 3), QUAT=(3, 4), VLIN=(7, 3), WANG=(10, 3), Q=(13, 12), QD=(25,
          ACT_PREV=(49, 12), CMD=(61, 3), HEADING=(64, 1), CMD_TIME=(65, 1), AIR=(66, 2), CONTACT=(68, 2),
          LAST_AIR=(70, 2), LAST_CONTACT=(72, 2), EPSUM=(74, 12), ANCHOR=(86, 16), ORIGIN=(102, 3), MU=(105, 4),
          DMASS=(109, 1), EPSUM2=(110, 8), PUSH_TIME=(118, 1), CSTR_SUM=(119, 10), CSTR_P=(129, 10),
-         SWING_H=(139, 2))
-NF_FLOAT = 141
+         SWING_H=(139, 2), METRIC=(141, 2))
+NF_FLOAT = 143
 I = dict(EPLEN=(0, 1), PACK=(1, 1), TERRAIN=(2, 1))
 NF_INT = 3
 

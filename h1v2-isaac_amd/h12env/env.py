@@ -24,12 +24,13 @@ import torch
 
 from . import _abi
 from ._abi import F as FIELDS
-from ._abi import NCSTR, NF_FLOAT, NF_INT, NJ, NLOG, NOBS_ROUGH, NREW, H12StepOut, check, load_library
+from ._abi import LOG_METRIC, NCSTR, NF_FLOAT, NF_INT, NJ, NLOG, NOBS_ROUGH, NREW, H12StepOut, check, load_library
 from .cfg import H12FlatEnvCfg
 from .model import body_names, build_model, joint_names
 
 _LOG_RING = 128   # log accumulator slots (zeroed in chunks, see _log_slot)
 _LOG_CHUNK = 32
+_LOG_LOOKBACK = _LOG_RING - 2 * _LOG_CHUNK  # persistence of extras["log"] (see _LazyLog)
 
 
 def env_origins_grid(num_envs: int, spacing: float, device) -> torch.Tensor:
@@ -43,38 +44,63 @@ def env_origins_grid(num_envs: int, spacing: float, device) -> torch.Tensor:
     return origins
 
 
-class _LazyLog(dict):
-    """extras["log"]: IsaacLab's Episode_Reward/* and Episode_Termination/* values, materialised on
-    first access from the step's device-side accumulator (no host sync inside step())."""
+def _raw_stream(dev_index: int) -> int:
+    """The current HIP stream of the device as a raw pointer (what torch.cuda.current_stream().cuda_stream
+    returns, without building a Stream object on every step)."""
+    return torch._C._cuda_getCurrentRawStream(dev_index)
 
-    def __init__(self, acc: torch.Tensor, max_episode_length_s: float, terms: list, term_map: torch.Tensor,
-                 cstr: list | None = None, extra: dict | None = None):
+
+class _LazyLog(dict):
+    """extras["log"]: IsaacLab's Episode_Reward/*, Episode_Termination/* and Metrics/base_velocity/* values,
+    materialised on first access from the step's device-side accumulator (no host sync inside step()).
+
+    Persistence (cat_env.py:217-245 / ManagerBasedRLEnv.step): the reference rebuilds extras["log"] only in
+    _reset_idx, i.e. on steps where some env resets; on a step without resets extras["log"] still holds the last
+    such step's values.  On materialisation the log therefore reads the most recent accumulator slot, this
+    step's or an earlier one within _LOG_LOOKBACK steps, that counts a reset (device-side gather, no host sync;
+    nothing is kept alive or computed per step for logs nobody reads)."""
+
+    def __init__(self, ring: torch.Tensor, slot: int, max_episode_length_s: float, terms: list, term_map: torch.Tensor,
+                 cstr: list | None = None, extra: dict | None = None, lookback: int = 1):
         super().__init__()
-        self._acc = acc
+        self._ring = ring
+        self._slot = slot
+        self._lookback = lookback
         self._T = max_episode_length_s
         self._terms = terms          # [(cfg name, kernel ids)] in RewardManager order
         self._map = term_map         # (terms, NREW) 0/1: a cfg term sums its kernel ids
         self._cstr = cstr or []      # [(constraint name, kernel constraint id)]
         self._extra = extra or {}
-        self._keys = [f"Episode_Reward/{t}" for t, _ in terms] + [
-            "Episode_Termination/time_out", "Episode_Termination/base_contact"]
-        self._keys += [f"Episode_Constraint_violation/{c}" for c, _ in self._cstr]
-        self._keys += [f"Episode_Constraint_probability/{c}" for c, _ in self._cstr]
-        self._keys += list(self._extra)
+        self._keys = None  # built on first access (step() stays cheap for logs nobody reads)
         self._done = False
+
+    def _key_list(self):
+        if self._keys is None:
+            keys = [f"Episode_Reward/{t}" for t, _ in self._terms]
+            keys += [f"Episode_Constraint_violation/{c}" for c, _ in self._cstr]
+            keys += [f"Episode_Constraint_probability/{c}" for c, _ in self._cstr]
+            keys += ["Metrics/base_velocity/error_vel_xy", "Metrics/base_velocity/error_vel_yaw",
+                     "Episode_Termination/time_out", "Episode_Termination/base_contact"]
+            self._nt = len(keys)
+            self._keys = keys + list(self._extra)
+        return self._keys
 
     def _fill(self):
         if self._done:
             return
-        a = self._acc
+        ring = self._ring
+        idx = (self._slot - torch.arange(self._lookback, device=ring.device)) % ring.shape[0]
+        k = torch.argmax((ring[idx, NREW] > 0).to(torch.int32)).view(1)  # first slot counting a reset (0 if none)
+        a = ring.index_select(0, idx.index_select(0, k))[0]  # device-side gather (a tensor index would sync)
         n = a[NREW].clamp(min=1.0)
-        parts = [self._map @ a[:NREW] / n / self._T, a[NREW + 1:NREW + 3]]
+        parts = [self._map @ a[:NREW] / n / self._T]
         if self._cstr:
             cid = torch.tensor([k for _, k in self._cstr], device=a.device, dtype=torch.long)
             parts += [a[NREW + 4 + cid] / n * 100.0, a[NREW + 4 + NCSTR + cid] / n]
+        parts += [a[LOG_METRIC:LOG_METRIC + 2] / n, a[NREW + 1:NREW + 3]]
         vals = torch.cat(parts)
-        nt = len(self._terms) + 2 + 2 * len(self._cstr)
-        for i, k in enumerate(self._keys[:nt]):
+        keys = self._key_list()
+        for i, k in enumerate(keys[:self._nt]):
             dict.__setitem__(self, k, vals[i])
         for k, f in self._extra.items():
             dict.__setitem__(self, k, f())
@@ -101,10 +127,10 @@ class _LazyLog(dict):
         return dict.__iter__(self)
 
     def __len__(self):
-        return len(self._keys)
+        return len(self._key_list())
 
     def __contains__(self, k):
-        return k in self._keys
+        return k in self._key_list()
 
 
 class _ObservationManager:
@@ -265,11 +291,11 @@ class H12VelocityEnv:
         self.reset_time_outs = torch.zeros(n, dtype=torch.bool, device=self.device)
         self.reset_buf = self.reset_terminated
         self._log_ring = torch.zeros(_LOG_RING, NLOG, device=self.device)
-        self._live_logs: dict = {}  # ring slot -> weakref of the _LazyLog reading it
+        self._live_logs: dict = {}  # creation step -> weakref of the _LazyLog reading the ring
         self._applied_torque = torch.zeros(n, NJ, device=self.device)
         # |net contact force| of the left / right foot over the last physics step (ContactSensor of the feet)
         self.foot_contact_force = torch.zeros(n, 2, device=self.device)
-        self._out = H12StepOut()
+        self._step_outs = []  # per observation buffer: (H12StepOut, byref), see _build_step_outs
         self.common_step_counter = 0
         self.extras: dict = {}
         self.terrain = None
@@ -293,6 +319,7 @@ class H12VelocityEnv:
         if self._cat:
             self.constraint_manager = _ConstraintManager(self)
             self._dones = torch.zeros(n, device=self.device)
+        self._build_step_outs()
         self._data = _ArticulationData(self)
         self.scene.articulations = {"robot": SimpleNamespace(data=self._data, joint_names=self._data.joint_names,
                                                              body_names=self._data.body_names,
@@ -300,6 +327,26 @@ class H12VelocityEnv:
         self.scene.__dict__["robot"] = self.scene.articulations["robot"]
         self._configure_spaces()
         self._closed = False
+
+    def _build_step_outs(self):
+        self._dev_index = self.device.index or 0
+        self._act_shape = torch.Size((self.num_envs, NJ))
+        """h12env_step output structs, one per observation buffer (their pointers never change), the log ring's
+        base pointer and the log's extra terms: step() then only sets the log slot."""
+        self._step_outs = []
+        for k in range(2):
+            o = H12StepOut()
+            o.obs = self._obs[k].data_ptr()
+            o.rew = self.reward_buf.data_ptr()
+            o.terminated = self.reset_terminated.data_ptr()
+            o.truncated = self.reset_time_outs.data_ptr()
+            o.applied_torque = self._applied_torque.data_ptr()
+            o.foot_force = self.foot_contact_force.data_ptr()
+            o.cstr_prob = self._dones.data_ptr() if self._cat else None
+            self._step_outs.append((o, C.byref(o)))
+        self._log_ptr = self._log_ring.data_ptr()
+        self._log_extra = ({"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()}
+                           if self.terrain is not None else None)
 
     # ------------------------------------------------------------------ properties (ManagerBasedEnv)
     @property
@@ -460,10 +507,10 @@ class H12VelocityEnv:
         return {"policy": obs.clone() if self.obs_copy else obs}, self.extras
 
     def step(self, action: torch.Tensor):
-        a = action.to(device=self.device, dtype=torch.float32)
-        if not a.is_contiguous():
-            a = a.contiguous()
-        if a.shape != (self.num_envs, NJ):
+        a = action
+        if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != self._act_shape:
             raise ValueError(f"actions must be ({self.num_envs}, {NJ}), got {tuple(a.shape)}")
         self.common_step_counter += 1
         if self._rw_pending:
@@ -475,31 +522,29 @@ class H12VelocityEnv:
         obs = self._obs[self._k]
         slot = self.common_step_counter % _LOG_RING
         if slot % _LOG_CHUNK == 0:
-            # a step's _LazyLog reads its slot lazily: materialise (device ops, no sync) every log still
-            # alive in the chunk before the chunk is recycled
-            for s0 in range(slot, slot + _LOG_CHUNK):
-                ref = self._live_logs.pop(s0, None)
-                log = ref() if ref is not None else None
-                if log is not None:
+            # a step's _LazyLog reads the ring lazily (its slot, or up to _LOG_LOOKBACK - 1 earlier ones): the
+            # chunk recycled now held steps C - RING .. C - RING + CHUNK - 1, so every log still alive whose window
+            # reaches into it (created at step <= C - RING + CHUNK + LOOKBACK - 2) is materialised first (device
+            # ops, no sync); newer logs, e.g. the one extras still holds, are left lazy
+            c = self.common_step_counter
+            for t0 in list(self._live_logs):
+                log = self._live_logs[t0]()
+                if log is None:
+                    del self._live_logs[t0]
+                elif t0 <= c - _LOG_RING + _LOG_CHUNK + _LOG_LOOKBACK - 2:
                     log._fill()
+                    del self._live_logs[t0]
             self._log_ring[slot:slot + _LOG_CHUNK].zero_()
-        acc = self._log_ring[slot]
-        o = self._out
-        o.obs = obs.data_ptr()
-        o.rew = self.reward_buf.data_ptr()
-        o.terminated = self.reset_terminated.data_ptr()
-        o.truncated = self.reset_time_outs.data_ptr()
-        o.log_acc = acc.data_ptr()
-        o.applied_torque = self._applied_torque.data_ptr()
-        o.foot_force = self.foot_contact_force.data_ptr()
-        o.cstr_prob = self._dones.data_ptr() if self._cat else None
-        rc = self._lib.h12env_step(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(prev.data_ptr()), C.byref(o),
-                                   self.common_step_counter, self._stream())
+        # the output pointers are fixed per observation buffer (built once, _step_outs); only the log slot moves
+        o, o_ref = self._step_outs[self._k]
+        o.log_acc = self._log_ptr + slot * (NLOG * 4)
+        rc = self._lib.h12env_step(self._h, a.data_ptr(), prev.data_ptr(), o_ref, self.common_step_counter,
+                                   _raw_stream(self._dev_index))
         if rc:
             check(self._lib, rc, "h12env_step")
-        extra = {"Curriculum/terrain_levels": lambda: self.terrain_levels().mean()} if self.terrain is not None else None
-        log = _LazyLog(acc, self.max_episode_length_s, self._reward_terms, self._reward_map, self._cstr_terms, extra)
-        self._live_logs[slot] = weakref.ref(log)
+        log = _LazyLog(self._log_ring, slot, self.max_episode_length_s, self._reward_terms, self._reward_map,
+                       self._cstr_terms, self._log_extra, _LOG_LOOKBACK)
+        self._live_logs[self.common_step_counter] = weakref.ref(log)
         self.extras = {"log": log, "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
         if self._cat:  # CaTEnv.step: dones = constraint termination probability, 1 where reset (cat_env.py:153-193)

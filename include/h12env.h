@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 6
+#define H12ENV_ABI_VERSION 7
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -50,9 +50,11 @@ extern "C" {
 #define H12_NREW_FLAT 12   /* terms 0-11: the Flat / Rough tables */
 #define H12_NCSTR 10       /* CaT constraint terms (cat_env_cfg.py:336-427, ConstraintsCfg order) */
 #define H12_NCSTR_COLS 56  /* their columns: 1 + 12 + 12 + 12 + 2 + 12 + 1 + 1 + 1 + 2 */
-#define H12_NLOG 44        /* log accumulator: 20 episode reward sums, reset count, time-out / base-contact counts,
+#define H12_NLOG 46        /* log accumulator: 20 episode reward sums, reset count, time-out / base-contact counts,
                               spare, then per constraint term the sums over reset envs of the episode's
-                              violation rate (10) and mean probability (10) */
+                              violation rate (10) and mean probability (10), then (ABI 7) the sums over reset
+                              envs of the command metrics error_vel_xy, error_vel_yaw (H12_LOG_METRIC) */
+#define H12_LOG_METRIC 44  /* UniformVelocityCommand._update_metrics accumulators, logged by CommandTerm.reset */
 /* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:128-188): no history, base_lin_vel
  * first, height scan last (velocity_env_cfg.py:118-137) */
 #define H12_ROUGH_FRAME 48 /* lin_vel 3, ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -276,7 +278,8 @@ enum {
   H12_F_CSTR_SUM = 119, /* 10 CaT: episode count of steps with the term violated (max prob > 0) */
   H12_F_CSTR_P = 129,   /* 10 CaT: episode sum of the term's max probability */
   H12_F_SWING_H = 139,  /* 2  CaT foot_clearance: max foot height of the current swing (left, right) */
-  H12_NF_FLOAT = 141
+  H12_F_METRIC = 141,   /* 2  (ABI 7) command metrics error_vel_xy, error_vel_yaw of the episode (base_velocity) */
+  H12_NF_FLOAT = 143
 };
 enum {
   H12_I_EPLEN = 0,      /* episode_length_buf (int32) */

@@ -922,6 +922,7 @@ typedef struct orc_env {
   orc_phys p;
   double act[NJ], act_prev[NJ], cmd[3], heading, cmd_time, air[2], con[2], last_air[2], last_con[2], epsum[H12_NREW];
   double push_t;
+  double metric[2]; /* UniformVelocityCommand metrics error_vel_xy, error_vel_yaw */
   int eplen, lag[3], since_reset, is_heading, is_standing;
   double origin[3];
   int32_t tcell; /* terrain level | type << 16 */
@@ -962,6 +963,7 @@ static void env_load(const float* F, const int32_t* I, int n, int i, orc_env* e)
   LD(e->epsum, H12_F_EPSUM, H12_NREW_FLAT);
   LD(e->epsum + H12_NREW_FLAT, H12_F_EPSUM2, H12_NREW - H12_NREW_FLAT);
   LD(&e->push_t, H12_F_PUSH_TIME, 1);
+  LD(e->metric, H12_F_METRIC, 2);
   LD(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
 #undef LD
   e->eplen = I[(size_t)H12_I_EPLEN * n + i];
@@ -982,6 +984,7 @@ static void env_store(float* F, int32_t* I, int n, int i, const orc_env* e) {
   ST(e->epsum, H12_F_EPSUM, H12_NREW_FLAT);
   ST(e->epsum + H12_NREW_FLAT, H12_F_EPSUM2, H12_NREW - H12_NREW_FLAT);
   ST(&e->push_t, H12_F_PUSH_TIME, 1);
+  ST(e->metric, H12_F_METRIC, 2);
   ST(&e->p.anchor[0][0][0], H12_F_ANCHOR, 2 * H12_NFOOT_PTS * 2);
 #undef ST
   I[(size_t)H12_I_EPLEN * n + i] = e->eplen;
@@ -1152,6 +1155,7 @@ static void env_reset_one(const h12env_model* m, const h12env_config* c, orc_env
   memset(e->last_air, 0, sizeof e->last_air);
   memset(e->last_con, 0, sizeof e->last_con);
   memset(e->epsum, 0, sizeof e->epsum);
+  memset(e->metric, 0, sizeof e->metric); /* CommandTerm.reset */
   e->eplen = 0;
   if (c->push_enable) { /* EventManager.reset: new interval for the reset envs */
     uint32_t r3[4];
@@ -1752,13 +1756,28 @@ int orc_env_step(const h12env_model* m, const h12env_config* c, int n, int64_t e
           log_acc[H12_NREW] += 1.0f;
           log_acc[H12_NREW + 1] += (float)tout;
           log_acc[H12_NREW + 2] += (float)term;
+          /* CommandTerm.reset: the ended episode's command metrics (mean over the reset envs on the host) */
+          log_acc[H12_LOG_METRIC] += (float)e.metric[0];
+          log_acc[H12_LOG_METRIC + 1] += (float)e.metric[1];
         }
       }
       env_reset_one(m, c, &e, g, lo, hi);
     } else {
       e.since_reset = e.since_reset < 2 ? e.since_reset + 1 : 2;
     }
-    /* CommandTerm.compute(dt) */
+    /* CommandTerm.compute(dt): UniformVelocityCommand._update_metrics on the post-reset state (IsaacLab 2.1:
+     * |v*_xy - root_lin_vel_b,xy| and |w*_z - root_ang_vel_b,z| over max_command_step =
+     * resampling_time_range[1] / step_dt), then the resampling clock */
+    {
+      m3 R;
+      quat_to_R(e.p.quat, R);
+      double vcom[3], vb[3];
+      base_com_vel(m, &e.p, R, vcom);
+      m3tv(R, vcom, vb);
+      const double mcs = c->cmd_resample_time_max / step_dt;
+      e.metric[0] += sqrt(sq(e.cmd[0] - vb[0]) + sq(e.cmd[1] - vb[1])) / mcs;
+      e.metric[1] += fabs(e.cmd[2] - e.p.wang[2]) / mcs;
+    }
     e.cmd_time = (float)(e.cmd_time - step_dt);
     if (e.cmd_time <= 0) cmd_resample(c, &e, g, lo, hi, 0);
     cmd_update(c, &e, g, lo, hi, dz_prev, n);

@@ -62,7 +62,7 @@ SELF_JITTER = (1e-7,) * 32 + (1e-6,) * 64 + (3e-6,) * 64
 SELF_AMPLIFY = 1e-6
 PERTURBS = (1e-7,) * 16 + (1e-6,) * 32 + (3e-6,) * 64 + (1e-5,) * 128
 PHYS = ("POS", "QUAT", "VLIN", "WANG", "Q", "QD")
-TERMS = ("EPSUM", "EPSUM2")  # episode sums of the 20 kernel reward terms (12 Flat + 8 Rsl)
+TERMS = ("EPSUM", "EPSUM2", "METRIC")  # episode sums of the 20 kernel reward terms (12 Flat + 8 Rsl), command metrics
 CRITERIA = ("phys", "flags", "ints", "rew", "terms", "obs")
 
 

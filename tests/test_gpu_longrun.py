@@ -18,7 +18,7 @@ import torch
 from forced import ForcedParity
 from h12env import H12FlatEnvCfg
 from h12env._abi import F as FIELDS
-from h12env._abi import NREW
+from h12env._abi import LOG_METRIC, NREW
 from h12env.env import H12VelocityEnv
 
 pytestmark = pytest.mark.gpu
@@ -58,9 +58,12 @@ def test_teacher_forced_flat_4096x1100(gpu):
             # log accumulator of this step's resetting envs (episode sums, count, time-out / base-contact counts)
             acc = env._log_ring[env.common_step_counter % len(env._log_ring)].cpu().numpy()
             lo = info["log"]
-            k = NREW + 3
-            np.testing.assert_allclose(acc[:k], lo[:k], rtol=1e-4, atol=1e-4 * max(1.0, float(np.abs(lo[:k]).max())),
+            k = list(range(NREW + 3)) + [LOG_METRIC, LOG_METRIC + 1]  # + the command metrics (ABI 7)
+            np.testing.assert_allclose(acc[k], lo[k], rtol=1e-4, atol=1e-4 * max(1.0, float(np.abs(lo[k]).max())),
                                        err_msg=f"episode log at step {t + 1}")
+            el = ex["log"]
+            np.testing.assert_allclose(float(el["Metrics/base_velocity/error_vel_xy"]), lo[LOG_METRIC] / lo[NREW],
+                                       rtol=1e-4, atol=1e-6)
             cov["log_steps"] += 1
         if (t + 1) % 100 == 0:
             print(f"[forced] step {t + 1}: {cov} explained {fp.explained} unexplained {len(fp.unexplained)}", flush=True)
