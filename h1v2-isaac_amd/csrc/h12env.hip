@@ -1743,11 +1743,8 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
 // root (composite COM) linear velocity in world: v_origin + w x (R c); c moves with the added torso mass
 template <int K>
 H12_DEV void base_com_vel(const KParams& P, const EnvSt& s, const float R[3][3], float* vcom) {
-  float c[3] = {h12m::BASE_COM[0], h12m::BASE_COM[1], h12m::BASE_COM[2]};
-  if (Feat<K>::ext && P.env_mass) {
-    float dm = s.lg.dmass, im = frcp(h12m::BASE_M + dm);
-    for (int a = 0; a < 3; ++a) c[a] = (h12m::BASE_MC[a] + dm * h12m::TORSO_COM[a]) * im;
-  }
+  // the pelvis rigid body's own COM (the added torso mass sits on torso_link, another rigid body)
+  const float c[3] = {h12m::ROOT_COM[0], h12m::ROOT_COM[1], h12m::ROOT_COM[2]};
   float ww[3], cw[3], wxc[3];
   mv(R, s.b.wang, ww);
   mv(R, c, cw);
@@ -2724,7 +2721,9 @@ int check_model(const h12env_model* m) {
   if (!close(m->base_mass, h12m::BASE_M) || !close(m->base_com[0], h12m::BASE_COM[0]) ||
       !close(m->base_com[2], h12m::BASE_COM[2]) || !close(m->foot_radius, h12m::FOOT_R) ||
       !close(m->knee_radius, h12m::KNEE_R) || !close(m->torso_com[0], h12m::TORSO_COM[0]) ||
-      !close(m->torso_com[1], h12m::TORSO_COM[1]) || !close(m->torso_com[2], h12m::TORSO_COM[2]))
+      !close(m->torso_com[1], h12m::TORSO_COM[1]) || !close(m->torso_com[2], h12m::TORSO_COM[2]) ||
+      !close(m->root_com[0], h12m::ROOT_COM[0]) || !close(m->root_com[1], h12m::ROOT_COM[1]) ||
+      !close(m->root_com[2], h12m::ROOT_COM[2]))
     return set_err(H12_E_ARG, "base / contact geometry differs from the compiled H1-2 model");
   for (int r = 0; r < 4; ++r)
     for (int e = 0; e < 2; ++e)

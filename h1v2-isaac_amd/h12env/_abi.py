@@ -98,6 +98,7 @@ class H12Model(C.Structure):
         ("gravity", f32),
         ("torso_com", f32 * 3),
         ("foot_rods", f32 * 3 * 2 * 4),
+        ("root_com", f32 * 3),
     ]
 
 

@@ -46,6 +46,8 @@ def build_model() -> H12Model:
         m.damping[j] = d["joint_defaults"]["damping"]
         m.frictionloss[j] = d["joint_defaults"]["frictionloss"]
         m.q_default[j] = DEFAULT_JOINT_POS[j]
+    for a in range(3):
+        m.root_com[a] = d["root_com"][a]
     m.base_mass = d["base"]["mass"]
     for a in range(3):
         m.base_com[a] = d["base"]["com"][a]

@@ -152,6 +152,9 @@ typedef struct h12env_model {
   /* ABI 6: the four sole rods (URDF cylinders r = foot_radius, h12_12dof.urdf:168-191) as segments in the
    * ankle-roll frame: heel, toe, two side rods (self-collision capsules) */
   float foot_rods[4][2][3];
+  /* ABI 7: COM of the pelvis rigid body alone (base frame, h12_12dof.xml pelvis <inertial>): IsaacLab's
+   * root_lin_vel_w is the root body's COM velocity, and the USD keeps torso_link / arms as separate bodies */
+  float root_com[3];
 } h12env_model;
 
 /* Task / simulation configuration. h12env_config_default() fills the Flat-H12_12dof values. */

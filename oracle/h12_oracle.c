@@ -1228,11 +1228,11 @@ static void obs_write(const double fr[H12_OBS_FRAME], const float* prev, float* 
   }
 }
 
-/* root (composite COM) linear velocity in world; the COM moves with the added torso mass */
+/* root_lin_vel_w: the linear velocity of the root rigid body's COM (the pelvis body alone, model root_com;
+ * IsaacLab ArticulationData.root_com_vel_w) in world axes */
 static void base_com_vel(const h12env_model* m, const orc_phys* p, const m3 R, double vcom[3]) {
-  double c[3], M = m->base_mass + (p->env_params ? p->dmass : 0.0);
-  for (int a = 0; a < 3; ++a)
-    c[a] = (m->base_mass * m->base_com[a] + (p->env_params ? p->dmass * m->torso_com[a] : 0.0)) / M;
+  (void)p->dmass;  /* the added torso mass sits on torso_link, another rigid body */
+  const double c[3] = {m->root_com[0], m->root_com[1], m->root_com[2]};
   double wb[3] = {p->wang[0], p->wang[1], p->wang[2]}, ww[3], cw[3], wxc[3];
   m3v(R, wb, ww);
   m3v(R, c, cw);

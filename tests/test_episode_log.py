@@ -73,8 +73,8 @@ def test_oracle_command_metrics(model):
         R = np.array([[1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy - qw * qz), 2 * (qx * qz + qw * qy)],
                       [2 * (qx * qy + qw * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz - qw * qx)],
                       [2 * (qx * qz - qw * qy), 2 * (qy * qz + qw * qx), 1 - 2 * (qx * qx + qy * qy)]])
-        c = np.asarray(model.base_com, dtype=np.float64)
-        vcom = v[i] + np.cross(R @ w[i], R @ c)  # root_lin_vel_w: the composite COM's velocity
+        c = np.asarray(model.root_com, dtype=np.float64)
+        vcom = v[i] + np.cross(R @ w[i], R @ c)  # root_lin_vel_w: the pelvis body COM velocity
         vb = R.T @ vcom
         cmd = F0[FIELDS["CMD"][0]:FIELDS["CMD"][0] + 3, i].astype(np.float64)
         d = env.F[o:o + 2, i] - F0[o:o + 2, i]

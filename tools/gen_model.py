@@ -204,6 +204,10 @@ def main():
         # torso_link is welded to the pelvis at the pelvis origin (no pos attribute, h12_12dof.xml:143)
         "torso_link": {"pos": [0.0, 0.0, 0.0], "com": inertial_of(pelvis.find(".//body[@name='torso_link']"))[1].tolist()},
         "gravity": 9.81,
+        # the pelvis rigid body's own COM (pelvis frame): IsaacLab's root_com_* quantities (root_lin_vel_w / _b) are
+        # those of the articulation's root body, and the USD keeps torso_link as a separate rigid body (the tasks
+        # address it by name, cat_env_cfg.py:246,258)
+        "root_com": inertial_of(pelvis)[1].tolist(),
     }
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(model, indent=1))
