@@ -39,6 +39,10 @@ namespace {
 constexpr int NJ = H12_NJ;
 constexpr int NL = 6;               // links per leg
 constexpr int ENVS_PER_BLOCK = 32;  // 64 lanes = 32 lane pairs
+// episode-log values step_kernel accumulates (the rest of the H12_NLOG slots are CaT's, added by cat_prob_kernel):
+// reward sums, reset count, time-out / base-contact counts, command metrics.  Partial slot pv -> log slot:
+constexpr int LOG_NPART = H12_NREW + 3 + 2;
+__host__ __device__ constexpr int log_slot(int pv) { return pv < H12_NREW + 3 ? pv : H12_LOG_METRIC + (pv - H12_NREW - 3); }
 constexpr int BLOCK = 64;
 // joint axes per leg link: hip yaw z, hip pitch y, hip roll x, knee y, ankle pitch y, ankle roll x
 constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
@@ -1857,8 +1861,33 @@ struct AsmArgs {
   int n;
   int64_t env_offset;
   uint32_t lo, hi;
+  float* log_part;  // step_kernel's per-block episode-log partials ([LOG_NPART][log_nb]) ...
+  float* log_acc;   // ... folded into the caller's accumulator by block 0 (null: nothing to fold)
+  int log_nb;
 };
 constexpr int ASM_BLOCK = 256;
+
+// Episode-log fold, in the assembly kernel: block pv < LOG_NPART (its first wave) sums step_kernel's partials of
+// value pv over the step's blocks into log_acc[log_slot(pv)] and zeroes them for the next step (stream order:
+// step_kernel wrote them, the next step_kernel starts after this kernel).  The loads are issued when the block
+// starts (log_load) and consumed when it ends (log_fold), so their round trip hides behind the block's own work.
+H12_DEV bool log_block(const AsmArgs& A) { return A.log_acc && blockIdx.x < LOG_NPART && threadIdx.x < 64; }
+H12_DEV float log_load(const AsmArgs& A) {
+  float acc = 0.f;
+  if (log_block(A)) {
+    const float* q = A.log_part + (size_t)blockIdx.x * A.log_nb;
+    for (int b = threadIdx.x; b < A.log_nb; b += 64) acc += q[b];
+  }
+  return acc;
+}
+H12_DEV void log_fold(const AsmArgs& A, float acc) {
+  if (!log_block(A)) return;
+  float* q = A.log_part + (size_t)blockIdx.x * A.log_nb;
+  for (int b = threadIdx.x; b < A.log_nb; b += 64) q[b] = 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (threadIdx.x == 0 && acc != 0.f) A.log_acc[log_slot(blockIdx.x)] += acc;
+}
 #ifndef H12_ASM_ROWS
 #define H12_ASM_ROWS 4
 #endif
@@ -1901,7 +1930,7 @@ H12_DEV uint32_t asm_col_entry(int col) {
 
 // NH: history length (10 Flat, 6 Rsl); the row is 45 * NH floats
 template <int NH>
-__global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
+H12_DEV void obs_assemble_body(const KParams& P, const AsmArgs& A) {
   constexpr int ROW = H12_OBS_FRAME * NH;
   constexpr int ASM_F4 = ASM_ROWS * ROW / 4;
   constexpr int ASM_CHUNKS = (ASM_F4 + 63) / 64;  // 1 KB LDS-DMA chunks (64 lanes x 16 B) per block
@@ -2039,6 +2068,12 @@ __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmA
     }
   }
 }
+template <int NH>
+__global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
+  const float lacc = log_load(A);
+  obs_assemble_body<NH>(P, A);
+  log_fold(A, lacc);
+}
 
 // Rough task observation (no history): one thread per (env, element) of the 235-float row --
 // base_lin_vel, base_ang_vel, projected_gravity, velocity_commands, joint_pos_rel, joint_vel_rel,
@@ -2055,6 +2090,7 @@ H12_DEV float rough_noise(const KParams& P, const AsmArgs& A, int e, int t) {
 }
 
 __global__ void __launch_bounds__(ASM_BLOCK) rough_obs_kernel(KParams P, AsmArgs A) {
+  log_fold(A, log_load(A));
   const int n = A.n;
   const int gid = blockIdx.x * ASM_BLOCK + threadIdx.x;
   if (gid >= n * H12_NOBS_ROUGH) return;
@@ -2202,7 +2238,7 @@ struct StepArgs {
   float* rew;
   uint8_t* term;
   uint8_t* trunc;
-  float* log_acc;
+  float* log_part;  // [LOG_NPART][gridDim.x] per-block episode-log partials (handle-owned), or null: no log
   float* applied_torque;
   float* foot_force;
   const uint8_t* reset_mask;
@@ -2328,17 +2364,25 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       A.term[e] = (uint8_t)term;
       A.trunc[e] = (uint8_t)tout;
     }
+#ifndef H12_EXP_NO_OUT  // experiment builds only (tools/phase_profile.py --plain -D ...): price the optional outputs
     if (A.applied_torque)
       for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
+#endif
     // ---- episode log: the (few) resetting envs add their sums directly (no-return atomics)
-    if (A.log_acc && reset && leg == 0) {
-      for (int t = 0; t < NT; ++t) atomicAdd(&A.log_acc[t], s.epsum[t]);
-      atomicAdd(&A.log_acc[H12_NREW], 1.f);
-      if (tout) atomicAdd(&A.log_acc[H12_NREW + 1], 1.f);
-      if (term) atomicAdd(&A.log_acc[H12_NREW + 2], 1.f);
-      atomicAdd(&A.log_acc[H12_LOG_METRIC], s.metric[0]);  // CommandTerm.reset: metrics of the ended episode
-      atomicAdd(&A.log_acc[H12_LOG_METRIC + 1], s.metric[1]);
+    // into this block's own partial slots (value-major [LOG_NPART][blocks]): the wave's resetting lanes are summed
+    // by the compiler's wave reduction, one no-return atomic per value and block -- no two blocks share an address.
+    // (One shared accumulator made every wave's 17 atomics queue on the same two L2 lines: +4.2 us per step.)
+    // The assembly kernel that follows folds the partials into log_acc (log_load / log_fold).
+    if (A.log_part && reset && leg == 0) {
+      float* lp = A.log_part + blockIdx.x;
+      const int nb = gridDim.x;
+      for (int t = 0; t < NT; ++t) atomicAdd(&lp[t * nb], s.epsum[t]);
+      atomicAdd(&lp[H12_NREW * nb], 1.f);
+      if (tout) atomicAdd(&lp[(H12_NREW + 1) * nb], 1.f);
+      if (term) atomicAdd(&lp[(H12_NREW + 2) * nb], 1.f);
+      atomicAdd(&lp[(H12_NREW + 3) * nb], s.metric[0]);  // CommandTerm.reset: metrics of the ended episode
+      atomicAdd(&lp[(H12_NREW + 4) * nb], s.metric[1]);
     }
     PH(4);
     if (reset) env_reset<K>(P, s, leg, g, A.lo, A.hi);
@@ -2672,6 +2716,7 @@ struct Handle {
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
   int16_t* asm_tab = nullptr;  // obs_assemble_kernel gather table for P.hist (Flat / Rsl layouts)
+  float* log_part = nullptr;   // [LOG_NPART][step blocks] episode-log partials (step_kernel -> assembly kernel)
   // kernel timing: 4 events per timed step bound to the launches themselves (hipExtLaunchKernelGGL:
   // the events take the dispatch packet's begin / end timestamps, as rocprofv3's kernel trace does) --
   // step_kernel begin / end, observation kernel begin / end
@@ -2923,8 +2968,11 @@ int feature_level(const KParams& P) {
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
-                    hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+                    hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, float* log_acc = nullptr) {
   AsmArgs A = {};
+  A.log_part = h->log_part;
+  A.log_acc = log_acc;
+  A.log_nb = n_blocks(h);
   A.obs_prev = obs_prev;
   A.obs = obs;
   A.frame = h->frame;
@@ -3107,6 +3155,9 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   }
   e = hipMalloc(&h->dz_cnt, 3 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(h->dz_cnt, 0, 3 * sizeof(int));
+  const size_t log_bytes = sizeof(float) * LOG_NPART * (size_t)((n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK);
+  if (e == hipSuccess) e = hipMalloc(&h->log_part, log_bytes);
+  if (e == hipSuccess) e = hipMemset(h->log_part, 0, log_bytes);
   if (e != hipSuccess) {
     if (h->own) (void)hipFree(state_dev);
     (void)hipFree(h->frame);
@@ -3175,6 +3226,7 @@ void h12env_destroy(h12env* hh) {
   if (h->own && h->W.F) (void)hipFree(h->W.F);
   if (h->frame) (void)hipFree(h->frame);
   if (h->dz_cnt) (void)hipFree(h->dz_cnt);
+  if (h->log_part) (void)hipFree(h->log_part);
   if (h->cat_mem) (void)hipFree(h->cat_mem);
   if (h->asm_tab) (void)hipFree(h->asm_tab);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
@@ -3215,7 +3267,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.rew = out->rew;
   A.term = out->terminated;
   A.trunc = out->truncated;
-  A.log_acc = out->log_acc;
+  A.log_part = out->log_acc ? h->log_part : nullptr;
   A.applied_torque = out->applied_torque;
   A.foot_force = out->foot_force;
   A.env_offset = h->env_offset;
@@ -3243,7 +3295,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   timing_events(h, 1, &t0, &t1);
   // fill = terminated | truncated: the envs reset inside the step restart their history
   return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
-                         (hipStream_t)stream, t0, t1);
+                         (hipStream_t)stream, t0, t1, out->log_acc);
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {

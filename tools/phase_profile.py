@@ -31,14 +31,15 @@ SLOTS = {0: "loads", 1: "physics", 2: "sensor", 3: "rewards", 4: "outputs+log", 
          12: "inner: inertia chain", 13: "inner: wait R2 (bias, self-contacts)", 14: "inner: bias chain .. integration + S"}
 
 
-def build(tag: str, flags: list[str]) -> Path:
+def build(tag: str, flags: list[str], plain: bool = False) -> Path:
     from h12env.build import ARCH, CSRC, hipcc
 
     VARIANTS.mkdir(parents=True, exist_ok=True)
     out = VARIANTS / f"lib_{tag}.so"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
            "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros", "-fPIC", "-shared", "-Wno-unused-function",
-           "-DH12_PHASE_PROFILE", *[f"-D{f}" for f in flags], "-o", str(out), str(CSRC / "h12env.hip")]
+           *([] if plain else ["-DH12_PHASE_PROFILE"]), *[f"-D{f}" for f in flags], "-o", str(out),
+           str(CSRC / "h12env.hip")]
     print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     return out
@@ -89,9 +90,11 @@ def main():
     ap.add_argument("--burn-in", type=int, default=200)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--no-self-collision", action="store_true")
+    ap.add_argument("--plain", action="store_true", help="--build without the phase marks (an experiment variant "
+                    "for H12ENV_LIB=tools/_variants/lib_TAG.so python bench.py)")
     a = ap.parse_args()
     if a.build:
-        build(a.tag, a.defs)
+        build(a.tag, a.defs, a.plain)
         return
     res = run(a.tag, a.steps, a.burn_in, a.envs, not a.no_self_collision)
     print(json.dumps({"tag": a.tag, "envs": a.envs, "cycles_per_wave_per_env_step": res}))
