@@ -1371,14 +1371,17 @@ H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return __builtin_amdgcn_
 #else
 H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return ws_rsrc(base); }
 #endif
+H12_DEV __amdgpu_buffer_rsrc_t st_F(const Workspace& W) { return ws_rsrc_st(W.F); }
+H12_DEV __amdgpu_buffer_rsrc_t st_I(const Workspace& W) { return ws_rsrc_st(W.I); }
 H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), ws_rsrc_st(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), st_F(W), (e + lf * W.n) * 4, f * W.n * 4,
+                                        0);
 }
 H12_DEV int ldi(const Workspace& W, int f, int e) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
 }
 H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, ws_rsrc_st(W.I), (e + lf * W.n) * 4, f * W.n * 4, 0);
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, 0);
 }
 
 struct EnvSt {
@@ -1462,14 +1465,16 @@ H12_DEV void load_env(const KParams& P, const Workspace& W, int e, int leg, EnvS
   load_mdp<K>(P, W, e, leg, s);
 }
 
-template <int K>
+// PARTS: bit 0 the physics state (base pose / velocity, q, qd, stiction anchors), bit 1 everything else
+template <int K, int PARTS = 3>
 H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, const EnvSt& s) {
+  constexpr bool PH_ = PARTS & 1, RE_ = PARTS & 2;
   const float sg = leg ? -1.f : 1.f;
   // an opaque copy of n made here: the field offsets of the stores are then computed here, not shared with the
   // loads at the top of the kernel (68 SGPRs kept live across the physics loop spill to VGPR lanes)
   Workspace W = W0;
   asm volatile("" : "+s"(W.n));
-  if (Feat<K>::terrain && leg == 0) {
+  if (RE_ && Feat<K>::terrain && leg == 0) {
     for (int i = 0; i < 3; ++i) stf(W, H12_F_ORIGIN + i, e, s.origin[i]);
     sti(W, H12_I_TERRAIN, e, s.tcell);
   }
@@ -1489,40 +1494,51 @@ H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, co
                           s.b.vlin[0], s.b.vlin[1], s.b.vlin[2], s.b.wang[0], s.b.wang[1], s.b.wang[2]};
     static_assert(H12_F_QUAT == H12_F_POS + 3 && H12_F_VLIN == H12_F_POS + 7 && H12_F_WANG == H12_F_POS + 10,
                   "base fields contiguous");
+    if (PH_) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) stf(W, H12_F_POS + i, e, lsel(bb[i], bb[i + 7]), 7 * leg);
-    static_assert(H12_F_HEADING == H12_F_CMD + 3 && H12_F_CMD_TIME == H12_F_CMD + 4, "command fields contiguous");
-    stf(W, H12_F_CMD, e, lsel(s.cmd[0], s.heading), 3 * leg);
-    stf(W, H12_F_CMD + 1, e, lsel(s.cmd[1], s.cmd_time), 3 * leg);
-#pragma unroll
-    for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(s.epsum[t], s.epsum[t + 6]), 6 * leg);
-    if (Feat<K>::ext && P.rsl) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        stf(W, H12_F_EPSUM2 + t, e, lsel(s.epsum[H12_NREW_FLAT + t], s.epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+      for (int i = 0; i < 6; ++i) stf(W, H12_F_POS + i, e, lsel(bb[i], bb[i + 7]), 7 * leg);
+      if (leg == 0) stf(W, H12_F_POS + 6, e, bb[6]);
     }
-    if (leg == 0) {
-      stf(W, H12_F_POS + 6, e, bb[6]);
-      stf(W, H12_F_CMD + 2, e, s.cmd[2]);
-      if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
+    if (RE_) {
+      static_assert(H12_F_HEADING == H12_F_CMD + 3 && H12_F_CMD_TIME == H12_F_CMD + 4, "command fields contiguous");
+      stf(W, H12_F_CMD, e, lsel(s.cmd[0], s.heading), 3 * leg);
+      stf(W, H12_F_CMD + 1, e, lsel(s.cmd[1], s.cmd_time), 3 * leg);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(s.epsum[t], s.epsum[t + 6]), 6 * leg);
+      if (Feat<K>::ext && P.rsl) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          stf(W, H12_F_EPSUM2 + t, e, lsel(s.epsum[H12_NREW_FLAT + t], s.epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+      }
+      if (leg == 0) {
+        stf(W, H12_F_CMD + 2, e, s.cmd[2]);
+        if (Feat<K>::ext && P.push) stf(W, H12_F_PUSH_TIME, e, s.push_t);
+      }
     }
   }
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     float js = jsign(k, sg);
-    stf(W, H12_F_Q + k, e, js * s.lg.q[k], NL * leg);
-    stf(W, H12_F_QD + k, e, js * s.lg.qd[k], NL * leg);
-    stf(W, H12_F_ACT + k, e, js * s.act[k], NL * leg);
-    stf(W, H12_F_ACT_PREV + k, e, js * s.act1[k], NL * leg);
+    if (PH_) {
+      stf(W, H12_F_Q + k, e, js * s.lg.q[k], NL * leg);
+      stf(W, H12_F_QD + k, e, js * s.lg.qd[k], NL * leg);
+    }
+    if (RE_) {
+      stf(W, H12_F_ACT + k, e, js * s.act[k], NL * leg);
+      stf(W, H12_F_ACT_PREV + k, e, js * s.act1[k], NL * leg);
+    }
   }
   int cm_real = 0;
 #pragma unroll
   for (int q = 0; q < H12_NFOOT_PTS; ++q) {
     int qr = leg ? (q ^ 1) : q;
-    stf(W, H12_F_ANCHOR + 2 * q, e, s.lg.anc[q][0], 8 * leg + 2 * (qr - q));
-    stf(W, H12_F_ANCHOR + 2 * q + 1, e, sg * s.lg.anc[q][1], 8 * leg + 2 * (qr - q));
+    if (PH_) {
+      stf(W, H12_F_ANCHOR + 2 * q, e, s.lg.anc[q][0], 8 * leg + 2 * (qr - q));
+      stf(W, H12_F_ANCHOR + 2 * q + 1, e, sg * s.lg.anc[q][1], 8 * leg + 2 * (qr - q));
+    }
     cm_real |= ((s.lg.cmask >> q) & 1) << qr;
   }
+  if (!RE_) return;
   stf(W, H12_F_METRIC, e, lsel(s.metric[0], s.metric[1]), leg);
   stf(W, H12_F_AIR, e, s.air, leg);
   stf(W, H12_F_CONTACT, e, s.con, leg);
@@ -2364,11 +2380,9 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       A.term[e] = (uint8_t)term;
       A.trunc[e] = (uint8_t)tout;
     }
-#ifndef H12_EXP_NO_OUT  // experiment builds only (tools/phase_profile.py --plain -D ...): price the optional outputs
     if (A.applied_torque)
       for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
-#endif
     // ---- episode log: the (few) resetting envs add their sums directly (no-return atomics)
     // into this block's own partial slots (value-major [LOG_NPART][blocks]): the wave's resetting lanes are summed
     // by the compiler's wave reduction, one no-return atomic per value and block -- no two blocks share an address.
@@ -2405,7 +2419,9 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     PH(5);
     obs_frame<K>(P, s, leg, e, W.n, A.frame);
     PH(6);
+#ifndef H12_EXP_NO_STORE  // experiment builds only (knock-out timing)
     store_env<K>(P, W, e, leg, s);
+#endif
     PH(7);
   }
 }
