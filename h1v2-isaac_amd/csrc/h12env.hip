@@ -39,10 +39,13 @@ namespace {
 constexpr int NJ = H12_NJ;
 constexpr int NL = 6;               // links per leg
 constexpr int ENVS_PER_BLOCK = 32;  // 64 lanes = 32 lane pairs
-// episode-log values step_kernel accumulates (the rest of the H12_NLOG slots are CaT's, added by cat_prob_kernel):
-// reward sums, reset count, time-out / base-contact counts, command metrics.  Partial slot pv -> log slot:
-constexpr int LOG_NPART = H12_NREW + 3 + 2;
-__host__ __device__ constexpr int log_slot(int pv) { return pv < H12_NREW + 3 ? pv : H12_LOG_METRIC + (pv - H12_NREW - 3); }
+// episode-log values accumulated per block (partial slots, folded by the assembly kernel): step_kernel's reward sums,
+// reset count, time-out / base-contact counts, command metrics, then cat_prob_kernel's constraint violation rates
+// and mean probabilities.  Partial slot pv -> log slot:
+constexpr int LOG_NSTEP = H12_NREW + 3 + 2, LOG_NPART = LOG_NSTEP + 2 * H12_NCSTR;
+__host__ __device__ constexpr int log_slot(int pv) {
+  return pv < H12_NREW + 3 ? pv : (pv < LOG_NSTEP ? H12_LOG_METRIC + (pv - H12_NREW - 3) : H12_NREW + 4 + (pv - LOG_NSTEP));
+}
 constexpr int BLOCK = 64;
 // joint axes per leg link: hip yaw z, hip pitch y, hip roll x, knee y, ankle pitch y, ankle roll x
 constexpr int AX[NL] = {2, 1, 0, 1, 1, 0};
@@ -1896,13 +1899,23 @@ H12_DEV float log_load(const AsmArgs& A) {
   }
   return acc;
 }
-H12_DEV void log_fold(const AsmArgs& A, float acc) {
-  if (!log_block(A)) return;
-  float* q = A.log_part + (size_t)blockIdx.x * A.log_nb;
+H12_DEV void log_fold_one(const AsmArgs& A, int pv, float acc) {
+  float* q = A.log_part + (size_t)pv * A.log_nb;
   for (int b = threadIdx.x; b < A.log_nb; b += 64) q[b] = 0.f;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (threadIdx.x == 0 && acc != 0.f) A.log_acc[log_slot(blockIdx.x)] += acc;
+  if (threadIdx.x == 0 && acc != 0.f) A.log_acc[log_slot(pv)] += acc;
+}
+H12_DEV void log_fold(const AsmArgs& A, float acc) {
+  if (!log_block(A)) return;
+  log_fold_one(A, blockIdx.x, acc);
+  // a grid smaller than LOG_NPART (a few envs): the remaining values, one round trip each
+  for (int pv = blockIdx.x + gridDim.x; pv < LOG_NPART; pv += gridDim.x) {
+    float a = 0.f;
+    const float* q = A.log_part + (size_t)pv * A.log_nb;
+    for (int b = threadIdx.x; b < A.log_nb; b += 64) a += q[b];
+    log_fold_one(A, pv, a);
+  }
 }
 #ifndef H12_ASM_ROWS
 #define H12_ASM_ROWS 4
@@ -2600,7 +2613,8 @@ struct CatArgs {
   const uint8_t* term;
   const uint8_t* trunc;
   float* cstr_prob;
-  float* log_acc;
+  float* log_part;  // the handle's per-block log partials ([LOG_NPART][log_nb]), or null: no log
+  int log_nb;
 };
 constexpr int CAT_PBLOCK = 64;
 __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspace W, CatArgs A) {
@@ -2650,9 +2664,9 @@ __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspa
     if (!((P.cmask >> t) & 1u)) continue;
     float a = vs[t] + (pt[t] > 0.f ? 1.f : 0.f), b = vp[t] + pt[t];
     if (reset) {
-      if (A.log_acc) {
-        atomicAdd(&A.log_acc[H12_NREW + 4 + t], a * inv_len);
-        atomicAdd(&A.log_acc[H12_NREW + 4 + H12_NCSTR + t], b * inv_len);
+      if (A.log_part) {  // this block's partial slots (see step_kernel's episode log)
+        atomicAdd(&A.log_part[(size_t)(LOG_NSTEP + t) * A.log_nb + blockIdx.x], a * inv_len);
+        atomicAdd(&A.log_part[(size_t)(LOG_NSTEP + H12_NCSTR + t) * A.log_nb + blockIdx.x], b * inv_len);
       }
       a = b = 0.f;
     }
@@ -3303,7 +3317,9 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
     HIP_TRY(hipGetLastError());
-    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, out->log_acc};
+    static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
+    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, out->log_acc ? h->log_part : nullptr,
+                 n_blocks(h)};
     hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0,
                        (hipStream_t)stream, h->P, h->W, C);
     HIP_TRY(hipGetLastError());

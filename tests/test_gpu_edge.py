@@ -153,3 +153,57 @@ def test_ragged_env_counts_rsl_cat(gpu, task, n):
         if task == "cat":
             assert np.isfinite(term.cpu().numpy()).all()
     env.close()
+
+
+@pytest.mark.parametrize("task", ["flat", "cat"])
+@pytest.mark.parametrize("n", [1, 37, 4096])
+def test_episode_log_fold_ragged(gpu, task, n):
+    """The episode log (reward sums, reset / time-out / base-contact counts, command metrics and, for CaT, the
+    constraint statistics) goes through per-block partial slots folded by the assembly kernel (log_load /
+    log_fold): compare the step's accumulator with the oracle's on steps with forced time-outs, including grids
+    smaller than the number of log values (n = 1, 37)."""
+    from h12env._abi import F as FIELDS, LOG_METRIC, NLOG, NREW
+    from h12env.cfg import H12CaTEnvCfg
+
+    cfg = H12FlatEnvCfg() if task == "flat" else H12CaTEnvCfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    O.cat_reset()
+    O.set_dz_count(0)
+    ref = O.OracleEnv(env._model, env._ccfg, n)
+    ref.F[:] = env._fstate.cpu().numpy()
+    ref.I[:] = env._istate.cpu().numpy()
+    ref.obs[:] = env._obs[env._k].cpu().numpy()
+    rng = np.random.default_rng(5)
+    checked = 0
+    for t in range(1, 7):
+        if t == 3:  # half of the envs (at least one) time out at step 4
+            el = env.episode_length_buf.clone()
+            el[: max(1, n // 2)] = int(env.max_episode_length) - 1
+            env.episode_length_buf = el
+            ref.I[:] = env._istate.cpu().numpy()
+        if task == "cat":
+            for name, cid in cfg.constraints.active():
+                if name != "contact":
+                    ref.cfg.cstr_max_p[cid] = 1.0 / (20 + min((t - 1) / 120000, 1.0) * (4 - 20))
+        F0, I0 = env._fstate.cpu().numpy().copy(), env._istate.cpu().numpy().copy()
+        a = (0.3 * rng.normal(size=(n, 12))).astype(np.float32)
+        env.step(torch.from_numpy(a).cuda())
+        ref.F[:], ref.I[:] = F0, I0  # teacher-forced: the oracle steps from the GPU's state
+        _, _, r_term, r_trunc, info = ref.step(a, t)
+        acc = env._log_ring[env.common_step_counter % len(env._log_ring)].cpu().numpy()
+        lo = info["log"]
+        if (r_term | r_trunc).any():
+            k = list(range(NREW + 3)) + [LOG_METRIC, LOG_METRIC + 1]
+            if task == "cat":
+                k += list(range(NREW + 4, NREW + 4 + 20))
+            np.testing.assert_allclose(acc[k], lo[k], rtol=2e-3, atol=2e-4 * max(1.0, float(np.abs(lo[k]).max())),
+                                       err_msg=f"{task} n={n} step {t}")
+            assert acc[NREW] == lo[NREW] and acc[NREW] >= 1
+            checked += 1
+        else:
+            assert not acc.any()
+    assert checked >= 1
+    env.close()

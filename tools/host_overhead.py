@@ -46,7 +46,7 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.steps * 1e6
     # host time alone: block the stream first so every launch of the loop only queues
-    n_host = min(a.steps, 500)
+    n_host = min(a.steps, 100)
     torch.cuda._sleep(int(2e9))  # ~1 s of GPU spin ahead of the launches
     t0 = time.perf_counter()
     for i in range(n_host):
