@@ -3445,9 +3445,10 @@ int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, doub
   const bool rough = P.task == H12_TASK_ROUGH;
   double bytes, flops;
   if (kernel == 0) {
-    // state fields the kernel reads and writes, actions, reward / terminated / truncated, applied torque
-    // and foot force (the ArticulationData / ContactSensor views), the noise-free frame
-    double fields = 104.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0) +
+    // state fields the kernel reads and writes (106 on the plane: ABI 7 added the two command metrics), actions,
+    // reward / terminated / truncated, applied torque and foot force (the ArticulationData / ContactSensor views),
+    // the noise-free frame
+    double fields = 106.0 + (P.terrain ? 4.0 : 0.0) + (P.env_mu ? 4.0 : 0.0) + (P.env_mass ? 1.0 : 0.0) +
                     (P.rsl ? 8.0 : 0.0) + (P.push ? 1.0 : 0.0) + (P.cat ? 22.0 : 0.0);
     // CaT: the constraint scratch written and read back, the no_move list entry, reward and dones rewritten
     const double cat_bytes = P.cat ? (double)CAT_ROWS * 4.0 * 2.0 + 4.0 + 4.0 * 2.0 + 4.0 : 0.0;
