@@ -946,7 +946,9 @@ H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], c
 struct HelpLds {
   float4 st[8][BLOCK];    // state: base pos (3), quat (4), v (3), w (3); leg q (6), qd (6) (lane frame); env origin (3);
                           // added torso mass (1)
-  float4 jt[7][BLOCK];    // joint terms: tq (6), dl (6); knee contact: wrench (6), reported force (3), ImplC (5), z (1)
+  float4 jt[9][BLOCK];    // joint terms: tq (6, incl. the delayed PD), dl (6); knee contact: wrench (6), reported force
+                          // (3), ImplC (5), z (1); spare (1); the delayed-PD torque alone (6), spare (2)
+  float4 pd[6][BLOCK];    // per env step: a_t, a_{t-1}, a_{t-2} of the leg (lane frame, 18), lags (3), steps since reset
   float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
 };
@@ -972,6 +974,53 @@ H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
   x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
   x[28] = lg.dmass; x[29] = x[30] = x[31] = 0.f;
   put4(help_lds().st, l, x, 8);
+}
+
+// DelayedPDActuator (IsaacLab mode; A/robots/h12.py:58-112): delayed target = CircularBuffer[lag] with the lag
+// clamped to pushes - 1, held over physics step st; MuJoCo mode: PD towards the current action
+struct PdIn {
+  float act[NL], act1[NL], act2[NL];
+  int lag[3], since_reset;
+};
+H12_DEV void pd_torque(const KParams& P, const PdIn& d, const Leg& lg, int st, float* tau) {
+  const int dec = P.decimation;
+  if (P.mode == H12_MODE_ISAACLAB) {
+    const int npush = d.since_reset * dec + st + 1;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      // the compiler folds this select into a runtime-indexed load of d.lag[], which keeps PdIn in scratch (92 B
+      // per lane, helper wave only).  Register-resident variants (bit-packed lags, arithmetic select) have the
+      // same loop ISA but measured 35-43 us per launch against 30.5 us; kept as measured.
+      const int dg = P.dgroup[k];
+      const int L = min(dg == 0 ? d.lag[0] : (dg == 1 ? d.lag[1] : d.lag[2]), npush - 1);
+      const float a = (L <= st) ? d.act[k] : ((L <= st + dec) ? d.act1[k] : d.act2[k]);
+      const float tgt = h12m::Q0[k] + P.action_scale * a;
+      const float v = P.kp[k] * (tgt - lg.q[k]) + P.kd[k] * (0.f - lg.qd[k]);
+      tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const float tgt = h12m::Q0[k] + P.action_scale * d.act[k];
+      const float v = P.kp[k] * (tgt - lg.q[k]) - P.kd[k] * lg.qd[k];
+      tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
+    }
+  }
+}
+H12_DEV void put_pd(int l, const PdIn& d) {
+  float x[24];
+  for (int k = 0; k < NL; ++k) { x[k] = d.act[k]; x[6 + k] = d.act1[k]; x[12 + k] = d.act2[k]; }
+  for (int g = 0; g < 3; ++g) x[18 + g] = (float)d.lag[g];
+  x[21] = (float)d.since_reset;
+  x[22] = x[23] = 0.f;
+  put4(help_lds().pd, l, x, 6);
+}
+H12_DEV void get_pd(int l, PdIn& d) {
+  float x[24];
+  get4(help_lds().pd, l, x, 6);
+  for (int k = 0; k < NL; ++k) { d.act[k] = x[k]; d.act1[k] = x[6 + k]; d.act2[k] = x[12 + k]; }
+  for (int g = 0; g < 3; ++g) d.lag[g] = (int)x[18 + g];
+  d.since_reset = (int)x[21];
 }
 
 // joint torques beyond the PD term (tq) and the implicit joint inertia of the active limits (dl), from q / qd
@@ -1084,6 +1133,8 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps) {
   const int leg = l & 1;
   const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
+  PdIn pd;
+  float tau_pd[NL];
   for (int it = 0; it < n_steps; ++it) {
     __syncthreads();  // S: the state of this inner step
     Base b;
@@ -1092,14 +1143,19 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps) {
     float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
     if (active) {
       get_state(l, b, lg, org);
-      float jt[28];
+      if (it == 0) get_pd(l, pd);
+      // the delayed PD torque is computed at the first inner step of each physics step and held over it
+      if (it % P.inner == 0) pd_torque(P, pd, lg, it / P.inner, tau_pd);
+      float jt[36];
       joint_terms(P, lg, P.h, jt, jt + 6);
+      for (int k = 0; k < NL; ++k) { jt[k] += tau_pd[k]; jt[28 + k] = tau_pd[k]; }
+      jt[34] = jt[35] = 0.f;
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
       ImplC ick;
       for (int i = 12; i < 21; ++i) jt[i] = 0.f;
       knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt + 12, jt + 18, ick, jt[26]);
       jt[21] = ick.beta; jt[22] = ick.gamma; jt[23] = ick.u[0]; jt[24] = ick.u[1]; jt[25] = ick.u[2]; jt[27] = 0.f;
-      put4(H.jt, l, jt, 7);
+      put4(H.jt, l, jt, 9);
     }
     __syncthreads();  // R1: joint terms, knee contact
     if (active) {
@@ -1149,11 +1205,11 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
 }
 
 // One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
-// lane's 6 joints (lane frame).  Adds this lane's contact forces into fr.  HW: the block has a helper wave
+// lane's 6 joints (lane frame): an input without a helper wave, the helper's delayed-PD torque on return with one.  Adds this lane's contact forces into fr.  HW: the block has a helper wave
 // (step_kernel; the state of this step is in LDS and, with more, the next one is put there), else the
 // contact-independent forces are evaluated in this wave.
 template <int K, bool HW>
-H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
+H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_pd, float h, Forces& fr,
                         const float* org, bool more) {
   PHX_INIT();
   const float sg = leg ? -1.f : 1.f;
@@ -1198,9 +1254,10 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, const float
   PHX(10);
   if constexpr (HW) {
     __syncthreads();  // R1
-    float jt[28];
-    get4(help_lds().jt, threadIdx.x, jt, 7);
-    for (int k = 0; k < NL; ++k) { tau[k] = tau_pd[k] + jt[k]; dl[k] = jt[6 + k]; }
+    float jt[36];
+    get4(help_lds().jt, threadIdx.x, jt, 9);
+    // tq includes the delayed PD (computed by the helper wave); tau_pd receives the PD torque alone
+    for (int k = 0; k < NL; ++k) { tau[k] = jt[k]; dl[k] = jt[6 + k]; tau_pd[k] = jt[28 + k]; }
     for (int i = 0; i < 6; ++i) fext_knee[i] = jt[12 + i];
     for (int a = 0; a < 3; ++a) fr.knee[a] += jt[18 + a];
     ick.beta = jt[21]; ick.gamma = jt[22]; ick.u[0] = jt[23]; ick.u[1] = jt[24]; ick.u[2] = jt[25];
@@ -2314,29 +2371,16 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     float fmax_knee = 0.f, fmax_torso = 0.f, fmax_foot = 0.f, flast_foot = 0.f;
     uint32_t cflags = 0;  // foot contact flag of every physics step (ContactSensor replay)
     const float wgt = frcp((float)P.inner);
+    {  // the helper wave computes the delayed PD (pd_torque) from these and each inner step's state
+      PdIn d;
+      for (int k = 0; k < NL; ++k) { d.act[k] = s.act[k]; d.act1[k] = s.act1[k]; d.act2[k] = a_t2[k]; }
+      for (int g = 0; g < 3; ++g) d.lag[g] = s.lag[g];
+      d.since_reset = s.since_reset;
+      put_pd(threadIdx.x, d);
+    }
     put_state(threadIdx.x, s.b, s.lg, s.origin);
     __syncthreads();  // S: the first inner step's state for the helper wave
     for (int st = 0; st < dec; ++st) {
-      if (P.mode == H12_MODE_ISAACLAB) {
-        // DelayedPDActuator: delayed target = CircularBuffer[lag] with lag clamped to pushes-1
-        int npush = s.since_reset * dec + st + 1;
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-          const int dg = P.dgroup[k];  // uniform; select instead of a runtime-indexed (scratch) array
-          int L = min(dg == 0 ? s.lag[0] : (dg == 1 ? s.lag[1] : s.lag[2]), npush - 1);
-          float a = (L <= st) ? s.act[k] : ((L <= st + dec) ? s.act1[k] : a_t2[k]);
-          float tgt = h12m::Q0[k] + P.action_scale * a;
-          float v = P.kp[k] * (tgt - s.lg.q[k]) + P.kd[k] * (0.f - s.lg.qd[k]);
-          tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < NL; ++k) {
-          float tgt = h12m::Q0[k] + P.action_scale * s.act[k];
-          float v = P.kp[k] * (tgt - s.lg.q[k]) - P.kd[k] * s.lg.qd[k];
-          tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
-        }
-      }
       const bool last = st == dec - 1;
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
