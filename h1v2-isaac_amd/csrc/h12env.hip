@@ -63,11 +63,24 @@ template <int K> struct Feat {
 // over waves (lane 0), read back with h12env_phase_profile.  Not part of the product library.
 #ifdef H12_PHASE_PROFILE
 __device__ unsigned long long g_phase[16];
-#define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter()
+__device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, [4]: after reset + command, [5]: spare  // per physics wave of the last launch: realtime start, end, end after waitcnt
+#define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter(); \
+  const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime()
+#define PH_WAVE_END()                                                          \
+  do {                                                                         \
+    const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();           \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
+    const unsigned long long _r2 = __builtin_amdgcn_s_memrealtime();           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                        \
+      g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
+    }                                                                          \
+  } while (0)
 #define PH(i)                                                                       \
   do {                                                                              \
     unsigned long long _t = __builtin_readcyclecounter();                           \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _ph_t);                \
+    if ((i == 1 || i == 5) && (threadIdx.x & 63) == 0 && blockIdx.x < 1024)          \
+      g_wave[blockIdx.x][i == 1 ? 3 : 4] = __builtin_amdgcn_s_memrealtime();        \
     _ph_t = _t;                                                                     \
   } while (0)
 // inside inner_step (its own clock mark): slots 10.. split the inner step around the helper hand-off
@@ -80,6 +93,7 @@ __device__ unsigned long long g_phase[16];
   } while (0)
 #else
 #define PH_INIT() (void)0
+#define PH_WAVE_END() (void)0
 #define PH(i) (void)0
 #define PHX_INIT() (void)0
 #define PHX(i) (void)0
@@ -176,6 +190,9 @@ struct Workspace {
   float* F;    // [H12_NF_FLOAT][n]
   int32_t* I;  // [H12_NF_INT][n]
   int n;
+#ifdef H12_EXP_DUMMY_HIP
+  float* xd;   // experiment builds only: a hipMalloc'd buffer nothing reads
+#endif
 };
 
 enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3, ST_PUSH = 4 };
@@ -951,6 +968,8 @@ struct HelpLds {
   float4 pd[6][BLOCK];    // per env step: a_t, a_{t-1}, a_{t-2} of the leg (lane frame, 18), lags (3), steps since reset
   float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
+  uint4 rnd[4][BLOCK];    // the env's reset / command-resample Philox blocks of this step (reset_draws)
+  float logv[LOG_NSTEP][ENVS_PER_BLOCK];  // episode-log values of this step's resetting envs (0 for the others)
 };
 // value barrier: x is computed before this point (an empty volatile asm that reads and rewrites it)
 H12_DEV void pin(float& x) { asm volatile("" : "+v"(x)); }
@@ -974,6 +993,14 @@ H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
   x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
   x[28] = lg.dmass; x[29] = x[30] = x[31] = 0.f;
   put4(help_lds().st, l, x, 8);
+}
+
+H12_DEV void rng(const KParams& P, uint32_t g, uint32_t lo, uint32_t hi, int stream, int block, uint32_t out[4]);
+H12_DEV void get_draws(int l, uint32_t* r) {
+  for (int c = 0; c < 4; ++c) {
+    const uint4 y = help_lds().rnd[c][l];
+    r[4 * c] = y.x; r[4 * c + 1] = y.y; r[4 * c + 2] = y.z; r[4 * c + 3] = y.w;
+  }
 }
 
 // DelayedPDActuator (IsaacLab mode; A/robots/h12.py:58-112): delayed target = CircularBuffer[lag] with the lag
@@ -1128,11 +1155,22 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
 }
 
 template <int K>
-H12_DEV void helper_wave(const KParams& P, int n, int n_steps) {
+H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi) {
   const int l = threadIdx.x - BLOCK;
   const int leg = l & 1;
   const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
+  // the Philox blocks a reset (ST_RESET 0, 1) or a command resample (ST_CMD 0, 1) of this step would draw: they
+  // depend only on the env id and the step counter, so they are drawn here while the physics wave loads its state
+  // (a resetting wave otherwise spends ~1.5 us on them after the physics loop, and the step time is the slowest
+  // wave's)
+  if (active) {
+    uint32_t r[4];
+    rng(P, g, lo, hi, ST_RESET, 0, r); H.rnd[0][l] = make_uint4(r[0], r[1], r[2], r[3]);
+    rng(P, g, lo, hi, ST_RESET, 1, r); H.rnd[1][l] = make_uint4(r[0], r[1], r[2], r[3]);
+    rng(P, g, lo, hi, ST_CMD, 0, r); H.rnd[2][l] = make_uint4(r[0], r[1], r[2], r[3]);
+    rng(P, g, lo, hi, ST_CMD, 1, r); H.rnd[3][l] = make_uint4(r[0], r[1], r[2], r[3]);
+  }
   PdIn pd;
   float tau_pd[NL];
   for (int it = 0; it < n_steps; ++it) {
@@ -1433,16 +1471,46 @@ H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return ws_rsrc(base); }
 #endif
 H12_DEV __amdgpu_buffer_rsrc_t st_F(const Workspace& W) { return ws_rsrc_st(W.F); }
 H12_DEV __amdgpu_buffer_rsrc_t st_I(const Workspace& W) { return ws_rsrc_st(W.I); }
+#ifdef H12_EXP_DUMMY_HIP
+#define H12_EXP_DUMMY_FM
+#endif
+#if defined(H12_EXP_DUMMY_FM) || defined(H12_EXP_DUMMY_COMPACT)
+// experiment builds only: the state write-back into a buffer nothing reads, field-major (the workspace layout)
+// or compact per block ([block][field][32 envs]: a wave's stores span 7 pages instead of ~200)
+__device__ float g_exp_dummy[1 << 22];
+H12_DEV void exp_st(const Workspace& W, int f, int e, uint32_t x, int lf, int region) {
+#ifdef H12_EXP_DUMMY_HIP
+  auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)W.xd, 0, -1, 0x00020000);
+#else
+  auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)g_exp_dummy, 0, -1, 0x00020000);
+#endif
+#ifdef H12_EXP_DUMMY_FM
+  __builtin_amdgcn_raw_buffer_store_b32(x, rs, (e + lf * 4096) * 4 + region * (8 << 20), f * 4096 * 4, 0);
+#else
+  __builtin_amdgcn_raw_buffer_store_b32(x, rs, (((e >> 5) * 256 + lf) * 128 + (e & 31) * 4) + region * (8 << 20),
+                                        f * 128, 0);
+#endif
+}
+H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) { exp_st(W, f, e, __builtin_bit_cast(uint32_t, x), lf, 0); }
+#else
+#ifndef H12_ST_POL
+#define H12_ST_POL 0
+#endif
 H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), st_F(W), (e + lf * W.n) * 4, f * W.n * 4,
-                                        0);
+                                        H12_ST_POL);
 }
+#endif
 H12_DEV int ldi(const Workspace& W, int f, int e) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
 }
+#if defined(H12_EXP_DUMMY_FM) || defined(H12_EXP_DUMMY_COMPACT)
+H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) { exp_st(W, f, e, (uint32_t)x, lf, 1); }
+#else
 H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, 0);
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, H12_ST_POL);
 }
+#endif
 
 struct EnvSt {
   Base b;
@@ -1632,10 +1700,15 @@ H12_DEV float wrap_pi(float x) {
 // CommandTerm._resample: UniformVelocityCommand._resample_command (upstream; in-repo twin
 // utils/mdp/commands.py:19-59) + time_left ~ U(resampling_time_range).  blk: first of the two Philox blocks
 // (0: reset / time-out resample, 3: the deadzone's re-activation resample of the same step)
-H12_DEV void cmd_resample(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi, int blk = 0) {
+H12_DEV void cmd_resample(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uint32_t hi, int blk = 0,
+                          const uint32_t* pre = nullptr) {
   uint32_t r0[4], r1[4];
-  rng(P, g, lo, hi, ST_CMD, blk, r0);
-  rng(P, g, lo, hi, ST_CMD, blk + 1, r1);
+  if (pre) {  // blk 0's two blocks drawn ahead by the helper wave (reset_draws)
+    for (int i = 0; i < 4; ++i) { r0[i] = pre[i]; r1[i] = pre[4 + i]; }
+  } else {
+    rng(P, g, lo, hi, ST_CMD, blk, r0);
+    rng(P, g, lo, hi, ST_CMD, blk + 1, r1);
+  }
   s.cmd[0] = uab(r0[0], P.cmd_x0, P.cmd_x1);
   s.cmd[1] = uab(r0[1], P.cmd_y0, P.cmd_y1);
   s.cmd[2] = uab(r0[2], P.cmd_w0, P.cmd_w1);
@@ -1761,10 +1834,15 @@ H12_DEV void push_event(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uin
 
 // _reset_idx: scene reset (delay lags, sensors), reset events, manager resets (cat_env.py:195-248)
 template <int K>
-H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi) {
+H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t lo, uint32_t hi,
+                       const uint32_t* pre = nullptr) {
   uint32_t r0[4], r1[4];
-  rng(P, g, lo, hi, ST_RESET, 0, r0);
-  rng(P, g, lo, hi, ST_RESET, 1, r1);
+  if (pre) {  // drawn ahead by the helper wave (reset_draws): ST_RESET blocks 0, 1, then ST_CMD blocks 0, 1
+    for (int i = 0; i < 4; ++i) { r0[i] = pre[i]; r1[i] = pre[4 + i]; }
+  } else {
+    rng(P, g, lo, hi, ST_RESET, 0, r0);
+    rng(P, g, lo, hi, ST_RESET, 1, r1);
+  }
   if (Feat<K>::terrain && P.curriculum) {
     // CurriculumManager.compute runs first in _reset_idx, on the pre-reset state:
     // terrain_levels_vel (velocity/mdp/curriculums.py:21-52) + TerrainImporter.update_env_origins
@@ -1817,7 +1895,7 @@ H12_DEV void env_reset(const KParams& P, EnvSt& s, int leg, uint32_t g, uint32_t
     rng(P, g, lo, hi, ST_RESET, 3, r3);
     s.push_t = uab(r3[0], P.push_t0, P.push_t1);
   }
-  cmd_resample(P, s, g, lo, hi);
+  cmd_resample(P, s, g, lo, hi, 0, pre ? pre + 8 : nullptr);
 }
 
 // root (composite COM) linear velocity in world: v_origin + w x (R c); c moves with the added torso mass
@@ -2339,8 +2417,27 @@ struct StepArgs {
 template <int K>
 __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
-    if (threadIdx.x < 2 * BLOCK) helper_wave<K>(P, W.n, P.decimation * P.inner);
-    else self_wave<K>(P, W.n, P.decimation * P.inner);
+    if (threadIdx.x < 2 * BLOCK) {
+      helper_wave<K>(P, W.n, P.decimation * P.inner,
+                     (uint32_t)(A.env_offset + blockIdx.x * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi);
+      if (A.log_part) {
+        __syncthreads();  // L: the physics wave's episode-log values
+        // lane v sums value v over the block's envs and adds it to this block's partial slot (one atomic per
+        // value and block; the slots are value-major [LOG_NPART][blocks], no two blocks share an address)
+        const int v = threadIdx.x - BLOCK;
+        constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+        const int ne = min(ENVS_PER_BLOCK, W.n - (int)blockIdx.x * ENVS_PER_BLOCK);
+        if (v < LOG_NSTEP && (v < NT || v >= H12_NREW)) {
+          const HelpLds& H = help_lds();
+          float acc = 0.f;
+          for (int j = 0; j < ne; ++j) acc += H.logv[v][j];
+          if (acc != 0.f) atomicAdd(A.log_part + (size_t)v * gridDim.x + blockIdx.x, acc);
+        }
+      }
+    } else {
+      self_wave<K>(P, W.n, P.decimation * P.inner);
+      if (A.log_part) __syncthreads();  // L
+    }
     return;
   }
   const int lane_pair = threadIdx.x >> 1;
@@ -2357,6 +2454,9 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     load_phys<K>(P, W, e, leg, s);
     // the MDP part of the state is loaded here too: its memory round trip overlaps the physics loop
     load_mdp<K>(P, W, e, leg, s);
+#ifdef H12_EXP_WAIT_LOADS  // experiment builds only: expose the state-load round trip in phase slot 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
@@ -2431,7 +2531,11 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     }
     if (Feat<K>::ext && P.cat) cat_constraints(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
     PH(3);
+#ifdef H12_EXP_NO_RESET  // experiment builds only: price the in-kernel reset path
+    const bool reset = false;
+#else
     const bool reset = term || tout;
+#endif
     if (leg == 0) {
       A.rew[e] = r;
       A.term[e] = (uint8_t)term;
@@ -2440,29 +2544,39 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     if (A.applied_torque)
       for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
-    // ---- episode log: the (few) resetting envs add their sums directly (no-return atomics)
-    // into this block's own partial slots (value-major [LOG_NPART][blocks]): the wave's resetting lanes are summed
-    // by the compiler's wave reduction, one no-return atomic per value and block -- no two blocks share an address.
-    // (One shared accumulator made every wave's 17 atomics queue on the same two L2 lines: +4.2 us per step.)
-    // The assembly kernel that follows folds the partials into log_acc (log_load / log_fold).
-    if (A.log_part && reset && leg == 0) {
-      float* lp = A.log_part + blockIdx.x;
-      const int nb = gridDim.x;
-      for (int t = 0; t < NT; ++t) atomicAdd(&lp[t * nb], s.epsum[t]);
-      atomicAdd(&lp[H12_NREW * nb], 1.f);
-      if (tout) atomicAdd(&lp[(H12_NREW + 1) * nb], 1.f);
-      if (term) atomicAdd(&lp[(H12_NREW + 2) * nb], 1.f);
-      atomicAdd(&lp[(H12_NREW + 3) * nb], s.metric[0]);  // CommandTerm.reset: metrics of the ended episode
-      atomicAdd(&lp[(H12_NREW + 4) * nb], s.metric[1]);
+    // ---- episode log: the resetting envs' sums go to LDS and the helper wave adds them into this block's own
+    // partial slots (value-major [LOG_NPART][blocks]; one shared accumulator made every wave's atomics queue on
+    // the same L2 lines: +4.2 us per step).  In this wave the wave-reduced atomics cost a resetting wave ~0.5 us,
+    // and the step time is the slowest wave's.  The assembly kernel that follows folds the partials into log_acc
+    // (log_load / log_fold).
+    if (A.log_part) {
+      if (leg == 0) {
+        float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
+        for (int t = 0; t < NT; ++t) L[t][lane_pair] = reset ? s.epsum[t] : 0.f;
+        L[H12_NREW][lane_pair] = reset ? 1.f : 0.f;
+        L[H12_NREW + 1][lane_pair] = (reset && tout) ? 1.f : 0.f;
+        L[H12_NREW + 2][lane_pair] = (reset && term) ? 1.f : 0.f;
+        L[H12_NREW + 3][lane_pair] = reset ? s.metric[0] : 0.f;  // CommandTerm.reset: metrics of the ended episode
+        L[H12_NREW + 4][lane_pair] = reset ? s.metric[1] : 0.f;
+      }
+      __syncthreads();  // L: the helper wave sums them into this block's partial slots
     }
     PH(4);
-    if (reset) env_reset<K>(P, s, leg, g, A.lo, A.hi);
+    if (reset) {
+      uint32_t pre[16];
+      get_draws(threadIdx.x, pre);
+      env_reset<K>(P, s, leg, g, A.lo, A.hi, pre);
+    }
     else s.since_reset = min(s.since_reset + 1, 2);
     // ---- CommandTerm.compute(step_dt): UniformVelocityCommand._update_metrics on the post-reset state, then
     // the resampling clock
     cmd_metrics<K>(P, s);
     s.cmd_time -= P.step_dt;
-    if (s.cmd_time <= 0.f) cmd_resample(P, s, g, A.lo, A.hi);
+    if (s.cmd_time <= 0.f) {
+      uint32_t pre[16];
+      get_draws(threadIdx.x, pre);
+      cmd_resample(P, s, g, A.lo, A.hi, 0, pre + 8);
+    }
     if (Feat<K>::ext && P.dz) {
       cmd_update<K>(P, s, g, A.lo, A.hi, P.dz_cnt[A.dz_slot], W.n);
       if (leg == 0 && s.cmd[0] * s.cmd[0] + s.cmd[1] * s.cmd[1] < P.dz_v * P.dz_v)
@@ -2480,6 +2594,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     store_env<K>(P, W, e, leg, s);
 #endif
     PH(7);
+    PH_WAVE_END();
   }
 }
 
@@ -3221,6 +3336,9 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->W.F = (float*)state_dev;
   h->W.I = (int32_t*)((float*)state_dev + (size_t)H12_NF_FLOAT * n_envs);
   h->W.n = n_envs;
+#ifdef H12_EXP_DUMMY_HIP
+  if (hipMalloc(&h->W.xd, 16 << 20) != hipSuccess) return set_err(H12_E_ALLOC, "exp dummy");
+#endif
   e = hipMalloc(&h->frame, sizeof(float) * FRAME_ROWS * (size_t)n_envs);
   if (e != hipSuccess) {
     if (h->own) (void)hipFree(state_dev);
@@ -3449,6 +3567,11 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
     unsigned long long z[16] = {};
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z));
   }
+  return 0;
+}
+int h12env_wave_times(unsigned long long* out, int nwaves) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave), sizeof(unsigned long long) * 6 * (size_t)nwaves));
   return 0;
 }
 #endif

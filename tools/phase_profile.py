@@ -77,6 +77,28 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
     lib.h12env_phase_profile(buf, 1)
     waves = (envs + 31) // 32
     res = {SLOTS[i]: round(buf[i] / waves / steps, 1) for i in SLOTS}
+    if hasattr(lib, "h12env_wave_times"):  # per-wave realtime stamps (100 MHz) of single launches
+        import numpy as np
+
+        wt = (C.c_ulonglong * (6 * waves))()
+        keys = ("span", "start_spread", "end_spread", "dur_mean", "dur_max", "drain_max")
+        rows, raw, rsets = [], [], []
+        for t in range(40):
+            env.step(acts[t])
+            torch.cuda.synchronize()
+            lib.h12env_wave_times(wt, waves)
+            a = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 6).astype(np.int64)[:, :5]
+            a -= a[:, 0].min()
+            raw.append(a.copy())
+            rs = (env.reset_terminated | env.reset_time_outs).view(-1, 32).sum(1).cpu().numpy()
+            rsets.append(rs)
+            d = a[:, 1] - a[:, 0]
+            rows.append([a[:, 2].max(), a[:, 0].max(), a[:, 1].max() - a[:, 1].min(), d.mean(), d.max(),
+                         (a[:, 2] - a[:, 1]).max()])
+        if os.environ.get("H12_WAVE_DUMP"):
+            np.save(os.environ["H12_WAVE_DUMP"], np.asarray(raw))
+            np.save(os.environ["H12_WAVE_DUMP"].replace(".npy", "_resets.npy"), np.asarray(rsets))
+        res["wave_realtime_us_median"] = dict(zip(keys, (np.median(np.asarray(rows), axis=0) / 100.0).round(2).tolist()))
     env.close()
     return res
 
