@@ -969,6 +969,8 @@ struct HelpLds {
   float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
   uint4 rnd[4][BLOCK];    // the env's reset / command-resample Philox blocks of this step (reset_draws)
+  float4 torso[4][BLOCK]; // torso-box ground contact (lane 0 of the pair): wrench (6), reported force (3), ImplC
+                          // beta, gamma, u (5), contact flag (1), spare (1)
   float logv[LOG_NSTEP][ENVS_PER_BLOCK];  // episode-log values of this step's resetting envs (0 for the others)
 };
 // value barrier: x is computed before this point (an empty volatile asm that reads and rewrites it)
@@ -1207,8 +1209,22 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
       if (leg) for (int i = 36; i < 42; ++i) o[i] = 0.f;
       o[42] = o[43] = 0.f;
       put4(H.bias, l, o, 11);
+      // torso-box corner contact (the base body; lane 0 of the pair) from the step's state: data-dependent work
+      // (a fallen robot's) kept off the physics wave's chain
+      float t[16] = {};
+      if (leg == 0) {
+        float corner[3];
+        for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+        ImplC ict;
+        float dummy[2];
+        const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
+                                                               org, P.mus, P.mud, ict);
+        t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
+        t[14] = c ? 1.f : 0.f;
+      }
+      put4(H.torso, l, t, 4);
     }
-    __syncthreads();  // R2: bias forces
+    __syncthreads();  // R2: bias forces, torso contact
   }
 }
 
@@ -1376,11 +1392,20 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     for (int i = 0; i < 6; ++i) pAcc[i] += pbase[i];
     for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float dummy[2];
-    if (contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org, P.mus, P.mud,
-                                                ict) &&
-        P.impl)
-      ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
+    bool c;
+    if constexpr (HW) {  // evaluated by the helper wave before R2
+      float t[16];
+      get4(help_lds().torso, threadIdx.x, t, 4);
+      for (int i = 0; i < 6; ++i) ft[i] = t[i];
+      for (int a = 0; a < 3; ++a) fr.torso[a] += t[6 + a];
+      ict.beta = t[9]; ict.gamma = t[10]; ict.u[0] = t[11]; ict.u[1] = t[12]; ict.u[2] = t[13];
+      c = t[14] != 0.f;
+    } else {
+      float dummy[2];
+      c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
+                                                   P.mus, P.mud, ict);
+    }
+    if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
   }
   // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
