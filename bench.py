@@ -324,6 +324,9 @@ def main():
     if rank == 0:
         achieved = bytes_env * n / (kern_ms_avg * 1e-3) / 1e9
         pmc, pmc_src = load_pmc(args.pmc_file)
+        if (args.task != "flat" or args.envs != 4096 or args.no_self_collision or args.decimation is not None
+                or args.inner_steps is not None or args.explicit_penalty):  # tools/profile.sh: the default workload
+            pmc, pmc_src = {}, "not collected for this workload (tools/profile.sh profiles the default flat line)"
         traffic = pmc.get("step_kernel", {}).get("hbm_bytes_per_launch")
         obs_traffic = pmc.get("obs_assemble_kernel", {}).get("hbm_bytes_per_launch")
         # VALU issue roofline of step_kernel: one wave per SIMD issues at most one VALU instruction per
