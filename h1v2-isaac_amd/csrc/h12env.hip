@@ -1156,11 +1156,17 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
   for (int k = 0; k < NL; ++k) { lg.q[k] = x[13 + k]; lg.qd[k] = x[19 + k]; }
 }
 
+// step_kernel's env chunk of this block: XCD-aware (xcd_block), so the blocks one XCD runs cover one contiguous
+// range of envs -- each XCD's state loads / stores are contiguous runs of every field instead of 128-B chunks
+// 1 KB apart (the round-robin order put the tail of the waves on some XCDs 2 us behind the others)
+H12_DEV int xcd_block(int b, int nb);
+H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
+
 template <int K>
 H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi) {
   const int l = threadIdx.x - BLOCK;
   const int leg = l & 1;
-  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
+  const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
   // the Philox blocks a reset (ST_RESET 0, 1) or a command resample (ST_CMD 0, 1) of this step would draw: they
   // depend only on the env id and the step counter, so they are drawn here while the physics wave loads its state
@@ -1232,7 +1238,7 @@ template <int K>
 H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
   const int l = threadIdx.x - 2 * BLOCK;
   const int leg = l & 1;
-  const bool active = (int)blockIdx.x * ENVS_PER_BLOCK + (l >> 1) < n;
+  const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
   for (int it = 0; it < n_steps; ++it) {
     __syncthreads();  // S: the state of this inner step
@@ -2444,14 +2450,14 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
     if (threadIdx.x < 2 * BLOCK) {
       helper_wave<K>(P, W.n, P.decimation * P.inner,
-                     (uint32_t)(A.env_offset + blockIdx.x * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi);
+                     (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi);
       if (A.log_part) {
         __syncthreads();  // L: the physics wave's episode-log values
         // lane v sums value v over the block's envs and adds it to this block's partial slot (one atomic per
         // value and block; the slots are value-major [LOG_NPART][blocks], no two blocks share an address)
         const int v = threadIdx.x - BLOCK;
         constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
-        const int ne = min(ENVS_PER_BLOCK, W.n - (int)blockIdx.x * ENVS_PER_BLOCK);
+        const int ne = min(ENVS_PER_BLOCK, W.n - step_block() * ENVS_PER_BLOCK);
         if (v < LOG_NSTEP && (v < NT || v >= H12_NREW)) {
           const HelpLds& H = help_lds();
           float acc = 0.f;
@@ -2468,7 +2474,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
-  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e0 = step_block() * ENVS_PER_BLOCK;
   const int e = e0 + lane_pair;
   const bool active = e < W.n;
   const uint32_t g = (uint32_t)(A.env_offset + e);
