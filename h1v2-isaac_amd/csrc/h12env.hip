@@ -965,7 +965,7 @@ struct HelpLds {
                           // added torso mass (1)
   float4 jt[9][BLOCK];    // joint terms: tq (6, incl. the delayed PD), dl (6); knee contact: wrench (6), reported force
                           // (3), ImplC (5), z (1); spare (1); the delayed-PD torque alone (6), spare (2)
-  float4 pd[6][BLOCK];    // per env step: a_t, a_{t-1}, a_{t-2} of the leg (lane frame, 18), lags (3), steps since reset
+  float4 pd[6][BLOCK];    // per env step: a_t, a_{t-1}, a_{t-2} of the leg (lane frame, 18), packed lags, steps since reset
   float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
   uint4 rnd[4][BLOCK];    // the env's reset / command-resample Philox blocks of this step (reset_draws)
@@ -1009,7 +1009,7 @@ H12_DEV void get_draws(int l, uint32_t* r) {
 // clamped to pushes - 1, held over physics step st; MuJoCo mode: PD towards the current action
 struct PdIn {
   float act[NL], act1[NL], act2[NL];
-  int lag[3], since_reset;
+  int lagpk, since_reset;  // the three delay groups' lags, 3 bits each (a runtime-indexed lag[] would live in scratch)
 };
 H12_DEV void pd_torque(const KParams& P, const PdIn& d, const Leg& lg, int st, float* tau) {
   const int dec = P.decimation;
@@ -1017,12 +1017,11 @@ H12_DEV void pd_torque(const KParams& P, const PdIn& d, const Leg& lg, int st, f
     const int npush = d.since_reset * dec + st + 1;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      // the compiler folds this select into a runtime-indexed load of d.lag[], which keeps PdIn in scratch (92 B
-      // per lane, helper wave only).  Register-resident variants (bit-packed lags, arithmetic select) have the
-      // same loop ISA but measured 35-43 us per launch against 30.5 us; kept as measured.
-      const int dg = P.dgroup[k];
-      const int L = min(dg == 0 ? d.lag[0] : (dg == 1 ? d.lag[1] : d.lag[2]), npush - 1);
-      const float a = (L <= st) ? d.act[k] : ((L <= st + dec) ? d.act1[k] : d.act2[k]);
+      const int L = min((d.lagpk >> (3 * P.dgroup[k])) & 7, npush - 1);
+      // bit-mask selects: a ?: chain over the three arrays is folded into a load from a selected address (scratch)
+      const uint32_t m0 = 0u - (uint32_t)(L <= st), m1 = 0u - (uint32_t)(L <= st + dec);
+      const uint32_t a12 = (__float_as_uint(d.act1[k]) & m1) | (__float_as_uint(d.act2[k]) & ~m1);
+      const float a = __uint_as_float((__float_as_uint(d.act[k]) & m0) | (a12 & ~m0));
       const float tgt = h12m::Q0[k] + P.action_scale * a;
       const float v = P.kp[k] * (tgt - lg.q[k]) + P.kd[k] * (0.f - lg.qd[k]);
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
@@ -1039,17 +1038,17 @@ H12_DEV void pd_torque(const KParams& P, const PdIn& d, const Leg& lg, int st, f
 H12_DEV void put_pd(int l, const PdIn& d) {
   float x[24];
   for (int k = 0; k < NL; ++k) { x[k] = d.act[k]; x[6 + k] = d.act1[k]; x[12 + k] = d.act2[k]; }
-  for (int g = 0; g < 3; ++g) x[18 + g] = (float)d.lag[g];
-  x[21] = (float)d.since_reset;
-  x[22] = x[23] = 0.f;
+  x[18] = (float)d.lagpk;
+  x[19] = (float)d.since_reset;
+  x[20] = x[21] = x[22] = x[23] = 0.f;
   put4(help_lds().pd, l, x, 6);
 }
 H12_DEV void get_pd(int l, PdIn& d) {
   float x[24];
   get4(help_lds().pd, l, x, 6);
   for (int k = 0; k < NL; ++k) { d.act[k] = x[k]; d.act1[k] = x[6 + k]; d.act2[k] = x[12 + k]; }
-  for (int g = 0; g < 3; ++g) d.lag[g] = (int)x[18 + g];
-  d.since_reset = (int)x[21];
+  d.lagpk = (int)x[18];
+  d.since_reset = (int)x[19];
 }
 
 // joint torques beyond the PD term (tq) and the implicit joint inertia of the active limits (dl), from q / qd
@@ -2505,7 +2504,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     {  // the helper wave computes the delayed PD (pd_torque) from these and each inner step's state
       PdIn d;
       for (int k = 0; k < NL; ++k) { d.act[k] = s.act[k]; d.act1[k] = s.act1[k]; d.act2[k] = a_t2[k]; }
-      for (int g = 0; g < 3; ++g) d.lag[g] = s.lag[g];
+      d.lagpk = (s.lag[0] & 7) | (s.lag[1] & 7) << 3 | (s.lag[2] & 7) << 6;
       d.since_reset = s.since_reset;
       put_pd(threadIdx.x, d);
     }
