@@ -165,7 +165,7 @@ struct KParams {
   float cvlim[NL], celim[NL];  // joint velocity / effort limits (leg-symmetric)
   float c_ff, c_nm_dz, c_nm_v, c_or, c_h, c_hstd, c_clr, c_clr_dz;
   float* cscr;            // [CAT_ROWS][n] raw constraints of the step (+ no_move flag, pre-reset episode length)
-  int* ckey;              // [H12_NCSTR_COLS] column maxima of the step (order-preserving int keys)
+  float* cpart;           // [H12_NCSTR_COLS][step_kernel blocks] each block's column maxima of the step
   float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
   int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised
@@ -177,12 +177,6 @@ constexpr int CAT_ROW_NOMOVE = H12_NCSTR_COLS;      // 1 if all |cmd| < no_move 
 constexpr int CAT_ROW_EPLEN = H12_NCSTR_COLS + 1;   // episode length before the reset of this step
 constexpr int CAT_ROWS = H12_NCSTR_COLS + 2;
 static_assert(C_COL0[H12_NCSTR] == H12_NCSTR_COLS, "constraint columns");
-// float -> int key with the same order (atomicMax on floats of either sign)
-H12_DEV int fkey(float f) {
-  int i = __float_as_int(f);
-  return i >= 0 ? i : i ^ 0x7FFFFFFF;
-}
-H12_DEV float fkey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
 constexpr float CAT_NEG = -3.0e38f;  // "no value" in the column maxima (finite: device code is finite-math)
 static_assert(sizeof(KParams) < 1024, "kernarg budget");
 
@@ -979,6 +973,11 @@ H12_DEV HelpLds& help_lds() {
   __shared__ HelpLds H;
   return H;
 }
+// CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the joint-term
+// hand-off array (free once the last inner step has read it; the LDS footprint stays the three-wave block's)
+typedef float CatLds[H12_NCSTR_COLS + 1][ENVS_PER_BLOCK];
+static_assert(sizeof(CatLds) <= sizeof(HelpLds::jt), "CaT values fit the joint-term array");
+H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().jt[0][0]); }
 H12_DEV void put4(float4 (*dst)[BLOCK], int l, const float* x, int n4) {
   for (int c = 0; c < n4; ++c) dst[c][l] = make_float4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
 }
@@ -1802,21 +1801,29 @@ H12_DEV bool cat_still(const KParams& P, const EnvSt& s) {
   return fabsf(s.cmd[0]) < P.c_nm_dz && fabsf(s.cmd[1]) < P.c_nm_dz && fabsf(s.cmd[2]) < P.c_nm_dz;
 }
 
+template <bool LDS>
 H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int leg, const EnvSt& s, const float* tau,
                              float fmax_foot, int term, const float R[3][3], int eplen_pre) {
   const int n = W.n;
   float* S = P.cscr;
+  // every value also goes to the block's LDS copy (step_kernel): the helper wave forms the block's column maxima
+  auto put = [&](int row, float v) {
+    S[(size_t)row * n + e] = v;
+    if constexpr (LDS) {
+      if (row <= CAT_ROW_NOMOVE) cat_lds()[row][e & (ENVS_PER_BLOCK - 1)] = v;
+    }
+  };
   const float sg = leg ? -1.f : 1.f;
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     const int j = NL * leg + k;
     const float q = s.lg.q[k], qd = fabsf(s.lg.qd[k]);
-    S[(size_t)(C_COL0[H12_C_JOINT_POS_LIMITS] + j) * n + e] = fmaxf(soft_lo(P, k) - q, q - soft_hi(P, k));
-    S[(size_t)(C_COL0[H12_C_JOINT_VEL_LIMITS] + j) * n + e] = qd - P.cvlim[k];
-    S[(size_t)(C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j) * n + e] = fabsf(tau[k]) - P.celim[k];
-    S[(size_t)(C_COL0[H12_C_NO_MOVE] + j) * n + e] = qd - P.c_nm_v;
+    put((C_COL0[H12_C_JOINT_POS_LIMITS] + j), fmaxf(soft_lo(P, k) - q, q - soft_hi(P, k)));
+    put((C_COL0[H12_C_JOINT_VEL_LIMITS] + j), qd - P.cvlim[k]);
+    put((C_COL0[H12_C_JOINT_TORQUE_LIMITS] + j), fabsf(tau[k]) - P.celim[k]);
+    put((C_COL0[H12_C_NO_MOVE] + j), qd - P.c_nm_v);
   }
-  S[(size_t)(C_COL0[H12_C_FOOT_CONTACT_FORCE] + leg) * n + e] = fmax_foot - P.c_ff;
+  put((C_COL0[H12_C_FOOT_CONTACT_FORCE] + leg), fmax_foot - P.c_ff);
   // foot_clearance: touchdown = ContactSensor.compute_first_contact(step_dt); command active = any |cmd| > dz
   {
     const bool touchdown = s.con > 0.f && s.con < P.step_dt + 1e-8f;
@@ -1831,19 +1838,19 @@ H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int le
     const float foot_z = s.b.pos[2] + p[2];  // body_link_pos_w z of the ankle-roll link
     float& sw = W.F[(size_t)(H12_F_SWING_H + leg) * n + e];
     const float sh = sw;
-    S[(size_t)(C_COL0[H12_C_FOOT_CLEARANCE] + leg) * n + e] = (touchdown && active) ? (P.c_clr - sh) : 0.f;
+    put((C_COL0[H12_C_FOOT_CLEARANCE] + leg), (touchdown && active) ? (P.c_clr - sh) : 0.f);
     sw = touchdown ? 0.f : fmaxf(sh, foot_z);
   }
   const int nfeet = (fmax_foot > 1.0f ? 1 : 0) + (pair_swap(fmax_foot) > 1.0f ? 1 : 0);
   if (leg == 0) {
-    S[(size_t)C_COL0[H12_C_CONTACT] * n + e] = term ? 1.f : 0.f;
+    put(C_COL0[H12_C_CONTACT], term ? 1.f : 0.f);
     const float gx = R[2][0], gy = R[2][1];  // projected gravity xy (sign irrelevant under the norm)
-    S[(size_t)C_COL0[H12_C_BASE_ORIENTATION] * n + e] = fsqrt(gx * gx + gy * gy) - P.c_or;
+    put(C_COL0[H12_C_BASE_ORIENTATION], fsqrt(gx * gx + gy * gy) - P.c_or);
     const float z = s.b.pos[2];
-    S[(size_t)C_COL0[H12_C_BASE_HEIGHT] * n + e] = (z < P.c_h - P.c_hstd || z > P.c_h + P.c_hstd) ? 1.f : 0.f;
-    S[(size_t)C_COL0[H12_C_FOOT_CONTACT] * n + e] = (nfeet < 1 || nfeet > 2) ? 1.f : 0.f;
-    S[(size_t)CAT_ROW_NOMOVE * n + e] = cat_still(P, s) ? 1.f : 0.f;
-    S[(size_t)CAT_ROW_EPLEN * n + e] = (float)eplen_pre;
+    put(C_COL0[H12_C_BASE_HEIGHT], (z < P.c_h - P.c_hstd || z > P.c_h + P.c_hstd) ? 1.f : 0.f);
+    put(C_COL0[H12_C_FOOT_CONTACT], (nfeet < 1 || nfeet > 2) ? 1.f : 0.f);
+    put(CAT_ROW_NOMOVE, cat_still(P, s) ? 1.f : 0.f);
+    put(CAT_ROW_EPLEN, (float)eplen_pre);
   }
 }
 
@@ -2450,8 +2457,28 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     if (threadIdx.x < 2 * BLOCK) {
       helper_wave<K>(P, W.n, P.decimation * P.inner,
                      (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi);
+      if (A.log_part || (Feat<K>::ext && P.cat)) {
+        __syncthreads();  // L: the physics wave's episode-log values (and CaT constraint values)
+        if (Feat<K>::ext && P.cat) {
+          // CaT: this block's column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs
+          // only), one value per column and block -- cat_reduce_kernel folds the blocks
+          const int col = threadIdx.x - BLOCK;
+          const int ne = min(ENVS_PER_BLOCK, W.n - step_block() * ENVS_PER_BLOCK);
+          if (col < H12_NCSTR_COLS) {
+            const CatLds& cv = cat_lds();
+            const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
+            float m = CAT_NEG;
+#pragma unroll
+            for (int j = 0; j < ENVS_PER_BLOCK; ++j) {  // unrolled: the LDS reads issue back to back
+              const float x = cv[col][j];
+              const bool ok = j < ne && (!nm || cv[CAT_ROW_NOMOVE][j] != 0.f);
+              m = ok ? fmaxf(m, x) : m;
+            }
+            P.cpart[(size_t)col * gridDim.x + blockIdx.x] = m;
+          }
+        }
+      }
       if (A.log_part) {
-        __syncthreads();  // L: the physics wave's episode-log values
         // lane v sums value v over the block's envs and adds it to this block's partial slot (one atomic per
         // value and block; the slots are value-major [LOG_NPART][blocks], no two blocks share an address)
         const int v = threadIdx.x - BLOCK;
@@ -2466,7 +2493,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       }
     } else {
       self_wave<K>(P, W.n, P.decimation * P.inner);
-      if (A.log_part) __syncthreads();  // L
+      if (A.log_part || (Feat<K>::ext && P.cat)) __syncthreads();  // L
     }
     return;
   }
@@ -2559,7 +2586,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       r += v;
       s.epsum[t] += v;
     }
-    if (Feat<K>::ext && P.cat) cat_constraints(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
+    if (Feat<K>::ext && P.cat) cat_constraints<true>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
     PH(3);
 #ifdef H12_EXP_NO_RESET  // experiment builds only: price the in-kernel reset path
     const bool reset = false;
@@ -2579,8 +2606,8 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     // the same L2 lines: +4.2 us per step).  In this wave the wave-reduced atomics cost a resetting wave ~0.5 us,
     // and the step time is the slowest wave's.  The assembly kernel that follows folds the partials into log_acc
     // (log_load / log_fold).
-    if (A.log_part) {
-      if (leg == 0) {
+    if (A.log_part || (Feat<K>::ext && P.cat)) {
+      if (A.log_part && leg == 0) {
         float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
         for (int t = 0; t < NT; ++t) L[t][lane_pair] = reset ? s.epsum[t] : 0.f;
         L[H12_NREW][lane_pair] = reset ? 1.f : 0.f;
@@ -2712,44 +2739,15 @@ __global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, Te
     T.term[e] = (uint8_t)term;
     T.trunc[e] = (uint8_t)(s.eplen >= P.max_len);
   }
-  if (Feat<K>::ext && P.cat) cat_constraints(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
+  if (Feat<K>::ext && P.cat) cat_constraints<false>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
 }
 
-// CaT, after step_kernel: per-column maxima over the envs (CaT.add: constraint.max(dim=0)).  Grid
-// (env chunks of CAT_CHUNK, columns): one block max per (chunk, column) through LDS, one atomic per block.
-// no_move columns only take the still envs -- the maximum over the reference's remapped rows.
-constexpr int CAT_CBLOCK = 256, CAT_CHUNK = 1024;
-__global__ void __launch_bounds__(CAT_CBLOCK) cat_colmax_kernel(KParams P, int n) {
-  __shared__ float s_red[CAT_CBLOCK / 64];
-  const int col = blockIdx.y;
-  const int i0 = blockIdx.x * CAT_CHUNK;
-  const float* S = P.cscr;
-  const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
-  float m = CAT_NEG;
-#pragma unroll
-  for (int u = 0; u < CAT_CHUNK / CAT_CBLOCK; ++u) {
-    const int i = i0 + u * CAT_CBLOCK + threadIdx.x;
-    if (i < n) {
-      const float v = S[(size_t)col * n + i];
-      const bool take = !nm || S[(size_t)CAT_ROW_NOMOVE * n + i] != 0.f;
-      if (take) m = fmaxf(m, v);
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float b = s_red[0];
-    for (int w = 1; w < CAT_CBLOCK / 64; ++w) b = fmaxf(b, s_red[w]);
-    atomicMax(&P.ckey[col], fkey(b));
-  }
-}
 
 // CaT: the running maxima (CaT.add, constraint_manager.py:42-78) and the compacted list of still envs in
 // ascending order (constraints.no_move hands env i the row of the (i mod m)-th still env,
 // constraints.py:202-238).  One block; per 1024-env chunk a ballot prefix in each wave and one LDS pass over
-// the wave totals.  Resets the column maxima for the next step.
+// the wave totals.  The column maxima (CaT.add: constraint.max(dim=0)) fold step_kernel's per-block maxima
+// (cpart, formed by its helper wave from LDS: no separate pass over the [col][n] scratch).
 constexpr int CAT_RBLOCK = 1024;
 __global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n) {
   __shared__ int s_wsum[CAT_RBLOCK / 64];
@@ -2776,8 +2774,22 @@ __global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n
     __syncthreads();
   }
   const int m = s_base;
+  // the column maxima: 16 threads per column fold step_kernel's per-block maxima, then a 16-lane shuffle
+  __shared__ float s_cm[H12_NCSTR_COLS];
+  static_assert(H12_NCSTR_COLS * 16 <= CAT_RBLOCK, "16 threads per column");
+  {
+    const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+    const int col = tid >> 4, sub = tid & 15;
+    float mx = CAT_NEG;
+    if (col < H12_NCSTR_COLS)
+      for (int b = sub; b < nb; b += 16) mx = fmaxf(mx, P.cpart[(size_t)col * nb + b]);
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if (sub == 0 && col < H12_NCSTR_COLS) s_cm[col] = mx;
+  }
+  __syncthreads();
   if (tid < H12_NCSTR_COLS) {
-    float cm = fkey_inv(P.ckey[tid]);
+    float cm = s_cm[tid];
     const bool nm = tid >= C_COL0[H12_C_NO_MOVE] && tid < C_COL0[H12_C_NO_MOVE + 1];
     if (nm && m == 0) cm = 0.f;  // constraints.no_move returns zeros when no env is still
     cm = fmaxf(cm, 1e-6f);       // constraint.max(dim=0).clamp(min=1e-6)
@@ -2785,7 +2797,6 @@ __global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n
     const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
     P.crun[tid] = run;
     P.crun[H12_NCSTR_COLS + tid] = 1.f / run;
-    P.ckey[tid] = fkey(CAT_NEG);
   }
   __syncthreads();
   if (tid == 0) {
@@ -3389,7 +3400,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->P.dz_cnt = h->dz_cnt;
   if (h->P.cat) {
     const size_t nn = (size_t)n_envs;
-    const size_t bytes_cat = sizeof(float) * CAT_ROWS * nn + sizeof(int) * H12_NCSTR_COLS +
+    const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+    const size_t bytes_cat = sizeof(float) * CAT_ROWS * nn + sizeof(float) * H12_NCSTR_COLS * nbk +
                              sizeof(float) * 2 * H12_NCSTR_COLS + sizeof(int) * nn + sizeof(int) * 4;
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
@@ -3402,22 +3414,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     }
     char* q = (char*)h->cat_mem;
     h->P.cscr = (float*)q; q += sizeof(float) * CAT_ROWS * nn;
-    h->P.ckey = (int*)q; q += sizeof(int) * H12_NCSTR_COLS;
+    h->P.cpart = (float*)q; q += sizeof(float) * H12_NCSTR_COLS * nbk;
     h->P.crun = (float*)q; q += sizeof(float) * 2 * H12_NCSTR_COLS;
     h->P.clist = (int*)q; q += sizeof(int) * nn;
     h->P.cmeta = (int*)q;
-    int keys[H12_NCSTR_COLS];
-    for (int i = 0; i < H12_NCSTR_COLS; ++i) {
-      float ninf = CAT_NEG;
-      int b;
-      memcpy(&b, &ninf, 4);
-      keys[i] = b >= 0 ? b : b ^ 0x7FFFFFFF;
-    }
-    e = hipMemcpy(h->P.ckey, keys, sizeof keys, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      h12env_destroy((h12env*)h);
-      return set_err(H12_E_HIP, "hipMemcpy(CaT keys): %s", hipGetErrorString(e));
-    }
   }
   h->device = device;
   if (h->P.task == H12_TASK_FLAT) {
@@ -3504,9 +3504,6 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
             h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (h->P.cat) {
-    const dim3 cg((h->W.n + CAT_CHUNK - 1) / CAT_CHUNK, H12_NCSTR_COLS);
-    hipLaunchKernelGGL(cat_colmax_kernel, cg, dim3(CAT_CBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
-    HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
     HIP_TRY(hipGetLastError());
     static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
