@@ -1785,7 +1785,9 @@ H12_DEV void cmd_update(const KParams& P, EnvSt& s, uint32_t g, uint32_t lo, uin
 // ---- CaT constraints (T/utils/cat/constraints.py) on the pre-reset state of the step, raw values into the
 // scratch [col][n] (each lane its leg's joint columns and its foot's columns, lane 0 of the pair the base
 // ones), the no_move activity flag and the pre-reset episode length for cat_prob_kernel.  foot_clearance
-// keeps its swing state (max foot height since the last touchdown) in H12_F_SWING_H.
+// keeps its swing state (max foot height since the last touchdown) in H12_F_SWING_H; WB = false (the term-evaluation
+// hook) evaluates the constraint on the stored swing state and writes the updated one to rows CAT_ROWS + leg of
+// the caller's buffer instead of the workspace.
 template <int LINK>
 H12_DEV void link_pos(const Leg& lg, float (&R)[3][3], float* p) {
   float sn, cs;
@@ -1801,7 +1803,7 @@ H12_DEV bool cat_still(const KParams& P, const EnvSt& s) {
   return fabsf(s.cmd[0]) < P.c_nm_dz && fabsf(s.cmd[1]) < P.c_nm_dz && fabsf(s.cmd[2]) < P.c_nm_dz;
 }
 
-template <bool LDS>
+template <bool LDS, bool WB = true>
 H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int leg, const EnvSt& s, const float* tau,
                              float fmax_foot, int term, const float R[3][3], int eplen_pre) {
   const int n = W.n;
@@ -1839,7 +1841,9 @@ H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int le
     float& sw = W.F[(size_t)(H12_F_SWING_H + leg) * n + e];
     const float sh = sw;
     put((C_COL0[H12_C_FOOT_CLEARANCE] + leg), (touchdown && active) ? (P.c_clr - sh) : 0.f);
-    sw = touchdown ? 0.f : fmaxf(sh, foot_z);
+    const float sw_new = touchdown ? 0.f : fmaxf(sh, foot_z);
+    if constexpr (WB) sw = sw_new;
+    else S[(size_t)(CAT_ROWS + leg) * n + e] = sw_new;  // the hook: to the caller's rows, workspace untouched
   }
   const int nfeet = (fmax_foot > 1.0f ? 1 : 0) + (pair_swap(fmax_foot) > 1.0f ? 1 : 0);
   if (leg == 0) {
@@ -2739,7 +2743,8 @@ __global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, Te
     T.term[e] = (uint8_t)term;
     T.trunc[e] = (uint8_t)(s.eplen >= P.max_len);
   }
-  if (Feat<K>::ext && P.cat) cat_constraints<false>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
+  // no swing-state write-back: the hook leaves the workspace as it found it
+  if (Feat<K>::ext && P.cat) cat_constraints<false, false>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
 }
 
 

@@ -329,10 +329,10 @@ class H12VelocityEnv:
         self._closed = False
 
     def _build_step_outs(self):
-        self._dev_index = self.device.index or 0
-        self._act_shape = torch.Size((self.num_envs, NJ))
         """h12env_step output structs, one per observation buffer (their pointers never change), the log ring's
         base pointer and the log's extra terms: step() then only sets the log slot."""
+        self._dev_index = self.device.index or 0
+        self._act_shape = torch.Size((self.num_envs, NJ))
         self._step_outs = []
         for k in range(2):
             o = H12StepOut()
@@ -561,14 +561,16 @@ class H12VelocityEnv:
         """Parity hook (h12env_eval_terms): step()'s reward-term / termination / CaT-constraint code on the
         workspace state as it stands, with injected applied torques (N, 12), joint accelerations (N, 12) and
         per-body contact-history maxima (N, 5: feet L/R, knees L/R, torso).  Returns (terms (NREW, N),
-        terminated (N,) bool, truncated (N,) bool, constraint rows (NCSTR_COLS + 2, N) or None)."""
+        terminated (N,) bool, truncated (N,) bool, constraint rows (NCSTR_COLS + 4, N) or None: the raw columns,
+        no_move flag, pre-reset episode length, and foot_clearance's updated swing height (left, right) -- the hook
+        itself leaves the workspace unchanged)."""
         n = self.num_envs
         f = lambda x, k: x.to(device=self.device, dtype=torch.float32).contiguous().reshape(n, k)  # noqa: E731
         tau, jacc, fmax = f(tau, NJ), f(jacc, NJ), f(fmax, 5)
         terms = torch.zeros(NREW, n, device=self.device)
         term = torch.zeros(n, dtype=torch.uint8, device=self.device)
         trunc = torch.zeros(n, dtype=torch.uint8, device=self.device)
-        cstr = torch.zeros(_abi.NCSTR_COLS + 2, n, device=self.device) if self._cat else None
+        cstr = torch.zeros(_abi.NCSTR_COLS + 4, n, device=self.device) if self._cat else None
         check(self._lib, self._lib.h12env_eval_terms(
             self._h, C.c_void_p(tau.data_ptr()), C.c_void_p(jacc.data_ptr()), C.c_void_p(fmax.data_ptr()),
             C.c_void_p(terms.data_ptr()), C.c_void_p(term.data_ptr()), C.c_void_p(trunc.data_ptr()),

@@ -180,6 +180,7 @@ class EmpiricalNormalization(nn.Module):
         self.register_buffer("_var", torch.ones(shape).unsqueeze(0))
         self.register_buffer("_std", torch.ones(shape).unsqueeze(0))
         self.register_buffer("count", torch.tensor(0, dtype=torch.long))
+        self._global_n: dict[int, int] = {}  # local batch size -> union size over the ranks (one sync per size)
 
     def forward(self, x):
         if self.training:
@@ -189,7 +190,10 @@ class EmpiricalNormalization(nn.Module):
     @torch.jit.unused
     def update(self, x):
         """Running update from one batch; under torch.distributed (world > 1) the batch is the union of
-        every rank's shard (count, mean and variance all-reduced), so all ranks keep identical statistics."""
+        every rank's shard, so all ranks keep identical statistics.  The shards' statistics are merged with
+        Chan's parallel formula (global mean from sum n_r mean_r, then M2 = sum n_r (var_r + (mean_r - mean)^2)):
+        no E[x^2] - mean^2 cancellation, so the merged variance is never negative.  The union size is
+        all-reduced once per local batch size and cached (no host sync per update)."""
         if self.until is not None and self.count >= self.until:
             return
         n = x.shape[0]
@@ -197,13 +201,16 @@ class EmpiricalNormalization(nn.Module):
         mean_x = torch.mean(x, dim=0, keepdim=True)
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
                 and torch.distributed.get_world_size() > 1:
-            s = torch.cat([mean_x, var_x + mean_x * mean_x]) * n   # per-rank sum and sum of squares
-            cnt = torch.tensor([float(n)], device=x.device)
-            D.all_reduce(s)
-            D.all_reduce(cnt)
-            n = int(cnt.item())
-            mean_x = s[:1] / n
-            var_x = s[1:] / n - mean_x * mean_x
+            if n not in self._global_n:
+                cnt = torch.tensor([float(n)], device=x.device)
+                D.all_reduce(cnt)
+                self._global_n[n] = int(cnt.item())
+            n_tot = self._global_n[n]
+            g_mean = mean_x * (n / n_tot)
+            D.all_reduce(g_mean)
+            m2 = (var_x + (mean_x - g_mean) ** 2) * (n / n_tot)
+            D.all_reduce(m2)
+            n, mean_x, var_x = n_tot, g_mean, m2
         self.count += n
         rate = n / self.count
         delta = mean_x - self._mean

@@ -336,10 +336,13 @@ int h12env_set_terrain(h12env* h, const float* heights, int nx, int ny, float hs
  * configured mode (PD, limits, contact), no MDP.  Mirrors H12Mujoco.step. */
 int h12env_step_physics(h12env* h, const float* q_ref, int n_substeps, void* stream);
 /* Parity hook: the MDP term code of h12env_step (unweighted reward terms [H12_NREW][N], terminated, truncated
- * and, on a CaT env, the constraint rows [H12_NCSTR_COLS + 2][N] into cstr) evaluated on the workspace state as
+ * and, on a CaT env, the constraint rows [H12_NCSTR_COLS + 4][N] into cstr: the 56 raw columns, the no_move flag,
+ * the pre-reset episode length, and foot_clearance's updated swing height (left, right)) evaluated on the workspace state as
  * it stands (post-physics, pre-reset; EPLEN already counted) with injected tau (N x 12, applied torque), jacc
  * (N x 12, joint acceleration) and fmax (N x 5: max over the contact history of |F| on the left / right foot,
- * left / right knee, torso).  Writes foot_clearance's swing height like a step.  Replaces nothing in the
+ * left / right knee, torso).  Read-only on the workspace: foot_clearance is evaluated on the stored swing height,
+ * which (unlike a step) is not updated -- the updated value goes to cstr's last two rows -- so calls between
+ * steps do not change the env.  Replaces nothing in the
  * reference: it exposes RewardManager / TerminationManager / ConstraintManager term functions
  * (velocity/mdp/rewards.py, utils/cat/constraints.py) for the reference-fixture tests. */
 int h12env_eval_terms(h12env* h, const float* tau, const float* jacc, const float* fmax, float* terms,

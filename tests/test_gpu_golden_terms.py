@@ -91,6 +91,12 @@ def test_kernel_constraints_match_reference_functions(gpu):
             src = ids[np.arange(n) % len(ids)]
             np.testing.assert_allclose(cs[nm][:, src].T, raw[:, nm], rtol=2e-6, atol=4e-6)
         assert (cs[0].astype(bool) == (raw[:, 0] > 0)).all() and (term.cpu().numpy() == (raw[:, 0] > 0)).all()
+        # the hook leaves the workspace's swing state alone and returns the updated one: carry it like a step
+        sw_ws = env._fstate[F["SWING_H"][0]:F["SWING_H"][0] + 2].clone()
+        _, _, _, cs2 = env.eval_terms(torch.as_tensor(d["tau"][t]), torch.zeros(n, 12), torch.as_tensor(fmax))
+        assert torch.equal(env._fstate[F["SWING_H"][0]:F["SWING_H"][0] + 2], sw_ws)   # read-only hook
+        assert np.array_equal(cs2.cpu().numpy(), cs)                                   # so a repeat is identical
+        env._fstate[F["SWING_H"][0]:F["SWING_H"][0] + 2] = torch.as_tensor(cs[58:60], device=env.device)
     sw = env._fstate[F["SWING_H"][0]:F["SWING_H"][0] + 2].T.cpu().numpy()
     np.testing.assert_allclose(sw, d["swing_max_height_final"], rtol=2e-6, atol=2e-6)
     env.close()
