@@ -7,8 +7,13 @@
 One step = one ManagerBasedRLEnv.step of every env on the GPU (4 physics steps of one implicit
 integration step each, delayed PD, contact, sensor, rewards, terminations, resets, commands,
 450-float observations).  Actions ~ N(0,1) are pre-generated and resident in HBM before timing.
-Envs shard across ranks (4096 per GPU, weak scaling, RNG keyed by global env id); no collective
-inside the timed region.
+Envs shard across ranks (4096 per GPU, weak scaling, RNG keyed by global env id).  With N > 1 the
+timed region is BASELINE config C4: every rank records its shard's rollout compactly (per env-step
+the new observation frame, action, reward, done flags: h12env.rollout), all-gathers it over RCCL in
+chunks of --gather-every steps on a side stream while it keeps stepping, and decodes the global
+(T = 24, N_global, 450) observation rows a PPO learner consumes; the line's c4_rollout_allgather
+splits env / all-gather / decode time.  N = 1 is config C2 (no collective; --rollout on forces the
+record + copy + decode path on one GPU).
 
 Steady state: episode_length_buf is randomised first (rsl_rl's init_at_random_ep_len) and a fixed
 burn-in (--burn-in, untimed, on top of --warmup) lets falls and time-outs reach their steady rate, so
@@ -68,6 +73,16 @@ def parse():
     p.add_argument("--explicit-penalty", action="store_true",
                    help="experiment: round-1 explicit penalty contact (use with --inner-steps 2)")
     p.add_argument("--no-self-collision", action="store_true", help="experiment: legs do not collide (not the metric)")
+    p.add_argument("--rollout", choices=("auto", "on", "off"), default="auto",
+                   help="BASELINE config C4: record the compact rollout (frame, action, reward, dones per env-step) and "
+                        "all-gather it over the ranks every --gather-every steps on a side stream, decoding the full "
+                        "(T, N_global, 450) observation rows on every rank, inside the timed region (auto: on when "
+                        "N > 1; N = 1 is config C2, the plain rollout)")
+    p.add_argument("--rollout-steps", type=int, default=24,
+                   help="rollout length T (num_steps_per_env, C12/agents/rsl_rl_ppo_cfg.py:12)")
+    p.add_argument("--gather-every", type=int, default=4, help="all-gather chunk length G in env steps (C4)")
+    p.add_argument("--dump-rollout", type=str, default=None,
+                   help="test hook: rank 0 saves the decoded rows and the gathered records of the timed window (.npz)")
     return p.parse_args()
 
 
@@ -276,11 +291,52 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    rollout = args.rollout == "on" or (args.rollout == "auto" and world > 1)
+    rg = None
+    if rollout:  # C4: compact rollout records all-gathered on a side stream and decoded on every rank
+        from h12env import distributed as D
+        from h12env.rollout import RolloutGather, RolloutRecorder
+
+        rec = RolloutRecorder(n, args.rollout_steps, dev, env.obs_dim // 45)
+        tail = torch.empty(world * n, env.obs_dim, device=dev)  # every env's row before the first step
+        if world > 1:
+            D.all_gather_into_tensor(tail, env.get_observations()["policy"].contiguous())
+        else:
+            tail.copy_(env.get_observations()["policy"])
+        rg = RolloutGather(rec, world, args.gather_every, tail, timing=True)
+        env.bind_rollout(rec)
+
+        def put_actions(i0):
+            def f(t0, t1):  # the chunk's actions (pool slices) into the records, one copy when contiguous
+                a0 = i0 % pool
+                span = t1 - t0
+                if a0 + span <= pool:
+                    rec.actions[t0:t1].copy_(actions[a0:a0 + span])
+                else:
+                    k = pool - a0
+                    rec.actions[t0:t0 + k].copy_(actions[a0:])
+                    rec.actions[t0 + k:t1].copy_(actions[:span - k])
+            return f
+
     barrier()
     snap = env.snapshot()  # replayed below (reset count + kernel timing of the same window)
+    ev_c = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     t0 = time.perf_counter()
+    ev_c[0].record()
     for i in range(K):
+        if rg is None:
+            env.step(actions[(B + W + i) % pool])
+            continue
+        rg.before_step()
+        tc = rec.t
         env.step(actions[(B + W + i) % pool])
+        rg.after_step(tc, put_actions(B + W + i - (tc - rg.chunk_of(tc)[1])))
+    if rg is not None:
+        tc = rec.t
+        rg.flush(tc if tc else 0, put_actions(B + W + K - (tc - rg.chunk_of(max(tc - 1, 0))[1])) if tc else None)
+    ev_c[1].record()
+    if rg is not None:
+        rg.wait()
     barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev)
@@ -289,6 +345,33 @@ def main():
 
         D.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    c4 = None
+    if rg is not None and args.dump_rollout and rank == 0:
+        import numpy as np
+
+        te = min(K, args.rollout_steps)
+        np.savez(args.dump_rollout, obs=rg.obs[:te].cpu().numpy(), gathered=rg.gathered.cpu().numpy(),
+                 tail=rg.tail.cpu().numpy(), off=np.array(rec.off), step_bytes=rec.step_bytes, T=te, G=rg.G,
+                 n=n, world=world, burn_in=B, warmup=W, steps=K, pool=pool)
+    if rg is not None:
+        st = rg.stats()
+        env_span = ev_c[0].elapsed_time(ev_c[1])
+        iters = K / args.rollout_steps
+        rec_b = rec.step_bytes
+        recv = st["gathered_bytes"] * (world - 1) / world  # bytes each rank receives from the others
+        c4 = {"rollout_steps": args.rollout_steps, "gather_every": rg.G, "chunks": st["chunks"],
+              "record_bytes_per_env_step": rec_b / n, "full_row_bytes_per_env_step": (env.obs_dim + 12 + 2) * 4,
+              "gathered_bytes": st["gathered_bytes"], "received_bytes_per_rank": recv,
+              "env_stream_ms_per_iter": env_span / iters, "allgather_ms_per_iter": st["gather_ms"] / iters,
+              "decode_ms_per_iter": st["decode_ms"] / iters, "ms_per_iter": 1e3 * dt / iters,
+              "allgather_algbw_gbs": st["gathered_bytes"] / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] else None,
+              "allgather_busbw_gbs": recv / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] and world > 1 else None,
+              "decoded_rows_bytes_per_iter": args.rollout_steps * world * n * env.obs_dim * 4,
+              "decode_gbs": (st["chunks"] and rg.G * world * n * env.obs_dim * 4 * st["chunks"] /
+                             (st["decode_ms"] * 1e-3) / 1e9) or None,
+              "overlap": "gathers + decodes on a side stream, concurrent with the next chunk's env steps",
+              "backend": (args.dist_backend if world > 1 else "copy (N = 1)")}
+        env.unbind_rollout()
     if args.profile_only:
         if rank == 0:
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * dt / K}))
@@ -373,8 +456,10 @@ def main():
                 "physics_dt": cfg.sim.dt,
                 "inner_steps": cfg.sim.inner_steps,
                 "implicit_penalty": bool(cfg.sim.implicit_penalty),
-                "parallelism": f"env-shard x{world}",
+                "parallelism": f"env-shard x{world}" + (f" + RCCL all-gather of the rollout every {rg.G} steps"
+                                                         if rg is not None and world > 1 else ""),
             },
+            "c4_rollout_allgather": c4,
             "burn_in": B,
             "resets_in_window": resets_in_window,
             "replay_bit_exact": replay_exact,

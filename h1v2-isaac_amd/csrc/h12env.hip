@@ -2059,6 +2059,7 @@ struct AsmArgs {
   float* log_part;  // step_kernel's per-block episode-log partials ([LOG_NPART][log_nb]) ...
   float* log_acc;   // ... folded into the caller's accumulator by block 0 (null: nothing to fold)
   int log_nb;
+  float* frame_out; // (n, 45) the new frames as they enter the history (h12env_step_out.frame_out), or null
 };
 constexpr int ASM_BLOCK = 256;
 
@@ -2218,7 +2219,10 @@ H12_DEV void obs_assemble_body(const KParams& P, const AsmArgs& A) {
     int tn = noise_index(c);
     float v = s_frame[k];
     if (tn >= 0) v += s_noise[row * 32 + tn];
-    s_frame[k] = v * P.oscale[term_index(c)];
+    v *= P.oscale[term_index(c)];
+    s_frame[k] = v;
+    // rollout record: the block's rows are consecutive, so its frames are one contiguous run of rows x 45 floats
+    if (A.frame_out && row < rows) A.frame_out[(size_t)r0 * H12_OBS_FRAME + k] = v;
   }
   __syncthreads();
   // phase 3: assemble + store (obs may alias obs_prev: every read of these rows happened in phase 1)
@@ -2936,6 +2940,124 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
   store_env<K>(P, W, e, leg, s);
 }
 
+// ------------------------------------------------------------------ rollout records (C4: all-gathered rollouts)
+// Step record of one shard (h12env_rollout_layout): frames f32 [n][45], actions f32 [n][12], rewards f32 [n],
+// terminated u8 [n], truncated u8 [n], each section 256-B aligned; gathered in chunks of G steps (see the header).
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+void rollout_offsets(int n, size_t* off, size_t* step) {
+  const size_t nn = (size_t)n;
+  off[0] = 0;
+  off[1] = align256(off[0] + nn * H12_OBS_FRAME * 4);
+  off[2] = align256(off[1] + nn * H12_NJ * 4);
+  off[3] = align256(off[2] + nn * 4);
+  off[4] = align256(off[3] + nn);
+  *step = align256(off[4] + nn);
+}
+
+// Observation rows from rollout records (h12env_rollout_decode).  One block per DEC_ENVS consecutive envs of one
+// shard, all rows of [t0, t1) in windows of DEC_WT rows: the block stages its envs' tail rows once and, per window,
+// the frames the window's rows can reach (steps [w0 - (H - 1), w1)) and each env's last done step per row, then
+// writes the rows -- for a fixed t the block's ne rows are one contiguous run of ne * 45H floats (float4 stores
+// when 16-B aligned).  HBM-bound on the row stores; each frame is read once per window.
+constexpr int DEC_ENVS = 8, DEC_BLOCK = 256, DEC_WT = 16, DEC_FR = DEC_WT + H12_NHIST - 1, DEC_MAX_BLOCKS = 96;
+struct DecArgs {
+  const uint8_t* rec;  // gathered records
+  size_t step_bytes, off[5];
+  int n_shards, n, T, G, t0, t1;
+  const float* tail;
+  float* out;
+};
+// step s of shard r in the gathered buffer (chunk-major, then shard, then step)
+__device__ __forceinline__ const uint8_t* dec_step(const DecArgs& D, int r, int s) {
+  const int c = s / D.G, gc = min(D.G, D.T - c * D.G);
+  return D.rec + ((size_t)c * D.G * D.n_shards + (size_t)r * gc + (size_t)(s - c * D.G)) * D.step_bytes;
+}
+// float copy global -> LDS, float4 when both ends are 16-B aligned (all loads issued before any use)
+__device__ __forceinline__ void dec_stage(float* dst, const float* src, int cnt, int tid) {
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int j = tid; j < cnt / 4; j += DEC_BLOCK) d4[j] = s4[j];
+    for (int k = (cnt / 4) * 4 + tid; k < cnt; k += DEC_BLOCK) dst[k] = src[k];
+  } else {
+    for (int k = tid; k < cnt; k += DEC_BLOCK) dst[k] = src[k];
+  }
+}
+
+template <int NH>
+__global__ void __launch_bounds__(DEC_BLOCK) rollout_decode_kernel(DecArgs D) {
+  constexpr int ROW = H12_OBS_FRAME * NH;
+  __shared__ __attribute__((aligned(16))) float s_tail[DEC_ENVS * ROW];
+  __shared__ __attribute__((aligned(16))) float s_fr[DEC_FR][DEC_ENVS * H12_OBS_FRAME];
+  __shared__ uint8_t s_dn[DEC_FR][DEC_ENVS];
+  __shared__ int s_last[DEC_ENVS][DEC_WT];
+  __shared__ uint32_t s_col[ROW];
+  const int tid = threadIdx.x;
+  const int bps = (D.n + DEC_ENVS - 1) / DEC_ENVS;
+  const size_t NG = (size_t)D.n_shards * D.n;
+  for (int col = tid; col < ROW; col += DEC_BLOCK) {  // frame component, term width, slot (0 oldest)
+    const uint32_t ce = asm_col_entry<NH>(col);
+    const int c = (int)(ce & 0xFFu);
+    const int h = c < 9 ? (col % (3 * NH)) / 3 : ((col - 9 * NH) % (12 * NH)) / 12;
+    s_col[col] = (ce & 0xFFFFu) | ((uint32_t)h << 16);
+  }
+  // a capped grid strides over the env groups (DEC_MAX_BLOCKS: the decode runs beside the env kernels on a side
+  // stream and must leave them CUs)
+  for (int grp = blockIdx.x; grp < D.n_shards * bps; grp += gridDim.x) {
+  const int shard = grp / bps, e0 = (grp - shard * bps) * DEC_ENVS;
+  const int ne = min(DEC_ENVS, D.n - e0);
+  const size_t g0 = (size_t)shard * D.n + e0;
+  __syncthreads();  // the previous group's stores read s_tail
+  // the envs' rows before step 0 (every read of them precedes the first row store: tail may alias the output)
+  dec_stage(s_tail, D.tail + g0 * ROW, ne * ROW, tid);
+  for (int w0 = D.t0; w0 < D.t1; w0 += DEC_WT) {
+    const int w1 = min(w0 + DEC_WT, D.t1);
+    // steps a row of the window can reach: [w0 - (H - 1), w1).  A done step before f0 cannot matter (every slot's
+    // step is >= t - (H - 1) >= f0), so the last done step is looked for inside the window only
+    const int f0 = max(0, w0 - (NH - 1)), nf = w1 - f0;
+    __syncthreads();  // the previous window's stores read s_fr / s_last
+    for (int ts = 0; ts < nf; ++ts)
+      dec_stage(s_fr[ts], reinterpret_cast<const float*>(dec_step(D, shard, f0 + ts) + D.off[0]) + (size_t)e0 * H12_OBS_FRAME,
+                ne * H12_OBS_FRAME, tid);
+    if (tid < nf * ne) {
+      const int ts = tid / ne, e = tid - ts * ne;
+      const uint8_t* st = dec_step(D, shard, f0 + ts);
+      s_dn[ts][e] = st[D.off[3] + e0 + e] | st[D.off[4] + e0 + e];
+    }
+    __syncthreads();
+    if (tid < ne) {
+      int last = -1;
+      for (int ts = 0; ts < nf; ++ts) {
+        if (s_dn[ts][tid]) last = f0 + ts;
+        if (f0 + ts >= w0) s_last[tid][f0 + ts - w0] = last;
+      }
+    }
+    __syncthreads();
+    for (int t = w0; t < w1; ++t) {
+      float* dst = D.out + ((size_t)t * NG + g0) * ROW;
+      auto value = [&](int k) -> float {
+        const int e = k / ROW, col = k - e * ROW;
+        const uint32_t ce = s_col[col];
+        const int c = (int)(ce & 0xFFu), d = (int)((ce >> 8) & 0xFFu), h = (int)(ce >> 16);
+        int src = t - (NH - 1 - h);
+        const int last = s_last[e][t - w0];
+        if (src < last) src = last;
+        return src >= 0 ? s_fr[src - f0][e * H12_OBS_FRAME + c] : s_tail[e * ROW + col + (t + 1) * d];
+      };
+      const int cnt = ne * ROW;
+      if (((uintptr_t)dst & 15u) == 0) {
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int j = tid; j < cnt / 4; j += DEC_BLOCK)
+          d4[j] = make_float4(value(4 * j), value(4 * j + 1), value(4 * j + 2), value(4 * j + 3));
+        for (int k = (cnt / 4) * 4 + tid; k < cnt; k += DEC_BLOCK) dst[k] = value(k);
+      } else {
+        for (int k = tid; k < cnt; k += DEC_BLOCK) dst[k] = value(k);
+      }
+    }
+  }
+  }
+}
+
 // ------------------------------------------------------------------ host side
 struct Handle {
   KParams P;
@@ -3203,8 +3325,10 @@ int feature_level(const KParams& P) {
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
-                    hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, float* log_acc = nullptr) {
+                    hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, float* log_acc = nullptr,
+                    float* frame_out = nullptr) {
   AsmArgs A = {};
+  A.frame_out = frame_out;
   A.log_part = h->log_part;
   A.log_acc = log_acc;
   A.log_nb = n_blocks(h);
@@ -3221,6 +3345,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.lo = lo;
   A.hi = hi;
   if (h->P.task == H12_TASK_ROUGH) {
+    if (frame_out) return set_err(H12_E_ARG, "frame_out needs the flat observation layout (history)");
     const int nb = (int)(((size_t)h->W.n * H12_NOBS_ROUGH + ASM_BLOCK - 1) / ASM_BLOCK);
     hipExtLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, h->P, A);
     HIP_TRY(hipGetLastError());
@@ -3521,7 +3646,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   timing_events(h, 1, &t0, &t1);
   // fill = terminated | truncated: the envs reset inside the step restart their history
   return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
-                         (hipStream_t)stream, t0, t1, out->log_acc);
+                         (hipStream_t)stream, t0, t1, out->log_acc, out->frame_out);
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
@@ -3576,6 +3701,42 @@ int h12env_eval_self_contacts(h12env* hh, float* out, void* stream) {
   if (!out) return set_err(H12_E_ARG, "out is required");
   if (!h->P.self_coll) return set_err(H12_E_STATE, "self_collision is off in this env's config");
   LAUNCH_K(selfc_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, out);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int h12env_rollout_layout(int n, size_t offsets[5], size_t* step_bytes) {
+  if (n < 1 || !offsets || !step_bytes) return set_err(H12_E_ARG, "n >= 1 and output pointers required");
+  rollout_offsets(n, offsets, step_bytes);
+  return 0;
+}
+
+int h12env_rollout_decode(const void* records, int n_shards, int n, int T, int G, int history, int t0, int t1,
+                          const float* tail, float* obs_out, void* stream) {
+  if (!records || !tail || !obs_out) return set_err(H12_E_ARG, "records, tail and obs_out are required");
+  if (n_shards < 1 || n < 1 || T < 1 || G < 1) return set_err(H12_E_ARG, "n_shards, n, T, G must be >= 1");
+  if (history < 1 || history > H12_NHIST) return set_err(H12_E_ARG, "history %d out of 1..%d", history, H12_NHIST);
+  if (t0 < 0 || t1 > T || t0 > t1) return set_err(H12_E_ARG, "rows [%d, %d) outside [0, %d]", t0, t1, T);
+  if (t0 == t1) return 0;
+  DecArgs D = {};
+  D.rec = (const uint8_t*)records;
+  rollout_offsets(n, D.off, &D.step_bytes);
+  D.n_shards = n_shards;
+  D.n = n;
+  D.T = T;
+  D.G = min(G, T);
+  D.t0 = t0;
+  D.t1 = t1;
+  D.tail = tail;
+  D.out = obs_out;
+  const int nb = min(n_shards * ((n + DEC_ENVS - 1) / DEC_ENVS), DEC_MAX_BLOCKS);
+  hipStream_t st = (hipStream_t)stream;
+#define H12_DEC_CASE(NH) case NH: hipLaunchKernelGGL(rollout_decode_kernel<NH>, dim3(nb), dim3(DEC_BLOCK), 0, st, D); break;
+  switch (history) {
+    H12_DEC_CASE(1) H12_DEC_CASE(2) H12_DEC_CASE(3) H12_DEC_CASE(4) H12_DEC_CASE(5)
+    H12_DEC_CASE(6) H12_DEC_CASE(7) H12_DEC_CASE(8) H12_DEC_CASE(9) H12_DEC_CASE(10)
+  }
+#undef H12_DEC_CASE
   HIP_TRY(hipGetLastError());
   return 0;
 }

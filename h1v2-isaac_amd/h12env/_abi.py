@@ -22,7 +22,7 @@ NLOG = 46        # log accumulator: NREW episode sums, count, time-out count, ba
                  # then per constraint term the summed violation rates (10) and mean probabilities (10),
                  # then the summed command metrics error_vel_xy, error_vel_yaw (LOG_METRIC)
 LOG_METRIC = 44
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MODE_ISAACLAB = 0
 MODE_MUJOCO = 1
@@ -210,6 +210,7 @@ class H12StepOut(C.Structure):
         ("applied_torque", C.c_void_p),
         ("foot_force", C.c_void_p),
         ("cstr_prob", C.c_void_p),
+        ("frame_out", C.c_void_p),
     ]
 
 
@@ -259,6 +260,10 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_set_terrain.restype = C.c_int
     lib.h12env_step_physics.argtypes = [vp, vp, C.c_int, vp]
     lib.h12env_step_physics.restype = C.c_int
+    lib.h12env_rollout_layout.argtypes = [C.c_int, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+    lib.h12env_rollout_layout.restype = C.c_int
+    lib.h12env_rollout_decode.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
+    lib.h12env_rollout_decode.restype = C.c_int
     lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
     lib.h12env_field_ptr.restype = vp
     lib.h12env_eval_terms.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -309,4 +314,5 @@ EXPORTED_SYMBOLS = [
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
     "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms", "h12env_eval_self_contacts",
+    "h12env_rollout_layout", "h12env_rollout_decode",
 ]

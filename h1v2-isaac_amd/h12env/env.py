@@ -296,6 +296,7 @@ class H12VelocityEnv:
         # |net contact force| of the left / right foot over the last physics step (ContactSensor of the feet)
         self.foot_contact_force = torch.zeros(n, 2, device=self.device)
         self._step_outs = []  # per observation buffer: (H12StepOut, byref), see _build_step_outs
+        self._rollout = None  # bind_rollout: compact rollout records written by the step kernels
         self.common_step_counter = 0
         self.extras: dict = {}
         self.terrain = None
@@ -536,7 +537,16 @@ class H12VelocityEnv:
                     del self._live_logs[t0]
             self._log_ring[slot:slot + _LOG_CHUNK].zero_()
         # the output pointers are fixed per observation buffer (built once, _step_outs); only the log slot moves
-        o, o_ref = self._step_outs[self._k]
+        rec = self._rollout
+        if rec is None:
+            o, o_ref = self._step_outs[self._k]
+        else:  # rollout record t: reward, done flags and the new frame go straight into it
+            t = rec.t
+            o, o_ref = self._rollout_outs[self._k]
+            o.rew, o.terminated, o.truncated, o.frame_out = self._rollout_ptrs[t]
+            self.reward_buf, self.reset_terminated, self.reset_time_outs = self._rollout_views[t]
+            self.reset_buf = self.reset_terminated
+            rec.t = t + 1 if t + 1 < rec.T else 0
         o.log_acc = self._log_ptr + slot * (NLOG * 4)
         rc = self._lib.h12env_step(self._h, a.data_ptr(), prev.data_ptr(), o_ref, self.common_step_counter,
                                    _raw_stream(self._dev_index))
@@ -550,6 +560,35 @@ class H12VelocityEnv:
         if self._cat:  # CaTEnv.step: dones = constraint termination probability, 1 where reset (cat_env.py:153-193)
             return {"policy": obs_out}, self.reward_buf, self._dones, self.reset_time_outs, self.extras
         return {"policy": obs_out}, self.reward_buf, self.reset_terminated, self.reset_time_outs, self.extras
+
+    def bind_rollout(self, rec):
+        """Record every following step into the compact rollout ``rec`` (h12env.rollout.RolloutRecorder; BASELINE
+        config C4): the step's reward, terminated / truncated flags and new observation frame (as it enters the
+        history) are written by the kernels straight into step record ``rec.t``, which then advances (mod T); the
+        returned reward / flag tensors are views of that record.  Flat observation layout only (the frames rebuild
+        the history rows)."""
+        if self.obs_dim == NOBS_ROUGH or self._cat:
+            raise ValueError("bind_rollout needs the flat observation layout (history) and a non-CaT task")
+        if rec.n != self.num_envs or rec.history * 45 != self.obs_dim:
+            raise ValueError("rollout recorder was built for another env shape")
+        self._rollout_saved = (self.reward_buf, self.reset_terminated, self.reset_time_outs)
+        self._rollout_ptrs = [(rec.rewards[t].data_ptr(), rec.terminated[t].data_ptr(), rec.truncated[t].data_ptr(),
+                               rec.frames[t].data_ptr()) for t in range(rec.T)]
+        self._rollout_views = [(rec.rewards[t], rec.terminated[t], rec.truncated[t]) for t in range(rec.T)]
+        self._rollout_outs = []
+        for k in range(2):
+            o = H12StepOut()
+            src = self._step_outs[k][0]
+            for name, _ in H12StepOut._fields_:
+                setattr(o, name, getattr(src, name))
+            self._rollout_outs.append((o, C.byref(o)))
+        self._rollout = rec
+
+    def unbind_rollout(self):
+        if self._rollout is not None:
+            self.reward_buf, self.reset_terminated, self.reset_time_outs = self._rollout_saved
+            self.reset_buf = self.reset_terminated
+            self._rollout = None
 
     def step_physics(self, q_ref: torch.Tensor, n_substeps: int):
         """Parity hook: physics only, PD towards a held joint target (h12env_step_physics)."""

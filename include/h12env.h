@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 7
+#define H12ENV_ABI_VERSION 8
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -303,6 +303,10 @@ typedef struct h12env_step_out {
   float* foot_force;       /* N x 2,  |net contact force| of the feet, last physics step */
   float* cstr_prob;        /* N, CaT task: the dones CaTEnv.step returns (constraint termination probability,
                               1 for envs reset this step); the reward is already scaled by 1 - p */
+  float* frame_out;        /* (ABI 8) N x 45, flat layout only: the step's new observation frame exactly as it
+                              enters the history (noise added, term scales applied) -- the newest slot of every
+                              term of obs.  With terminated / truncated it is the rollout record of the step from
+                              which h12env_rollout_decode rebuilds the observation rows bit for bit */
 } h12env_step_out;
 
 typedef struct h12env h12env;
@@ -353,6 +357,29 @@ int h12env_eval_terms(h12env* h, const float* tau, const float* jacc, const floa
  * right), body (knee, foot): moment xyz, force xyz in body coordinates.  Replaces nothing in the reference (its
  * self-collisions live inside PhysX, ArticulationCfg enabled_self_collisions, A/robots/h12.py:32). */
 int h12env_eval_self_contacts(h12env* env, float* out, void* stream);
+/* ---- Rollout records (ABI 8; BASELINE config C4: the rollout buffer all-gathered over xGMI for PPO).
+ * rsl_rl's RolloutStorage keeps (T, N, 450) observations per iteration (T = num_steps_per_env 24,
+ * C12/agents/rsl_rl_ppo_cfg.py:12).  A 450-float row is 10 frames of 45 floats, nine of them already in the previous
+ * row (CircularBuffer, T/utils/history/circular_buffer.py:79-170), so a shard's rollout is recorded compactly --
+ * per env-step the new frame (h12env_step_out.frame_out), the action, the reward and the two done flags: 238 B
+ * instead of 1856 B -- gathered over the ranks, and the full rows are rebuilt on every receiving GPU.
+ * Step record of one shard of n envs (byte offsets from h12env_rollout_layout, each section 256-B aligned):
+ *   [0] frames f32 [n][45]   [1] actions f32 [n][12]   [2] rewards f32 [n]   [3] terminated u8 [n]
+ *   [4] truncated u8 [n]
+ * A shard's rollout is T step records back to back ([T][step_bytes]).  It is all-gathered in chunks of G steps
+ * (the last chunk may be shorter): chunk c (steps [cG, cG + Gc)) is one all_gather_into_tensor of the shards'
+ * bytes [cG, cG + Gc) x step_bytes, so the gathered buffer is, per chunk in order, n_shards runs of Gc step
+ * records (G = T: n_shards whole rollouts back to back).  Global env id = shard * n + local id. */
+int h12env_rollout_layout(int n, size_t offsets[5], size_t* step_bytes);
+/* Rebuild observation rows from gathered rollout records: obs_out[t][g][:] (T x n_shards*n x 45*history) is the
+ * observation the env returned after step t for global env g, for t in [t0, t1) (the records of steps < t1 must be
+ * present).  tail (n_shards*n x 45*history) holds each env's observation before step 0 of the records (the last
+ * row of the previous iteration); it may alias obs_out's row T - 1 (every block reads its envs' tail rows before
+ * it writes any of their rows).  Rows are bit-identical to the env's own: slot h of row t is the frame of step
+ * t - (history - 1 - h), or of the env's last done step <= t if that is later (a reset refills the history), or,
+ * before step 0, the tail row's slot h + t + 1. */
+int h12env_rollout_decode(const void* records, int n_shards, int n, int T, int G, int history, int t0, int t1,
+                          const float* tail, float* obs_out, void* stream);
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);
