@@ -133,6 +133,7 @@ struct KParams {
   int self_coll;          // self-collision between the legs (h12env_config.self_collision)
   float sk, sc, sct, smu; // its normal stiffness / damping, tangential damping, Coulomb cap
   float dl;               // implicit joint-limit inertia h (lc + h lk) (lc already includes h lk)
+  float lproj;            // hard-limit projection tolerance (h12env_config.limit_projection; 3e38: off)
   float cmd_T, cmd_x0, cmd_x1, cmd_y0, cmd_y1, cmd_w0, cmd_w1, cmd_h0, cmd_h1;
   float rel_stand, rel_head, head_k;
   float rx0, rx1, ry0, ry1, ryaw0, ryaw1, root_z;
@@ -329,13 +330,15 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   } else {
     depth = rad - xw[2];
   }
-  if (!(depth > 0.f)) return false;
   float vl[3];
   cross(vb, pl, vl);
   vl[0] += vb[3]; vl[1] += vb[4]; vl[2] += vb[5];
   float vw[3];
   mv(Rb, vl, vw);
   float vn = TERRAIN ? nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2] : vw[2];
+  // active when the point is predicted below the ground at the end of the step (implicit: depth - h vn; oracle
+  // contact_point), so a point arriving at speed is caught within the step instead of one step deep
+  if (!(depth - (P.impl ? P.h * vn : 0.f) > 0.f)) return false;
   float fn = P.ck * depth - P.cc * vn;
   if (!(fn > 0.f)) return false;
   float ft0, ft1;
@@ -627,10 +630,10 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
     float r[3];
     mv(R, h12m::FOOT[q], r);
     const float depth = h12m::FOOT_R - (r[2] + pf[2]);
-    if (!(depth > 0.f)) continue;
     float vw[3];
     cross(ww, r, vw);
     vw[0] += v0[0]; vw[1] += v0[1]; vw[2] += v0[2];
+    if (!(depth - (P.impl ? P.h * vw[2] : 0.f) > 0.f)) continue;  // predicted end-of-step depth (contact_sphere)
     const float fn = P.ck * depth - P.cc * vw[2];
     if (!(fn > 0.f)) continue;
     const float x0 = r[0] + pf[0], x1 = r[1] + pf[1];
@@ -1055,11 +1058,12 @@ H12_DEV void joint_terms(const KParams& P, const Leg& lg, float h, float* tq, fl
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     const float q = lg.q[k], qd = lg.qd[k];
-    // joint-limit penalty, branch-free (selects instead of divergent branches); dl: h (lc + h lk) of an active
-    // limit (oracle joint_limit_torque)
-    const float dhi = q - h12m::QHI[k], dlo = q - h12m::QLO[k];
+    // joint limit, branch-free (selects instead of divergent branches): with the implicit penalty active when the
+    // predicted end-of-step position q + h qd is beyond the range; dl: h (lc + h lk) of an active limit (oracle
+    // joint_limit_torque)
+    const float dhi = q - h12m::QHI[k], dlo = q - h12m::QLO[k], hq = P.impl ? h * qd : 0.f;
     const float thi = fminf(0.f, -P.lk * dhi - P.lc * qd), tlo = fmaxf(0.f, -P.lk * dlo - P.lc * qd);
-    const float tl = dhi > 0.f ? thi : (dlo < 0.f ? tlo : 0.f);
+    const float tl = dhi + hq > 0.f ? thi : (dlo + hq < 0.f ? tlo : 0.f);
     float t = tl;
     dl[k] = tl != 0.f ? P.dl : 0.f;
     // PhysX max joint velocity: implicit stiff damper on the excess with a C1 ramp-in over H12_VLIM_RAMP
@@ -1472,7 +1476,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     lg.qd[k] += h * qdd[k];
-    lg.q[k] += h * lg.qd[k];
+    float q = lg.q[k] + h * lg.qd[k];
+    // hard-limit residual (oracle limit_projection): beyond the range by more than lproj -> back to the tolerance,
+    // outward velocity zeroed; branch-free
+    const float hi = h12m::QHI[k] + P.lproj, lo = h12m::QLO[k] - P.lproj;
+    const bool over = q > hi, under = q < lo;
+    lg.qd[k] = over ? fminf(lg.qd[k], 0.f) : (under ? fmaxf(lg.qd[k], 0.f) : lg.qd[k]);
+    lg.q[k] = fminf(fmaxf(q, lo), hi);
   }
   if constexpr (HW) {
     if (more) {
@@ -3184,6 +3194,8 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.impl = c->implicit_penalty != 0;
   P.self_coll = c->self_collision != 0;
   P.sk = c->self_k; P.sc = c->self_c; P.sct = c->self_ct; P.smu = c->self_mu;
+  if (!(c->limit_projection >= 0.f)) return set_err(H12_E_ARG, "limit_projection must be >= 0");
+  P.lproj = c->limit_projection > 0.f ? c->limit_projection : 3.0e38f;
   P.dl = 0.f;
   if (P.impl) {  // the springs act at the end of the substep: extra damping h k (oracle contact_point)
     P.cc = c->contact_c + P.h * c->contact_k;
@@ -3406,8 +3418,9 @@ int h12env_config_default(h12env_config* c) {
   for (int j = 0; j < H12_NJ; ++j) c->max_joint_vel[j] = vmax[j % 6];
   c->max_joint_vel_damping = 1.0e3f;
   c->self_collision = 1; c->self_k = 3e4f; c->self_c = 50.f; c->self_ct = 50.f; c->self_mu = 0.36f;
-  c->contact_k = 3e4f; c->contact_c = 100.f; c->friction_k = 3e4f; c->friction_c = 100.f;
-  c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1000.f; c->limit_c = 2.f; c->contact_threshold = 1.f;
+  c->contact_k = 5e5f; c->contact_c = 300.f; c->friction_k = 3e4f; c->friction_c = 100.f;
+  c->limit_projection = 0.01f;
+  c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1.0e6f; c->limit_c = 2.f; c->contact_threshold = 1.f;
   c->cmd_resample_time = 10.f;
   c->cmd_lin_x[0] = 0.f; c->cmd_lin_x[1] = 1.f; c->cmd_lin_y[0] = -0.5f; c->cmd_lin_y[1] = 0.5f;
   c->cmd_ang_z[0] = -1.f; c->cmd_ang_z[1] = 1.f;
@@ -3738,6 +3751,52 @@ int h12env_rollout_decode(const void* records, int n_shards, int n, int T, int G
   }
 #undef H12_DEC_CASE
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+struct h12env_fence {
+  uint64_t* ctr;
+  int n;
+  int device;
+};
+
+int h12env_fence_create(int device, int n_slots, h12env_fence** out) {
+  if (!out || n_slots < 1) return set_err(H12_E_ARG, "n_slots >= 1 and out required");
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(device));
+  int ok = 0;
+  HIP_TRY(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, device));
+  if (!ok) return set_err(H12_E_STATE, "device %d does not support hipStreamWaitValue64", device);
+  h12env_fence* f = new (std::nothrow) h12env_fence();
+  if (!f) return set_err(H12_E_ALLOC, "host allocation failed");
+  hipError_t e = hipExtMallocWithFlags((void**)&f->ctr, sizeof(uint64_t) * (size_t)n_slots, hipMallocSignalMemory);
+  if (e == hipSuccess) e = hipMemset(f->ctr, 0, sizeof(uint64_t) * (size_t)n_slots);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    delete f;
+    return set_err(H12_E_ALLOC, "signal memory: %s", hipGetErrorString(e));
+  }
+  f->n = n_slots;
+  f->device = device;
+  *out = f;
+  return 0;
+}
+
+void h12env_fence_destroy(h12env_fence* f) {
+  if (!f) return;
+  if (f->ctr) (void)hipFree(f->ctr);
+  delete f;
+}
+
+int h12env_fence_signal(h12env_fence* f, int slot, uint64_t value, void* stream) {
+  if (!f || slot < 0 || slot >= f->n) return set_err(H12_E_ARG, "bad fence or slot");
+  HIP_TRY(hipStreamWriteValue64((hipStream_t)stream, f->ctr + slot, value, 0));
+  return 0;
+}
+
+int h12env_fence_wait(h12env_fence* f, int slot, uint64_t value, void* stream) {
+  if (!f || slot < 0 || slot >= f->n) return set_err(H12_E_ARG, "bad fence or slot");
+  HIP_TRY(hipStreamWaitValue64((hipStream_t)stream, f->ctr + slot, value, hipStreamWaitValueGte, ~0ull));
   return 0;
 }
 

@@ -197,6 +197,7 @@ class H12Config(C.Structure):
         ("self_c", f32),
         ("self_ct", f32),
         ("self_mu", f32),
+        ("limit_projection", f32),
     ]
 
 
@@ -264,6 +265,14 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_rollout_layout.restype = C.c_int
     lib.h12env_rollout_decode.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
     lib.h12env_rollout_decode.restype = C.c_int
+    lib.h12env_fence_create.argtypes = [C.c_int, C.c_int, C.POINTER(vp)]
+    lib.h12env_fence_create.restype = C.c_int
+    lib.h12env_fence_destroy.argtypes = [vp]
+    lib.h12env_fence_destroy.restype = None
+    lib.h12env_fence_signal.argtypes = [vp, C.c_int, C.c_uint64, vp]
+    lib.h12env_fence_signal.restype = C.c_int
+    lib.h12env_fence_wait.argtypes = [vp, C.c_int, C.c_uint64, vp]
+    lib.h12env_fence_wait.restype = C.c_int
     lib.h12env_field_ptr.argtypes = [vp, C.c_int, C.c_int]
     lib.h12env_field_ptr.restype = vp
     lib.h12env_eval_terms.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -314,5 +323,6 @@ EXPORTED_SYMBOLS = [
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
     "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms", "h12env_eval_self_contacts",
-    "h12env_rollout_layout", "h12env_rollout_decode",
+    "h12env_rollout_layout", "h12env_rollout_decode", "h12env_fence_create", "h12env_fence_destroy",
+    "h12env_fence_signal", "h12env_fence_wait",
 ]

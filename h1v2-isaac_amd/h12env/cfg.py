@@ -46,12 +46,25 @@ class SimCfg:
     self_c: float = 50.0
     self_ct: float = 50.0
     self_mu: float = 0.36
-    contact_k: float = 3.0e4
-    contact_c: float = 100.0
+    # ground contact: sole spheres / knee / torso; stiff (PhysX's contacts are rigid: median sole penetration
+    # 1.8 mm under random actions), active on the predicted end-of-step depth, implicit
+    contact_k: float = 5.0e5
+    contact_c: float = 300.0
+    # the explicit integrator (implicit_penalty = False: MuJoCo mode, the round-1 scheme) keeps the soft contact it is
+    # stable with
+    contact_k_explicit: float = 3.0e4
+    contact_c_explicit: float = 100.0
     friction_k: float = 3.0e4
     friction_c: float = 100.0
-    limit_k: float = 1.0e3
+    # joint limits: PhysX holds the URDF ranges as hard limits; here a stiff spring on the predicted end-of-step
+    # position, integrated implicitly.  The explicit integrator (implicit_penalty = False:
+    # MuJoCo mode, the round-1 scheme) keeps the soft limit_k_explicit, all it is stable with
+    limit_k: float = 1.0e6
+    limit_k_explicit: float = 1.0e3
     limit_c: float = 2.0
+    # a joint still carried further than this past its range within a step is projected back (hard-limit residual;
+    # implicit scheme only)
+    limit_projection: float = 0.01
     static_friction: float = 0.8   # randomize_rigid_body_material startup (velocity_env_cfg.py:153-163)
     dynamic_friction: float = 0.6
 
@@ -537,10 +550,12 @@ class H12FlatEnvCfg:
         c.fix_base = int(self.fix_base)
         c.use_frictionloss = 0
         s = self.sim
-        c.contact_k, c.contact_c = s.contact_k, s.contact_c
+        c.contact_k, c.contact_c = ((s.contact_k, s.contact_c) if s.implicit_penalty
+                                    else (s.contact_k_explicit, s.contact_c_explicit))
         c.friction_k, c.friction_c = s.friction_k, s.friction_c
         c.mu_static, c.mu_dynamic = s.static_friction, s.dynamic_friction
-        c.limit_k, c.limit_c = s.limit_k, s.limit_c
+        c.limit_k, c.limit_c = (s.limit_k if s.implicit_penalty else s.limit_k_explicit), s.limit_c
+        c.limit_projection = s.limit_projection if s.implicit_penalty else 0.0
         c.contact_threshold = self.terminations.base_contact_threshold
         bv = self.commands.base_velocity
         c.cmd_resample_time, c.cmd_resample_time_max = bv.resampling_time_range

@@ -80,6 +80,37 @@ def decode(records: torch.Tensor, n_shards: int, n: int, T: int, G: int, history
         check(lib, rc, "h12env_rollout_decode")
 
 
+class StreamFence:
+    """Counters in signal memory ordering two streams without HIP events (h12env_fence_*): ``signal`` enqueues
+    counter[slot] = value behind the stream's earlier work, ``wait`` holds the stream's later work until
+    counter[slot] >= value."""
+
+    def __init__(self, device, n_slots: int):
+        self._lib = load_library()
+        h = C.c_void_p()
+        dev = torch.device(device)
+        check(self._lib, self._lib.h12env_fence_create(dev.index or 0, n_slots, C.byref(h)), "h12env_fence_create")
+        self._h = h
+
+    def signal(self, slot: int, value: int, stream) -> None:
+        rc = self._lib.h12env_fence_signal(self._h, slot, value, stream.cuda_stream)
+        if rc:
+            check(self._lib, rc, "h12env_fence_signal")
+
+    def wait(self, slot: int, value: int, stream) -> None:
+        rc = self._lib.h12env_fence_wait(self._h, slot, value, stream.cuda_stream)
+        if rc:
+            check(self._lib, rc, "h12env_fence_wait")
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._lib.h12env_fence_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
 class RolloutGather:
     """Chunked all-gather of the shards' rollout records on a side stream, each chunk decoded into the global
     (T, N_global, 45H) observation rows right after it arrives -- while the env keeps stepping on its own stream.
@@ -90,7 +121,8 @@ class RolloutGather:
     that chunk (``before_step``), so the records are double-use safe with one buffer.  world == 1: the gather is a
     device copy (same code path, no collective)."""
 
-    def __init__(self, rec: RolloutRecorder, world: int, G: int, tail: torch.Tensor, timing: bool = False):
+    def __init__(self, rec: RolloutRecorder, world: int, G: int, tail: torch.Tensor, timing: bool = False,
+                 sync: str = "fence"):
         self.rec, self.world, self.G = rec, int(world), max(1, min(int(G), rec.T))
         dev = rec.record.device
         self.gathered = torch.empty(self.world * rec.record.numel(), dtype=torch.uint8, device=dev)
@@ -106,6 +138,12 @@ class RolloutGather:
         self._ev = [(torch.cuda.Event(), torch.cuda.Event()) for _ in range(nchunks)]  # (ready, done), reused
         self._last_row = self.obs[rec.T - 1]     # the next iteration's tail
         self.prof = None                         # diagnostics: host seconds per _launch segment (dict)
+        # stream ordering: "fence" (signal-memory counters: slot 0 = chunks recorded, slot 1 = chunks gathered) or
+        # "event" (HIP events; ~100 us of host time per hand-off on this stack, tools/stream_diag.py)
+        self.sync = sync
+        self.fence = StreamFence(dev, 2) if sync == "fence" else None
+        self.seq = 0                              # chunks launched so far
+        self.chunk_seq = [0] * nchunks            # per chunk index: sequence number of its last gather
         self.timing = timing
         self.times: list[tuple] = []             # (chunk bytes, gather event pair, decode event pair)
         self.iterations = 0
@@ -119,7 +157,12 @@ class RolloutGather:
         """Call before env.step: the step record about to be written must have left in the previous gather."""
         t = self.rec.t
         c, t0, _ = self.chunk_of(t)
-        if t == t0 and self.done_ev[c] is not None:
+        if t != t0:
+            return
+        if self.fence is not None:
+            if self.chunk_seq[c]:
+                self.fence.wait(1, self.chunk_seq[c], self.compute)
+        elif self.done_ev[c] is not None:
             self.compute.wait_event(self.done_ev[c])
 
     def after_step(self, t: int, actions=None):
@@ -150,9 +193,15 @@ class RolloutGather:
             p0 = time.perf_counter()
         if actions is not None:
             actions(t0, t1)
+        self.seq += 1
+        seq = self.seq
         ready, done = self._ev[c]
-        ready.record(self.compute)
-        self.comm.wait_event(ready)
+        if self.fence is not None:
+            self.fence.signal(0, seq, self.compute)
+            self.fence.wait(0, seq, self.comm)
+        else:
+            ready.record(self.compute)
+            self.comm.wait_event(ready)
         if prof is not None:
             p1 = time.perf_counter()
         gc = t1 - t0
@@ -169,6 +218,9 @@ class RolloutGather:
                 out.copy_(src)
             if ev:
                 ev[1].record(self.comm)
+            if self.fence is not None:  # the records of this chunk may be rewritten from here on
+                self.fence.signal(1, seq, self.comm)
+                self.chunk_seq[c] = seq
             if prof is not None:
                 p2 = time.perf_counter()
             tail = self.tail if self.iterations == 0 else self._last_row
@@ -178,8 +230,10 @@ class RolloutGather:
             if ev:
                 ev[2].record(self.comm)
                 self.times.append((out.numel(), ev))
-            done.record(self.comm)
-        self.done_ev[c] = done
+            if self.fence is None:
+                done.record(self.comm)
+        if self.fence is None:
+            self.done_ev[c] = done
         if prof is not None:
             p3 = time.perf_counter()
             for k, v in (("actions+events", p1 - p0), ("gather", p2 - p1), ("decode+done", p3 - p2)):

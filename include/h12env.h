@@ -252,6 +252,12 @@ typedef struct h12env_config {
   int32_t self_collision;
   float self_k, self_c;        /* normal stiffness [N/m], damping [N s/m] */
   float self_ct, self_mu;      /* tangential damping [N s/m], Coulomb cap (0.6 x 0.6, material multiply) */
+  /* ABI 8: hard joint limits (PhysX holds the URDF ranges, A/robots/h12.py:18-35).  The stiff implicit limit spring
+   * (limit_k, activated on the predicted end-of-step position) stops a joint at its range inside the solve, with
+   * the reaction on the whole articulation; a joint that other forces (a foot slammed into the ground) still carry
+   * further than limit_projection past its range within a step is projected back to that tolerance and its outward
+   * velocity zeroed (PhysX's position-level limit correction; 0 = off, MuJoCo mode: its limits are soft) */
+  float limit_projection;      /* [rad] */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */
@@ -380,6 +386,17 @@ int h12env_rollout_layout(int n, size_t offsets[5], size_t* step_bytes);
  * before step 0, the tail row's slot h + t + 1. */
 int h12env_rollout_decode(const void* records, int n_shards, int n, int T, int G, int history, int t0, int t1,
                           const float* tail, float* obs_out, void* stream);
+/* Stream fences (ABI 8): 64-bit counters in signal memory for ordering two streams without HIP events --
+ * h12env_fence_signal enqueues "counter[slot] = value" behind all earlier work of the stream
+ * (hipStreamWriteValue64), h12env_fence_wait makes every later command of the stream wait until
+ * counter[slot] >= value (hipStreamWaitValue64).  The rollout all-gather orders its side stream against the env
+ * stream with these (an event record + cross-stream wait cost ~100 us of host time per hand-off here; DESIGN.md
+ * section 6).  Counters start at 0; values must increase per slot. */
+typedef struct h12env_fence h12env_fence;
+int h12env_fence_create(int device, int n_slots, h12env_fence** out);
+void h12env_fence_destroy(h12env_fence* f);
+int h12env_fence_signal(h12env_fence* f, int slot, uint64_t value, void* stream);
+int h12env_fence_wait(h12env_fence* f, int slot, uint64_t value, void* stream);
 /* Device pointer of a state field (see H12_F_* / H12_I_*), NULL on error. */
 void* h12env_field_ptr(h12env* h, int is_int, int field);
 int h12env_num_envs(const h12env* h);

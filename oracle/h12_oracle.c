@@ -279,13 +279,15 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   double gx, gy, hg = orc_ground(c, xw[0], xw[1], &gx, &gy);
   double in = 1.0 / sqrt(1.0 + gx * gx + gy * gy), nrm[3] = {-gx * in, -gy * in, in};
   double depth = rad - (xw[2] - hg) * in;
-  if (depth <= 0) return 0;
   double vl[3];
   cross3(k->v[b], pl, vl);
   for (int a = 0; a < 3; ++a) vl[a] += k->v[b][3 + a];
   double vw[3];
   m3v(k->R[b], vl, vw);
   double vn = nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2];
+  /* active when the point is predicted below the ground at the end of the substep (implicit: depth - hi vn), so a
+   * point arriving at speed is caught within the substep instead of one substep deep */
+  if (depth - hi * vn <= 0) return 0;
   /* implicit contact (hi > 0): the spring-damper force at the END of the substep, k (d - hi vn') - c vn'
    * with vn' = vn + hi an, is the explicit force with damping c + hi k plus the term -hi (c + hi k) an,
    * linear in the contact point's acceleration: an added point inertia (alpha along the normal, beta
@@ -681,17 +683,21 @@ int orc_mass_matrix(const h12env_model* m, const orc_phys* s, double M[18 * 18])
   return 0;
 }
 
-/* joint-limit penalty (one-sided spring-damper outside the MJCF range).  With the implicit penalty (hi > 0)
- * the torque at the end of the substep is linearised like the contacts: damping lc + hi lk, and dl[j]
- * receives the added joint inertia hi (lc + hi lk) of an active limit. */
+/* joint limits (PhysX holds the URDF ranges as hard limits, A/robots/h12.py:18-35, h12_12dof.urdf:53-198): a stiff
+ * one-sided spring-damper outside the MJCF range.  With the implicit penalty (hi > 0) it acts on the joint's
+ * position at the END of the substep, q + hi qd': active when the predicted end position q + hi qd is beyond the
+ * range (a joint arriving at speed is stopped at the limit within the step instead of one step past it), torque
+ * -lk (q + hi qd' - limit) - lc qd' linearised in the acceleration: explicit part -lk (q - limit) - (lc + hi lk) qd
+ * (repulsive only) and the added joint inertia dl[j] = hi (lc + hi lk) -- implicit Euler on the limit spring,
+ * stable at any stiffness.  Explicit integration (hi = 0): active past the range. */
 static void joint_limit_torque(const h12env_model* m, const h12env_config* c, const orc_phys* s, double hi,
                                double hdyn, double tau[NJ], double dl[NJ]) {
   double cl = c->limit_c + hi * c->limit_k;
   for (int j = 0; j < NJ; ++j) {
-    double q = s->q[j], qd = s->qd[j], t = 0;
+    double q = s->q[j], qd = s->qd[j], t = 0, qe = q + hi * qd;
     dl[j] = 0;
-    if (q > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - cl * qd; if (t > 0) t = 0; else dl[j] = hi * cl; }
-    else if (q < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - cl * qd; if (t < 0) t = 0; else dl[j] = hi * cl; }
+    if (qe > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - cl * qd; if (t > 0) t = 0; else dl[j] = hi * cl; }
+    else if (qe < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - cl * qd; if (t < 0) t = 0; else dl[j] = hi * cl; }
     /* PhysX max joint velocity: stiff damper on the excess, implicit over the substep (always: the solve
      * must carry the reaction; h = 0 would make it explicit and unstable) */
     double vm = c->max_joint_vel[j], cv = c->max_joint_vel_damping, ex = fabs(qd) - vm, rp = H12_VLIM_RAMP;
@@ -875,6 +881,19 @@ static void integrate(orc_phys* s, const double nd[18], double dt, int fix_base)
   for (int j = 0; j < NJ; ++j) { s->qd[j] += dt * nd[6 + j]; s->q[j] += dt * s->qd[j]; }
 }
 
+/* hard-limit residual: a joint that the other forces carried further than limit_projection past its range within
+ * the step (the limit spring acts only where the step started or was predicted beyond the range) is projected back
+ * to that tolerance and its outward velocity zeroed -- the position-level limit correction of a hard-limit solver.
+ * Off (0) in MuJoCo mode, whose limits are soft. */
+static void limit_projection(const h12env_model* m, const h12env_config* c, orc_phys* s) {
+  if (!(c->limit_projection > 0)) return;
+  for (int j = 0; j < NJ; ++j) {
+    double hi = m->q_upper[j] + c->limit_projection, lo = m->q_lower[j] - c->limit_projection;
+    if (s->q[j] > hi) { s->q[j] = hi; if (s->qd[j] > 0) s->qd[j] = 0; }
+    else if (s->q[j] < lo) { s->q[j] = lo; if (s->qd[j] < 0) s->qd[j] = 0; }
+  }
+}
+
 int orc_physics_step(const h12env_model* m, const h12env_config* c, orc_phys* s, const double tau_pd[NJ],
                      int with_contact, int algo, orc_contact_report* rep) {
   int n = c->inner_steps < 1 ? 1 : c->inner_steps;
@@ -895,6 +914,7 @@ int orc_physics_step(const h12env_model* m, const h12env_config* c, orc_phys* s,
     const double* pr = (const double*)&r;
     for (size_t i = 0; i < sizeof acc / sizeof(double); ++i) pa[i] += pr[i] / n;
     integrate(s, nd, h, c->fix_base);
+    limit_projection(m, c, s);
     memcpy(s->anchor, nanc, sizeof nanc);
     s->cmask = nmask;
   }

@@ -68,6 +68,7 @@ def _free_cfg(dt):
     c = H12FlatEnvCfg().to_c()
     c.limit_k = 0.0
     c.limit_c = 0.0
+    c.limit_projection = 0.0  # no joint limits at all: free-articulation invariants
     c.physics_dt = dt
     c.inner_steps = 1
     return c

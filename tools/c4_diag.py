@@ -43,11 +43,13 @@ def main():
         rec = rg = None
         if mode != "plain":
             rec = RolloutRecorder(n, 24, dev, 10)
-            rg = RolloutGather(rec, 1, a.gather_every, env.get_observations()["policy"].clone())
+            rg = RolloutGather(rec, 1, a.gather_every, env.get_observations()["policy"].clone(),
+                               sync="event" if mode.endswith("-ev") else "fence")
+            mode_base = mode.split("-")[0]
             env.bind_rollout(rec)
-            if mode == "record":
+            if mode_base == "record":
                 rg = None
-            elif mode == "copy":
+            elif mode_base == "copy":
                 rg.decode_off = True
             if rg is not None:
                 rg.prof = {}
@@ -72,7 +74,7 @@ def main():
             print("   host us per chunk:", {k: round(1e6 * v / c, 1) for k, v in rg.prof.items()}, flush=True)
         print(f"{mode:8s} wall {1e3 * tw / a.steps:.4f} ms/step   host loop {1e3 * th / a.steps:.4f} ms/step", flush=True)
 
-    for mode in ("plain", "record", "copy", "decode", "plain"):
+    for mode in ("plain", "record", "copy-ev", "copy", "decode-ev", "decode", "plain"):
         run(mode)
     # the decode kernel alone: one chunk and one whole iteration of rows, back to back
     rec = RolloutRecorder(n, 24, dev, 10)
