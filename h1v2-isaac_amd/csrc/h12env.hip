@@ -111,7 +111,10 @@ int set_err(int code, const char* fmt, ...) {
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
     hipError_t _e = (expr);                                                                  \
-    if (_e != hipSuccess) return set_err(H12_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    if (_e != hipSuccess) {                                                                  \
+      (void)hipGetLastError(); /* no sticky error left for the caller's next HIP call */     \
+      return set_err(H12_E_HIP, "%s: %s", #expr, hipGetErrorString(_e));                     \
+    }                                                                                        \
   } while (0)
 
 // ------------------------------------------------------------------ runtime parameters (kernarg)
@@ -134,6 +137,7 @@ struct KParams {
   float sk, sc, sct, smu; // its normal stiffness / damping, tangential damping, Coulomb cap
   float dl;               // implicit joint-limit inertia h (lc + h lk) (lc already includes h lk)
   float lproj;            // hard-limit projection tolerance (h12env_config.limit_projection; 3e38: off)
+  float dcap;             // depth cap of the contact spring, h * max_depenetration_velocity (3e38: off)
   float cmd_T, cmd_x0, cmd_x1, cmd_y0, cmd_y1, cmd_w0, cmd_w1, cmd_h0, cmd_h1;
   float rel_stand, rel_head, head_k;
   float rx0, rx1, ry0, ry1, ryaw0, ryaw1, root_z;
@@ -339,7 +343,7 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   // active when the point is predicted below the ground at the end of the step (implicit: depth - h vn; oracle
   // contact_point), so a point arriving at speed is caught within the step instead of one step deep
   if (!(depth - (P.impl ? P.h * vn : 0.f) > 0.f)) return false;
-  float fn = P.ck * depth - P.cc * vn;
+  float fn = P.ck * fminf(depth, P.dcap) - P.cc * vn;  // depenetration capped at h v_max (PhysX)
   if (!(fn > 0.f)) return false;
   float ft0, ft1;
   bool stick;
@@ -634,7 +638,7 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
     cross(ww, r, vw);
     vw[0] += v0[0]; vw[1] += v0[1]; vw[2] += v0[2];
     if (!(depth - (P.impl ? P.h * vw[2] : 0.f) > 0.f)) continue;  // predicted end-of-step depth (contact_sphere)
-    const float fn = P.ck * depth - P.cc * vw[2];
+    const float fn = P.ck * fminf(depth, P.dcap) - P.cc * vw[2];
     if (!(fn > 0.f)) continue;
     const float x0 = r[0] + pf[0], x1 = r[1] + pf[1];
     const bool was = (lg.cmask >> q) & 1;
@@ -1081,10 +1085,12 @@ H12_DEV void joint_terms(const KParams& P, const Leg& lg, float h, float* tq, fl
 
 // pass 1 from the state: lane-frame base pose / velocity, then the 6 links' joint sin / cos, spatial velocities
 // and world poses; Rk / pk: the knee's pose, R / p on exit: the foot's.
+// rel: positions relative to the base origin (the self-contact geometry: only differences of body points enter it,
+// and pelvis-relative fp32 points carry the ulp of ~1 m instead of the env's world position)
 template <int K>
 H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, float (&R0)[3][3], float* vb,
                        float* pb0, float (&cs)[NL][2], float (&v)[NL][6], float (&Rk)[3][3], float* pk,
-                       float (&R)[3][3], float* p) {
+                       float (&R)[3][3], float* p, bool rel = false) {
   const float sg = leg ? -1.f : 1.f;
   quat_R(b.quat, R0);
   mtv(R0, b.vlin, vb);
@@ -1097,6 +1103,7 @@ H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, 
   // base position: env-local on terrain (contact geometry relative to the env origin, ground_local)
   pb0[0] = b.pos[0]; pb0[1] = b.pos[1]; pb0[2] = b.pos[2];
   if constexpr (Feat<K>::terrain) { pb0[0] -= org[0]; pb0[1] -= org[1]; pb0[2] -= org[2]; }
+  if (rel) { pb0[0] = 0.f; pb0[1] = 0.f; pb0[2] = 0.f; }
   p[0] = pb0[0]; p[1] = sg * pb0[1]; p[2] = pb0[2];
   link_pass1<0>(lg, cs, vl0, v, R, p);
   link_pass1<1>(lg, cs, v[0], v, R, p);
@@ -1252,7 +1259,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
       float org[3];
       get_state(l, b, lg, org);
       float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
-      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
+      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
       act = self_stage(P, leg, Rk, pk, v[3], R, p, v[5]);
     }
     __syncthreads();  // R1
@@ -1367,9 +1374,11 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   } else {
     leg_bias(v, pbias);
     base_body<K>(P, lg, v0, Rg, pbase);
-    if (P.self_coll) {
+    if (P.self_coll) {  // pelvis-relative geometry, as the self wave's (subtracted here: one pass 1 in this wave)
       Forces fs = {};
-      self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wk, wf, fs);
+      const float pbl[3] = {pb0[0], sg * pb0[1], pb0[2]};
+      const float pkr[3] = {pk[0] - pbl[0], pk[1] - pbl[1], pk[2] - pbl[2]}, pr[3] = {p[0] - pbl[0], p[1] - pbl[1], p[2] - pbl[2]};
+      self_contacts(P, leg, Rk, pkr, v[3], R, pr, v[5], wk, wf, fs);
     }
   }
   PHX(13);
@@ -2694,7 +2703,7 @@ __global__ void __launch_bounds__(BLOCK) selfc_kernel(KParams P, Workspace W, fl
     for (int j = 0; j < 3; ++j) R[i][j] = mm[i] * mm[j] * R0[i][j];
   float v0[6] = {s.b.wang[0], s.b.wang[1], s.b.wang[2], vb[0], vb[1], vb[2]};
   for (int i = 0; i < 6; ++i) v0[i] *= s6(i, sg);
-  float p[3] = {s.b.pos[0], sg * s.b.pos[1], s.b.pos[2]};
+  float p[3] = {0.f, 0.f, 0.f};  // pelvis-relative positions, as step_kernel's self-contact wave
   float cs[NL][2], v[NL][6];
   link_pass1<0>(s.lg, cs, v0, v, R, p);
   link_pass1<1>(s.lg, cs, v[0], v, R, p);
@@ -3196,6 +3205,7 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
   P.sk = c->self_k; P.sc = c->self_c; P.sct = c->self_ct; P.smu = c->self_mu;
   if (!(c->limit_projection >= 0.f)) return set_err(H12_E_ARG, "limit_projection must be >= 0");
   P.lproj = c->limit_projection > 0.f ? c->limit_projection : 3.0e38f;
+  if (!(c->max_depenetration_velocity >= 0.f)) return set_err(H12_E_ARG, "max_depenetration_velocity must be >= 0");
   P.dl = 0.f;
   if (P.impl) {  // the springs act at the end of the substep: extra damping h k (oracle contact_point)
     P.cc = c->contact_c + P.h * c->contact_k;
@@ -3203,6 +3213,7 @@ int build_params(const h12env_model* m, const h12env_config* c, KParams& P) {
     P.lc = c->limit_c + P.h * c->limit_k;
     P.dl = P.h * P.lc;
   }
+  P.dcap = (P.impl && c->max_depenetration_velocity > 0.f) ? P.h * c->max_depenetration_velocity : 3.0e38f;
   P.cthr = c->contact_threshold;
   P.cmd_T = c->cmd_resample_time;
   P.cmd_x0 = c->cmd_lin_x[0]; P.cmd_x1 = c->cmd_lin_x[1];
@@ -3418,8 +3429,9 @@ int h12env_config_default(h12env_config* c) {
   for (int j = 0; j < H12_NJ; ++j) c->max_joint_vel[j] = vmax[j % 6];
   c->max_joint_vel_damping = 1.0e3f;
   c->self_collision = 1; c->self_k = 3e4f; c->self_c = 50.f; c->self_ct = 50.f; c->self_mu = 0.36f;
-  c->contact_k = 5e5f; c->contact_c = 300.f; c->friction_k = 3e4f; c->friction_c = 100.f;
+  c->contact_k = 7e5f; c->contact_c = 300.f; c->friction_k = 3e4f; c->friction_c = 100.f;
   c->limit_projection = 0.01f;
+  c->max_depenetration_velocity = 1.f;
   c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1.0e6f; c->limit_c = 2.f; c->contact_threshold = 1.f;
   c->cmd_resample_time = 10.f;
   c->cmd_lin_x[0] = 0.f; c->cmd_lin_x[1] = 1.f; c->cmd_lin_y[0] = -0.5f; c->cmd_lin_y[1] = 0.5f;
@@ -3755,10 +3767,16 @@ int h12env_rollout_decode(const void* records, int n_shards, int n, int T, int G
 }
 
 struct h12env_fence {
-  uint64_t* ctr;
-  int n;
+  std::vector<uint64_t*> ctr;  // one HSA signal (8 bytes, hipMallocSignalMemory) per slot
   int device;
 };
+
+void h12env_fence_destroy(h12env_fence* f) {
+  if (!f) return;
+  for (uint64_t* c : f->ctr)
+    if (c) (void)hipFree(c);
+  delete f;
+}
 
 int h12env_fence_create(int device, int n_slots, h12env_fence** out) {
   if (!out || n_slots < 1) return set_err(H12_E_ARG, "n_slots >= 1 and out required");
@@ -3769,34 +3787,39 @@ int h12env_fence_create(int device, int n_slots, h12env_fence** out) {
   if (!ok) return set_err(H12_E_STATE, "device %d does not support hipStreamWaitValue64", device);
   h12env_fence* f = new (std::nothrow) h12env_fence();
   if (!f) return set_err(H12_E_ALLOC, "host allocation failed");
-  hipError_t e = hipExtMallocWithFlags((void**)&f->ctr, sizeof(uint64_t) * (size_t)n_slots, hipMallocSignalMemory);
-  if (e == hipSuccess) e = hipMemset(f->ctr, 0, sizeof(uint64_t) * (size_t)n_slots);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e != hipSuccess) {
-    delete f;
-    return set_err(H12_E_ALLOC, "signal memory: %s", hipGetErrorString(e));
-  }
-  f->n = n_slots;
   f->device = device;
+  for (int i = 0; i < n_slots; ++i) {
+    uint64_t* c = nullptr;
+    hipError_t e = hipExtMallocWithFlags((void**)&c, sizeof(uint64_t), hipMallocSignalMemory);
+    if (e == hipSuccess) {
+      f->ctr.push_back(c);
+      e = hipStreamWriteValue64(nullptr, c, 0, 0);  // counters start at 0
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // leave no sticky error behind for the caller's next HIP call
+      h12env_fence_destroy(f);
+      return set_err(H12_E_ALLOC, "signal memory: %s", hipGetErrorString(e));
+    }
+  }
+  hipError_t e = hipStreamSynchronize(nullptr);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    h12env_fence_destroy(f);
+    return set_err(H12_E_HIP, "fence init: %s", hipGetErrorString(e));
+  }
   *out = f;
   return 0;
 }
 
-void h12env_fence_destroy(h12env_fence* f) {
-  if (!f) return;
-  if (f->ctr) (void)hipFree(f->ctr);
-  delete f;
-}
-
 int h12env_fence_signal(h12env_fence* f, int slot, uint64_t value, void* stream) {
-  if (!f || slot < 0 || slot >= f->n) return set_err(H12_E_ARG, "bad fence or slot");
-  HIP_TRY(hipStreamWriteValue64((hipStream_t)stream, f->ctr + slot, value, 0));
+  if (!f || slot < 0 || slot >= (int)f->ctr.size()) return set_err(H12_E_ARG, "bad fence or slot");
+  HIP_TRY(hipStreamWriteValue64((hipStream_t)stream, f->ctr[slot], value, 0));
   return 0;
 }
 
 int h12env_fence_wait(h12env_fence* f, int slot, uint64_t value, void* stream) {
-  if (!f || slot < 0 || slot >= f->n) return set_err(H12_E_ARG, "bad fence or slot");
-  HIP_TRY(hipStreamWaitValue64((hipStream_t)stream, f->ctr + slot, value, hipStreamWaitValueGte, ~0ull));
+  if (!f || slot < 0 || slot >= (int)f->ctr.size()) return set_err(H12_E_ARG, "bad fence or slot");
+  HIP_TRY(hipStreamWaitValue64((hipStream_t)stream, f->ctr[slot], value, hipStreamWaitValueGte, ~0ull));
   return 0;
 }
 

@@ -198,6 +198,7 @@ class H12Config(C.Structure):
         ("self_ct", f32),
         ("self_mu", f32),
         ("limit_projection", f32),
+        ("max_depenetration_velocity", f32),
     ]
 
 

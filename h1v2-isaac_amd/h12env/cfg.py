@@ -48,12 +48,15 @@ class SimCfg:
     self_mu: float = 0.36
     # ground contact: sole spheres / knee / torso; stiff (PhysX's contacts are rigid: median sole penetration
     # 1.8 mm under random actions), active on the predicted end-of-step depth, implicit
-    contact_k: float = 5.0e5
+    contact_k: float = 7.0e5
     contact_c: float = 300.0
     # the explicit integrator (implicit_penalty = False: MuJoCo mode, the round-1 scheme) keeps the soft contact it is
     # stable with
     contact_k_explicit: float = 3.0e4
     contact_c_explicit: float = 100.0
+    # RigidBodyPropertiesCfg.max_depenetration_velocity (A/robots/h12.py:29): the contact spring pushes a penetration
+    # out at most this fast (implicit scheme)
+    max_depenetration_velocity: float = 1.0
     friction_k: float = 3.0e4
     friction_c: float = 100.0
     # joint limits: PhysX holds the URDF ranges as hard limits; here a stiff spring on the predicted end-of-step
@@ -65,6 +68,9 @@ class SimCfg:
     # a joint still carried further than this past its range within a step is projected back (hard-limit residual;
     # implicit scheme only)
     limit_projection: float = 0.01
+    # MuJoCo mode: the MJCF joints' frictionloss (0.1 N m, a dry-friction constraint in MuJoCo) as a smooth
+    # -f tanh(100 qd) torque; off by default
+    frictionloss: bool = False
     static_friction: float = 0.8   # randomize_rigid_body_material startup (velocity_env_cfg.py:153-163)
     dynamic_friction: float = 0.6
 
@@ -548,7 +554,7 @@ class H12FlatEnvCfg:
         if c.max_delay > 2 * self.decimation:
             raise ValueError("max_delay must be <= 2 * decimation (delay ring holds two env steps)")
         c.fix_base = int(self.fix_base)
-        c.use_frictionloss = 0
+        c.use_frictionloss = int(self.sim.frictionloss)
         s = self.sim
         c.contact_k, c.contact_c = ((s.contact_k, s.contact_c) if s.implicit_penalty
                                     else (s.contact_k_explicit, s.contact_c_explicit))
@@ -556,6 +562,7 @@ class H12FlatEnvCfg:
         c.mu_static, c.mu_dynamic = s.static_friction, s.dynamic_friction
         c.limit_k, c.limit_c = (s.limit_k if s.implicit_penalty else s.limit_k_explicit), s.limit_c
         c.limit_projection = s.limit_projection if s.implicit_penalty else 0.0
+        c.max_depenetration_velocity = s.max_depenetration_velocity if s.implicit_penalty else 0.0
         c.contact_threshold = self.terminations.base_contact_threshold
         bv = self.commands.base_velocity
         c.cmd_resample_time, c.cmd_resample_time_max = bv.resampling_time_range

@@ -258,6 +258,11 @@ typedef struct h12env_config {
    * further than limit_projection past its range within a step is projected back to that tolerance and its outward
    * velocity zeroed (PhysX's position-level limit correction; 0 = off, MuJoCo mode: its limits are soft) */
   float limit_projection;      /* [rad] */
+  /* ABI 8: PhysX's max_depenetration_velocity (RigidBodyPropertiesCfg, A/robots/h12.py:29: 1.0 m/s): the
+   * implicit ground-contact spring pushes a penetration out at most this fast -- its elastic term uses
+   * min(depth, h * v) -- so a deep initial penetration is resolved over several steps instead of launching the
+   * body (0 = off; explicit integration: off) */
+  float max_depenetration_velocity; /* [m/s] */
 } h12env_config;
 
 /* Persistent per-env state fields (field-major SoA in the workspace). */

@@ -293,7 +293,9 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
    * linear in the contact point's acceleration: an added point inertia (alpha along the normal, beta
    * tangentially while the stiction spring sticks / the viscous drag is below its cap) */
   double cn = c->contact_c + hi * c->contact_k;
-  double fn = c->contact_k * depth - cn * vn;
+  /* PhysX max_depenetration_velocity (A/robots/h12.py:29): the spring pushes a penetration out at most this fast */
+  double dcap = (hi > 0 && c->max_depenetration_velocity > 0) ? hi * c->max_depenetration_velocity : 1e300;
+  double fn = c->contact_k * (depth < dcap ? depth : dcap) - cn * vn;
   if (fn <= 0) return 0;
   double ft0, ft1, beta = 0;
   if (anc_out) {
@@ -423,31 +425,41 @@ static double sj_draw(void) { /* splitmix64 -> uniform [-1, 1) */
   return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
 }
 
+/* The self-contact geometry runs in PELVIS-RELATIVE world axes (positions minus the base origin, |x| < 1.2 m): only
+ * differences of body points enter it, and the kernel does the same so that its fp32 points carry the ulp of ~1 m,
+ * not of the env's world position.  po(k, b): body b's origin relative to the base origin. */
+static void po(const kin_t* k, int b, double out[3]) {
+  for (int a = 0; a < 3; ++a) out[a] = k->p[b][a] - k->p[0][a];
+}
+
 static void capsule_world(const kin_t* k, int b, const float* p0, const float* p1, double r, capsule_w* out) {
-  double a0[3] = {p0[0], p0[1], p0[2]}, a1[3] = {p1[0], p1[1], p1[2]};
+  double a0[3] = {p0[0], p0[1], p0[2]}, a1[3] = {p1[0], p1[1], p1[2]}, ob[3];
   out->b = b;
   out->r = r;
   m3v(k->R[b], a0, out->p0);
   m3v(k->R[b], a1, out->p1);
-  for (int a = 0; a < 3; ++a) { out->p0[a] += k->p[b][a]; out->p1[a] += k->p[b][a]; }
+  po(k, b, ob);
+  for (int a = 0; a < 3; ++a) { out->p0[a] += ob[a]; out->p1[a] += ob[a]; }
   if (g_sj_eps > 0.0)
     for (int a = 0; a < 3; ++a) { out->p0[a] += g_sj_eps * sj_draw(); out->p1[a] += g_sj_eps * sj_draw(); }
 }
 
-/* world velocity of the body-b material point at world x */
+/* world velocity of the body-b material point at x (pelvis-relative, see po) */
 static void point_vel(const kin_t* k, int b, const double x[3], double v[3]) {
-  double w[3], vo[3], rx[3], wr[3];
+  double w[3], vo[3], rx[3], wr[3], ob[3];
   m3v(k->R[b], k->v[b], w);
   m3v(k->R[b], k->v[b] + 3, vo);
-  for (int a = 0; a < 3; ++a) rx[a] = x[a] - k->p[b][a];
+  po(k, b, ob);
+  for (int a = 0; a < 3; ++a) rx[a] = x[a] - ob[a];
   cross3(w, rx, wr);
   for (int a = 0; a < 3; ++a) v[a] = vo[a] + wr[a];
 }
 
-/* world force F at world point x on body b -> body-coordinate spatial force */
+/* world force F at point x (pelvis-relative, see po) on body b -> body-coordinate spatial force */
 static void apply_world_force(const kin_t* k, int b, const double x[3], const double F[3], double fext[NB][6]) {
-  double rx[3], xb[3], fb[3], nb[3];
-  for (int a = 0; a < 3; ++a) rx[a] = x[a] - k->p[b][a];
+  double rx[3], xb[3], fb[3], nb[3], ob[3];
+  po(k, b, ob);
+  for (int a = 0; a < 3; ++a) rx[a] = x[a] - ob[a];
   m3tv(k->R[b], rx, xb);
   m3tv(k->R[b], F, fb);
   cross3(xb, fb, nb);

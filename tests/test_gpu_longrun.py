@@ -54,7 +54,8 @@ def test_teacher_forced_flat_4096x1100(gpu):
         cov["resamples"] += int(((Fo[ct] > F0_ct + 1e-3) & ~(to | tro)).sum())
         done = to | tro
         cov["air_time_reward"] += int((((Fo[o_ep + 6] - fp.last_F0[o_ep + 6]) > 0) & ~done).sum())
-        if done.any() and ok[done].all():
+        done_any = done | tg | trg  # envs resetting in either run (a threshold-sensitive flip resets one only)
+        if done.any() and ok[done_any].all():
             # log accumulator of this step's resetting envs (episode sums, count, time-out / base-contact counts)
             acc = env._log_ring[env.common_step_counter % len(env._log_ring)].cpu().numpy()
             lo = info["log"]

@@ -118,7 +118,7 @@ def test_self_collision_mdp_forced_knee_contacts_terminate(gpu):
         terms += int(to.sum())
         assert np.isfinite(rew).all()
     # every env is pressed into self-contact here: the fp32 self-contact allowance is per such env-step
-    fp.check(max_bad_frac=0.02, self_rate=1e-3)
+    fp.check(max_bad_frac=0.02, self_rate=0.0)
     assert terms > 50, terms
     env.close()
 
@@ -145,10 +145,28 @@ def test_self_contact_wrenches_match_oracle(gpu):
         scale = max(1.0, np.abs(f).max())
         worst.append(max(np.abs(g[i, leg, b] - f[body]).max() / scale for leg, b, body in bodies))
     worst = np.array(worst)
-    print("self-contact wrench error quantiles (0.5, 0.9, 0.99, max):", np.quantile(worst, [0.5, 0.9, 0.99, 1.0]),
-          "envs in contact", hit)
+    # a pair at its contact onset (depth within the fp32 rounding of its pelvis-relative points, ~1e-7 m) switches
+    # its force c |v_n| on or off: such an env is threshold-sensitive when the oracle with its capsule end points
+    # jittered at that scale reproduces the kernel's wrenches (the harness's rule, tests/helpers/forced.py);
+    # every other env is bounded by the fp32 error of the contact law itself
+    BOUND = 2e-4
+    flipped = 0
+    for i in np.nonzero(worst > BOUND)[0]:
+        s = Fm[0:37, i].astype(np.float64)
+        for k, eps in enumerate((1e-7,) * 32 + (3e-7,) * 32):
+            O.set_self_jitter(eps, 1000 + k)
+            try:
+                f, _ = O.self_contacts(env._model, env._ccfg, s)
+            finally:
+                O.set_self_jitter(0.0)
+            scale = max(1.0, np.abs(f).max())
+            if max(np.abs(g[i, leg, b] - f[body]).max() / scale for leg, b, body in bodies) <= 0.5 * worst[i]:
+                flipped += 1
+                worst[i] = 0.0  # explained
+                break
+    print("self-contact wrench error quantiles (0.5, 0.9, 0.99, max) of the non-flipped envs:",
+          np.quantile(worst, [0.5, 0.9, 0.99, 1.0]), "envs in contact", hit, "onset flips", flipped)
     assert hit > n // 4
-    # fp32 geometry of rods 5 mm thick: depth errors ~1e-6 m -> 0.03 N on k = 3e4 (contact onsets excepted)
-    assert np.quantile(worst, 0.99) < 1e-3, np.quantile(worst, [0.5, 0.9, 0.99, 1.0])
-    assert (worst < 1e-2).mean() > 0.997, np.sort(worst)[-10:]
+    assert worst.max() <= BOUND, np.sort(worst)[-10:]
+    assert flipped <= 0.01 * hit, flipped
     env.close()
