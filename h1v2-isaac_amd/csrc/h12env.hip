@@ -343,7 +343,9 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   // active when the point is predicted below the ground at the end of the step (implicit: depth - h vn; oracle
   // contact_point), so a point arriving at speed is caught within the step instead of one step deep
   if (!(depth - (P.impl ? P.h * vn : 0.f) > 0.f)) return false;
-  float fn = P.ck * fminf(depth, P.dcap) - P.cc * vn;  // depenetration capped at h v_max (PhysX)
+  // a sole contact that opens with a penetration is pushed out at most at PhysX's max_depenetration_velocity
+  // (elastic term capped at h v_max); a persistent one carries any load (oracle contact_point)
+  float fn = P.ck * ((ANCHOR && !was_in) ? fminf(depth, P.dcap) : depth) - P.cc * vn;
   if (!(fn > 0.f)) return false;
   float ft0, ft1;
   bool stick;
@@ -638,10 +640,11 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
     cross(ww, r, vw);
     vw[0] += v0[0]; vw[1] += v0[1]; vw[2] += v0[2];
     if (!(depth - (P.impl ? P.h * vw[2] : 0.f) > 0.f)) continue;  // predicted end-of-step depth (contact_sphere)
-    const float fn = P.ck * fminf(depth, P.dcap) - P.cc * vw[2];
+    const bool was = (lg.cmask >> q) & 1;
+    // an opening contact is pushed out at most at max_depenetration_velocity (contact_sphere)
+    const float fn = P.ck * (was ? depth : fminf(depth, P.dcap)) - P.cc * vw[2];
     if (!(fn > 0.f)) continue;
     const float x0 = r[0] + pf[0], x1 = r[1] + pf[1];
-    const bool was = (lg.cmask >> q) & 1;
     float ax = was ? lg.anc[q][0] : x0, ay = was ? lg.anc[q][1] : x1;
     float ft0 = -P.fk * (x0 - ax) - P.fc * vw[0];
     float ft1 = -P.fk * (x1 - ay) - P.fc * vw[1];
@@ -3429,7 +3432,7 @@ int h12env_config_default(h12env_config* c) {
   for (int j = 0; j < H12_NJ; ++j) c->max_joint_vel[j] = vmax[j % 6];
   c->max_joint_vel_damping = 1.0e3f;
   c->self_collision = 1; c->self_k = 3e4f; c->self_c = 50.f; c->self_ct = 50.f; c->self_mu = 0.36f;
-  c->contact_k = 7e5f; c->contact_c = 300.f; c->friction_k = 3e4f; c->friction_c = 100.f;
+  c->contact_k = 1e5f; c->contact_c = 100.f; c->friction_k = 3e4f; c->friction_c = 100.f;
   c->limit_projection = 0.01f;
   c->max_depenetration_velocity = 1.f;
   c->mu_static = 0.8f; c->mu_dynamic = 0.6f; c->limit_k = 1.0e6f; c->limit_c = 2.f; c->contact_threshold = 1.f;

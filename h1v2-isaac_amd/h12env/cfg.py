@@ -48,8 +48,8 @@ class SimCfg:
     self_mu: float = 0.36
     # ground contact: sole spheres / knee / torso; stiff (PhysX's contacts are rigid: median sole penetration
     # 1.8 mm under random actions), active on the predicted end-of-step depth, implicit
-    contact_k: float = 7.0e5
-    contact_c: float = 300.0
+    contact_k: float = 1.0e5
+    contact_c: float = 100.0
     # the explicit integrator (implicit_penalty = False: MuJoCo mode, the round-1 scheme) keeps the soft contact it is
     # stable with
     contact_k_explicit: float = 3.0e4

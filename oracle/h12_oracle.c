@@ -293,8 +293,10 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
    * linear in the contact point's acceleration: an added point inertia (alpha along the normal, beta
    * tangentially while the stiction spring sticks / the viscous drag is below its cap) */
   double cn = c->contact_c + hi * c->contact_k;
-  /* PhysX max_depenetration_velocity (A/robots/h12.py:29): the spring pushes a penetration out at most this fast */
-  double dcap = (hi > 0 && c->max_depenetration_velocity > 0) ? hi * c->max_depenetration_velocity : 1e300;
+  /* PhysX max_depenetration_velocity (A/robots/h12.py:29): a sole contact that OPENS with a penetration is pushed
+   * out at most this fast (elastic term capped at hi v_max); a persistent contact carries any load */
+  double dcap = (hi > 0 && c->max_depenetration_velocity > 0 && anc_out && !was_in) ? hi * c->max_depenetration_velocity
+                                                                                     : 1e300;
   double fn = c->contact_k * (depth < dcap ? depth : dcap) - cn * vn;
   if (fn <= 0) return 0;
   double ft0, ft1, beta = 0;

@@ -270,10 +270,13 @@ class ForcedParity:
         f0 = F0[:, e:e + 1]
         d_og = _distance(f0, g_e, o_e, exact=False)
         try:
-            for eps in SELF_JITTER:
+            for k, eps in enumerate(SELF_JITTER):
                 O.set_dz_count(self._dz0)
                 O.set_self_jitter(eps, int(self.rng.integers(1 << 62)))
-                ref.F[:], ref.I[:], ref.obs[:] = f0, I0[:, e:e + 1], obs0[e:e + 1]
+                # every other draw also perturbs the state at the fp32 scale: a self-contact step can flip a ground
+                # contact or slip decision as well, which neither perturbation reproduces alone
+                fs = f0 if k % 2 == 0 else perturbed(self.rng, f0, min(eps, 1e-6))
+                ref.F[:], ref.I[:], ref.obs[:] = fs, I0[:, e:e + 1], obs0[e:e + 1]
                 po, pr, pt, ptr, _ = ref.step(a_np[e:e + 1], t)
                 p_e = (ref.F.copy(), ref.I.copy(), po, pr, pt, ptr)
                 if _distance(f0, g_e, p_e, o_e) <= 0.5 * d_og:

@@ -194,7 +194,9 @@ def test_contact_force_and_torque_parity(gpu, integrator):
     base = rerun(F0)
     torch.cuda.synchronize()
     g = np.concatenate([env.foot_contact_force.cpu().numpy(), env._applied_torque.cpu().numpy()], axis=1)
-    assert (base[:, :2] > 1.0).mean() > 0.3  # most envs have a foot on the ground
+    # many envs end the step with a loaded foot (the stiffer round-3 contacts push random initial penetrations out,
+    # at most at max_depenetration_velocity: ~30 % of these states keep a foot loaded, ~300 envs)
+    assert (base[:, :2] > 1.0).mean() > 0.2
     gerr = err(g, base)
     bad = unexplained_envs(F0, gerr, 1.0, rerun, err, base, g)
     assert bad.size == 0, f"{bad.size} envs off the oracle and not threshold-sensitive: {bad[:10]} {gerr[bad[:10]]}"
