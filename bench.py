@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--rollout-steps", type=int, default=24,
                    help="rollout length T (num_steps_per_env, C12/agents/rsl_rl_ppo_cfg.py:12)")
     p.add_argument("--gather-every", type=int, default=4, help="all-gather chunk length G in env steps (C4)")
+    p.add_argument("--rollout-decode", action="store_true",
+                   help="C4: also rebuild the global (T, N_global, 450) observation rows on every rank after each "
+                        "gathered chunk (off: the gathered records are handed over; a learner rebuilds its minibatch rows)")
     p.add_argument("--dump-rollout", type=str, default=None,
                    help="test hook: rank 0 saves the decoded rows and the gathered records of the timed window (.npz)")
     return p.parse_args()
@@ -303,7 +306,7 @@ def main():
             D.all_gather_into_tensor(tail, env.get_observations()["policy"].contiguous())
         else:
             tail.copy_(env.get_observations()["policy"])
-        rg = RolloutGather(rec, world, args.gather_every, tail, timing=True)
+        rg = RolloutGather(rec, world, args.gather_every, tail, timing=True, decode=args.rollout_decode)
         env.bind_rollout(rec)
 
         def put_actions(i0):
@@ -350,6 +353,10 @@ def main():
         import numpy as np
 
         te = min(K, args.rollout_steps)
+        if not args.rollout_decode:  # the check rebuilds the rows of the gathered records once, untimed
+            from h12env.rollout import decode as _decode
+
+            _decode(rg.gathered, world, n, te, rg.G, rec.history, 0, te, rg.tail, rg.obs[:te])
         np.savez(args.dump_rollout, obs=rg.obs[:te].cpu().numpy(), gathered=rg.gathered.cpu().numpy(),
                  tail=rg.tail.cpu().numpy(), off=np.array(rec.off), step_bytes=rec.step_bytes, T=te, G=rg.G,
                  n=n, world=world, burn_in=B, warmup=W, steps=K, pool=pool)
@@ -366,10 +373,12 @@ def main():
               "decode_ms_per_iter": st["decode_ms"] / iters, "ms_per_iter": 1e3 * dt / iters,
               "allgather_algbw_gbs": st["gathered_bytes"] / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] else None,
               "allgather_busbw_gbs": recv / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] and world > 1 else None,
-              "decoded_rows_bytes_per_iter": args.rollout_steps * world * n * env.obs_dim * 4,
-              "decode_gbs": (st["chunks"] and rg.G * world * n * env.obs_dim * 4 * st["chunks"] /
-                             (st["decode_ms"] * 1e-3) / 1e9) or None,
-              "overlap": "gathers + decodes on a side stream, concurrent with the next chunk's env steps",
+              "rows_rebuilt": bool(args.rollout_decode),
+              "decoded_rows_bytes_per_iter": args.rollout_steps * world * n * env.obs_dim * 4 if args.rollout_decode else 0,
+              "decode_gbs": (args.rollout_decode and st["chunks"] and st["decode_ms"] and
+                             rg.G * world * n * env.obs_dim * 4 * st["chunks"] / (st["decode_ms"] * 1e-3) / 1e9) or None,
+              "overlap": "gathers (+ row rebuilds) on a side stream ordered by signal-memory fences, concurrent with "
+                         "the next chunk's env steps",
               "backend": (args.dist_backend if world > 1 else "copy (N = 1)")}
         env.unbind_rollout()
     if args.profile_only:

@@ -10,8 +10,8 @@ config:
   - actuators: packages/biped_assets/biped_assets/robots/h12.py:58-112 (DelayedPD, Kp/Kd/E, 0-5 delay)
   - commands: velocity_env_cfg.py:90-104 + flat_env_cfg.py:46-48
   - observations: velocity_env_cfg.py:124-132, flat_env_cfg.py:25-27 (no lin vel, history 10, noise on)
-  - events: rough_env_cfg.py:80-92 (x,y +-0.5, yaw +-3.14, joints x1.0, no push, no mass)
-  - rewards: rough_env_cfg.py:18-62 (term table), 111-120 (weights) + flat_env_cfg.py:35-44
+  - events: rough_env_cfg.py:77-92 (x,y +-0.5, yaw +-3.14, joints x1.0, no push, no mass)
+  - rewards: rough_env_cfg.py:19-62 (term table), 111-120 (weights) + flat_env_cfg.py:35-44
   - terminations: velocity_env_cfg.py:264-268 + rough_env_cfg.py:95-109 (illegal-contact bodies)
 """
 from __future__ import annotations
@@ -46,8 +46,9 @@ class SimCfg:
     self_c: float = 50.0
     self_ct: float = 50.0
     self_mu: float = 0.36
-    # ground contact: sole spheres / knee / torso; stiff (PhysX's contacts are rigid: median sole penetration
-    # 1.8 mm under random actions), active on the predicted end-of-step depth, implicit
+    # ground contact: sole spheres / knee / torso, active on the predicted end-of-step depth, implicit.  PhysX's
+    # contacts are rigid; 1e5 N/m gives a median sole penetration of 3.7 mm under random actions, 7e5 would give
+    # 1.8 mm at 4x the fp32 threshold sensitivity
     contact_k: float = 1.0e5
     contact_c: float = 100.0
     # the explicit integrator (implicit_penalty = False: MuJoCo mode, the round-1 scheme) keeps the soft contact it is
@@ -698,7 +699,7 @@ class H12FlatEnvCfg:
 
 @dataclass
 class H12RoughEnvCfg(H12FlatEnvCfg):
-    """Isaac-Velocity-Rough-H12_12dof-v0 (H12_12dof_RoughEnvCfg, rough_env_cfg.py:128-188 on
+    """Isaac-Velocity-Rough-H12_12dof-v0 (H12_12dof_RoughEnvCfg, rough_env_cfg.py:65-125 on
     LocomotionVelocityRoughEnvCfg): generated heightfield + terrain curriculum, height scanner, base_lin_vel
     in the 235-float observation (no history), rough reward weights, lin_vel_y command 0."""
 
@@ -712,19 +713,19 @@ class H12RoughEnvCfg(H12FlatEnvCfg):
         po.height_scan = Unoise(-0.1, 0.1)
         self.curriculum.terrain_levels = True
         r = self.rewards
-        r.feet_air_time.weight = 0.25              # rough_env_cfg.py:97-105
-        r.dof_torques_l2.weight = -1.5e-7          # :177
-        r.dof_acc_l2.weight = -1.25e-7             # :179
-        r.action_rate_l2.weight = -0.005           # :178
-        r.flat_orientation_l2.weight = -1.0        # :176
-        self.commands.base_velocity.ranges.lin_vel_x = (0.0, 1.0)   # :186-188
+        r.feet_air_time.weight = 0.25              # rough_env_cfg.py:34-42
+        r.dof_torques_l2.weight = -1.5e-7          # :114
+        r.dof_acc_l2.weight = -1.25e-7             # :116
+        r.action_rate_l2.weight = -0.005           # :115
+        r.flat_orientation_l2.weight = -1.0        # :113
+        self.commands.base_velocity.ranges.lin_vel_x = (0.0, 1.0)   # :123-125
         self.commands.base_velocity.ranges.lin_vel_y = (0.0, 0.0)
         self.commands.base_velocity.ranges.ang_vel_z = (-1.0, 1.0)
 
 
 @dataclass
 class H12RoughEnvCfg_PLAY(H12RoughEnvCfg):
-    """rough_env_cfg.py:191-214: 50 envs, 40 s episodes, random initial levels, 5 x 5 terrain, no noise."""
+    """rough_env_cfg.py:128-154: 50 envs, 40 s episodes, random initial levels, 5 x 5 terrain, no noise."""
 
     def __post_init__(self):
         super().__post_init__()

@@ -122,7 +122,7 @@ class RolloutGather:
     device copy (same code path, no collective)."""
 
     def __init__(self, rec: RolloutRecorder, world: int, G: int, tail: torch.Tensor, timing: bool = False,
-                 sync: str = "fence"):
+                 sync: str = "fence", decode: bool = True):
         self.rec, self.world, self.G = rec, int(world), max(1, min(int(G), rec.T))
         dev = rec.record.device
         self.gathered = torch.empty(self.world * rec.record.numel(), dtype=torch.uint8, device=dev)
@@ -147,7 +147,9 @@ class RolloutGather:
         self.timing = timing
         self.times: list[tuple] = []             # (chunk bytes, gather event pair, decode event pair)
         self.iterations = 0
-        self.decode_off = False                  # diagnostics only (tools/c4_diag.py): gather without the rebuild
+        # decode=False: the gathered records are the product (a PPO learner rebuilds the rows of each minibatch it
+        # draws; the full (T, N_global, 45H) rebuild is then never needed)
+        self.decode_off = not decode
 
     def chunk_of(self, t: int) -> tuple[int, int, int]:
         c = t // self.G

@@ -8,10 +8,10 @@
  *
  *   h12env_create      ManagerBasedRLEnv.__init__ -> load_managers + scene cloning
  *                      (packages/biped_tasks/biped_tasks/utils/cat/cat_env.py:31-93; task cfg
- *                      .../velocity/config/h12_12dof/flat_env_cfg.py:13-48, rough_env_cfg.py:128-188;
+ *                      .../velocity/config/h12_12dof/flat_env_cfg.py:13-48, rough_env_cfg.py:65-125;
  *                      robot cfg packages/biped_assets/biped_assets/robots/h12.py:18-114)
  *   h12env_reset       ManagerBasedRLEnv._reset_idx + reset events + ObservationManager.compute
- *                      (cat_env.py:195-248; rough_env_cfg.py:80-92; observation_manager.py:271-355)
+ *                      (cat_env.py:195-248; rough_env_cfg.py:77-92; observation_manager.py:271-355)
  *   h12env_step        ManagerBasedRLEnv.step (cat_env.py:95-193): action processing, 4 x (delayed PD
  *                      actuator -> PhysX step -> sensor update), terminations, rewards, resets,
  *                      commands, observations with 10-frame history (circular_buffer.py:79-170)
@@ -55,7 +55,7 @@ extern "C" {
                               violation rate (10) and mean probability (10), then (ABI 7) the sums over reset
                               envs of the command metrics error_vel_xy, error_vel_yaw (H12_LOG_METRIC) */
 #define H12_LOG_METRIC 44  /* UniformVelocityCommand._update_metrics accumulators, logged by CommandTerm.reset */
-/* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:128-188): no history, base_lin_vel
+/* Rough task (Isaac-Velocity-Rough-H12_12dof-v0, rough_env_cfg.py:65-125): no history, base_lin_vel
  * first, height scan last (velocity_env_cfg.py:118-137) */
 #define H12_ROUGH_FRAME 48 /* lin_vel 3, ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
 #define H12_SCAN_NX 17     /* GridPatternCfg(resolution 0.1, size (1.6, 1.0)), velocity_env_cfg.py:60-66 */
@@ -88,18 +88,18 @@ extern "C" {
  * the Flat table in its RewardManager order; 12-19 complete the Rsl table (rsl_env_cfg.py:279-407).
  * The host maps each cfg term (name, mdp function, joint set) onto one of these ids. */
 enum {
-  H12_R_TRACK_LIN_VEL_XY = 0, /* track_lin_vel_xy_yaw_frame_exp, std 0.5   rough_env_cfg.py:87-91 */
-  H12_R_TRACK_ANG_VEL_Z,      /* track_ang_vel_z_world_exp, std 0.5       rough_env_cfg.py:92-96 */
+  H12_R_TRACK_LIN_VEL_XY = 0, /* track_lin_vel_xy_yaw_frame_exp, std 0.5   rough_env_cfg.py:24-28 */
+  H12_R_TRACK_ANG_VEL_Z,      /* track_ang_vel_z_world_exp, std 0.5       rough_env_cfg.py:29-33 */
   H12_R_ANG_VEL_XY_L2,        /* ang_vel_xy_l2                            velocity_env_cfg.py:237 */
   H12_R_DOF_TORQUES_L2,       /* joint_torques_l2                         flat_env_cfg.py:40-44 */
   H12_R_DOF_ACC_L2,           /* joint_acc_l2                             flat_env_cfg.py:37 */
   H12_R_ACTION_RATE_L2,       /* action_rate_l2                           flat_env_cfg.py:36 */
-  H12_R_FEET_AIR_TIME,        /* feet_air_time_positive_biped, thr 0.4    rough_env_cfg.py:97-105 */
-  H12_R_FLAT_ORIENTATION_L2,  /* flat_orientation_l2                      rough_env_cfg.py:176 */
-  H12_R_DOF_POS_LIMITS,       /* joint_pos_limits (ankles)                rough_env_cfg.py:115-119 */
-  H12_R_TERMINATION,          /* is_terminated                            rough_env_cfg.py:85 */
-  H12_R_FEET_SLIDE,           /* feet_slide                               rough_env_cfg.py:106-113 */
-  H12_R_JOINT_DEV_HIP,        /* joint_deviation_l1 (hip yaw/roll)        rough_env_cfg.py:121-125 */
+  H12_R_FEET_AIR_TIME,        /* feet_air_time_positive_biped, thr 0.4    rough_env_cfg.py:34-42 */
+  H12_R_FLAT_ORIENTATION_L2,  /* flat_orientation_l2                      rough_env_cfg.py:113 */
+  H12_R_DOF_POS_LIMITS,       /* joint_pos_limits (ankles)                rough_env_cfg.py:52-56 */
+  H12_R_TERMINATION,          /* is_terminated                            rough_env_cfg.py:22 */
+  H12_R_FEET_SLIDE,           /* feet_slide                               rough_env_cfg.py:43-50 */
+  H12_R_JOINT_DEV_HIP,        /* joint_deviation_l1 (hip yaw/roll)        rough_env_cfg.py:58-62 */
   H12_R_TRACK_LIN_VEL_XY_BASE,/* track_lin_vel_xy_exp (base frame)        rsl_env_cfg.py:283-287 */
   H12_R_TRACK_ANG_VEL_Z_BASE, /* track_ang_vel_z_exp (base frame)         rsl_env_cfg.py:288-292 */
   H12_R_BASE_HEIGHT_L2,       /* base_height_l2, (z - target)^2           rsl_env_cfg.py:322-328 */
@@ -181,7 +181,7 @@ typedef struct h12env_config {
   float cmd_resample_time;
   float cmd_lin_x[2], cmd_lin_y[2], cmd_ang_z[2], cmd_heading[2];
   float rel_standing_envs, rel_heading_envs, heading_stiffness;
-  /* reset events (rough_env_cfg.py:143-155) */
+  /* reset events (rough_env_cfg.py:77-92) */
   float reset_x[2], reset_y[2], reset_yaw[2];
   /* observation corruption: AdditiveUniformNoise half-widths (velocity_env_cfg.py:124-131) */
   int32_t enable_corruption;

@@ -104,7 +104,7 @@ def test_two_rank_bench_rollout_allgather(tmp_path):
         log = open(tmp_path / f"rank{rank}.log", "w")
         cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--dist-backend", "gloo", "--envs", str(n),
                "--steps", str(K), "--warmup", str(W), "--burn-in", str(B), "--gather-every", "4",
-               "--no-cpu-baseline", "--dump-rollout", str(dump)]
+               "--no-cpu-baseline", "--rollout-decode", "--dump-rollout", str(dump)]
         procs.append((subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, cwd=str(ROOT)), log))
     try:
         for p, _ in procs:
