@@ -116,6 +116,21 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def usable_cpus() -> dict:
+    """The CPUs this process may actually run on: its affinity mask and the cgroup CPU quota (cpu.max), whichever is
+    smaller -- os.cpu_count() is the whole machine's."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota) if quota else aff))
+    return {"affinity": aff, "cgroup_quota": quota, "usable": usable}
+
+
 def cpu_baseline(seconds: float):
     """The CPU oracle (C, fp64, OpenMP over envs) on this host, bounded sample of the same workload."""
     import numpy as np
@@ -125,8 +140,9 @@ def cpu_baseline(seconds: float):
     from h12env import H12FlatEnvCfg
     from h12env.model import build_model
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    avail = usable_cpus()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or avail["usable"]
+    threads = max(1, min(threads, avail["usable"], 16))
     n = 4096
     cfg = H12FlatEnvCfg()
     cfg.scene.num_envs = n
@@ -160,7 +176,7 @@ def cpu_baseline(seconds: float):
               "sample": "C1: oracle MuJoCo mode (sim2sim semantics), 1 env x 1000 policy steps x 20 substeps, "
                         f"random q_ref, ground contact ({dt1:.2f} s)"}
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "cpus_available": avail,
             "single_env_sim2sim": mujoco,
             "sample": f"oracle/h12_oracle.c (fp64, OpenMP) on {n} envs x {steps} env steps "
                       f"({dt:.1f} s) of the same random-action Flat-H12 workload, {threads} host threads"}

@@ -252,6 +252,39 @@ static void kinematics(const h12env_model* m, const orc_phys* s, kin_t* k) {
   }
 }
 
+/* ------------------------------------------------------------------ test hooks: fp32-rounding jitters
+ * (tests/helpers/forced.py only; single-env re-runs, the draw sequences are global and not thread-safe; eps = 0, the
+ * default, is the exact model).
+ * Self contacts: every capsule end point of the self-contacts gets an independent uniform +-eps (m) per
+ * coordinate -- the GPU rounds each rod end it computes independently (fp32, ~1e-7 m at ~1 m), a perturbation that
+ * no perturbation of the joint state reproduces.
+ * Switching thresholds: the joint-limit activation (predicted end-of-step position against the range, and the
+ * one-sided torque test) and the ground-contact activation (predicted end-of-step depth, and the one-sided normal
+ * force test) are DECIDED with the limit / the depth shifted by a fresh uniform +-eps (rad / m) per evaluation; the
+ * forces themselves use the exact values.  A joint pressed against its limit is pinned by the stiff implicit spring
+ * onto the activation surface itself (q + h qd = q_upper to ~1e-9 rad), where the kernel's fp32 evaluation decides
+ * either way and a perturbation of the step's initial state is contracted away by that same spring. */
+static double g_sj_eps = 0.0, g_tj_lim = 0.0, g_tj_ct = 0.0;
+static uint64_t g_sj_state = 0, g_tj_state = 0;
+void orc_set_self_jitter(double eps, uint64_t seed) {
+  g_sj_eps = eps;
+  g_sj_state = seed;
+}
+void orc_set_threshold_jitter(double lim_eps, double contact_eps, uint64_t seed) {
+  g_tj_lim = lim_eps;
+  g_tj_ct = contact_eps;
+  g_tj_state = seed;
+}
+static double splitmix_u(uint64_t* st) { /* splitmix64 -> uniform [-1, 1) */
+  uint64_t z = (*st += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+static double sj_draw(void) { return splitmix_u(&g_sj_state); }
+static double tj_draw(double eps) { return eps > 0.0 ? eps * splitmix_u(&g_tj_state) : 0.0; }
+
 /* ------------------------------------------------------------------ penalty contact */
 /* Penalty force on a sphere (centre pl in body b coords, radius rad).  Normal: spring-damper,
  * clipped at 0.  Tangential: for sole spheres (anc != NULL) an anchored stiction spring-damper
@@ -287,7 +320,8 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   double vn = nrm[0] * vw[0] + nrm[1] * vw[1] + nrm[2] * vw[2];
   /* active when the point is predicted below the ground at the end of the substep (implicit: depth - hi vn), so a
    * point arriving at speed is caught within the substep instead of one substep deep */
-  if (depth - hi * vn <= 0) return 0;
+  const double dj = tj_draw(g_tj_ct); /* 0 unless the threshold-jitter test hook is on */
+  if (depth + dj - hi * vn <= 0) return 0;
   /* implicit contact (hi > 0): the spring-damper force at the END of the substep, k (d - hi vn') - c vn'
    * with vn' = vn + hi an, is the explicit force with damping c + hi k plus the term -hi (c + hi k) an,
    * linear in the contact point's acceleration: an added point inertia (alpha along the normal, beta
@@ -298,7 +332,10 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   double dcap = (hi > 0 && c->max_depenetration_velocity > 0 && anc_out && !was_in) ? hi * c->max_depenetration_velocity
                                                                                      : 1e300;
   double fn = c->contact_k * (depth < dcap ? depth : dcap) - cn * vn;
-  if (fn <= 0) return 0;
+  if (dj != 0.0) {
+    if (c->contact_k * (depth + dj < dcap ? depth + dj : dcap) - cn * vn <= 0) return 0;
+    if (fn < 0) fn = 0;
+  } else if (fn <= 0) return 0;
   double ft0, ft1, beta = 0;
   if (anc_out) {
     double ax = was_in ? anc_in[0] : xw[0], ay = was_in ? anc_in[1] : xw[1];
@@ -408,24 +445,6 @@ typedef struct capsule_w {
   double p0[3], p1[3]; /* world segment */
   double r;
 } capsule_w;
-
-/* Test hook (tests/helpers/forced.py only): jitter every capsule end point of the self-contacts by an independent
- * uniform +-eps (m) per coordinate -- the GPU rounds each rod end it computes independently (fp32, ~1e-7 m at
- * the env's ~1 m scale), a perturbation that no perturbation of the joint state reproduces.  eps = 0 (the
- * default) is the exact model.  Single-env re-runs only (the draw sequence is global, not thread-safe). */
-static double g_sj_eps = 0.0;
-static uint64_t g_sj_state = 0;
-void orc_set_self_jitter(double eps, uint64_t seed) {
-  g_sj_eps = eps;
-  g_sj_state = seed;
-}
-static double sj_draw(void) { /* splitmix64 -> uniform [-1, 1) */
-  uint64_t z = (g_sj_state += 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
-}
 
 /* The self-contact geometry runs in PELVIS-RELATIVE world axes (positions minus the base origin, |x| < 1.2 m): only
  * differences of body points enter it, and the kernel does the same so that its fp32 points carry the ulp of ~1 m,
@@ -709,9 +728,15 @@ static void joint_limit_torque(const h12env_model* m, const h12env_config* c, co
   double cl = c->limit_c + hi * c->limit_k;
   for (int j = 0; j < NJ; ++j) {
     double q = s->q[j], qd = s->qd[j], t = 0, qe = q + hi * qd;
+    const double uh = m->q_upper[j] + tj_draw(g_tj_lim), ul = m->q_lower[j] + tj_draw(g_tj_lim); /* decisions */
     dl[j] = 0;
-    if (qe > m->q_upper[j]) { t = -c->limit_k * (q - m->q_upper[j]) - cl * qd; if (t > 0) t = 0; else dl[j] = hi * cl; }
-    else if (qe < m->q_lower[j]) { t = -c->limit_k * (q - m->q_lower[j]) - cl * qd; if (t < 0) t = 0; else dl[j] = hi * cl; }
+    if (qe > uh) {
+      t = -c->limit_k * (q - m->q_upper[j]) - cl * qd;
+      if (-c->limit_k * (q - uh) - cl * qd > 0) t = 0; else { dl[j] = hi * cl; if (t > 0) t = 0; }
+    } else if (qe < ul) {
+      t = -c->limit_k * (q - m->q_lower[j]) - cl * qd;
+      if (-c->limit_k * (q - ul) - cl * qd < 0) t = 0; else { dl[j] = hi * cl; if (t < 0) t = 0; }
+    }
     /* PhysX max joint velocity: stiff damper on the excess, implicit over the substep (always: the solve
      * must carry the reaction; h = 0 would make it explicit and unstable) */
     double vm = c->max_joint_vel[j], cv = c->max_joint_vel_damping, ex = fabs(qd) - vm, rp = H12_VLIM_RAMP;

@@ -155,6 +155,8 @@ int orc_obs_dim(const h12env_config* c);
 void orc_set_dz_count(int v);
 /* test hook: jitter of the self-contact capsule end points (m), see h12_oracle.c capsule_world */
 void orc_set_self_jitter(double eps, uint64_t seed);
+/* test hook: jitter the joint-limit (rad) / ground-contact (m) switching decisions (forced.py only) */
+void orc_set_threshold_jitter(double lim_eps, double contact_eps, uint64_t seed);
 int orc_dz_count(void);
 
 /* RNG shared by both sides (Philox4x32-10). */

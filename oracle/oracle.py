@@ -113,6 +113,8 @@ def lib():
         L.orc_dz_count.restype = C.c_int
         L.orc_set_self_jitter.argtypes = [C.c_double, C.c_uint64]
         L.orc_set_self_jitter.restype = None
+        L.orc_set_threshold_jitter.argtypes = [C.c_double, C.c_double, C.c_uint64]
+        L.orc_set_threshold_jitter.restype = None
         Tp = C.POINTER(TermIn)
         L.orc_mdp_terms.argtypes = [M, Cf, Tp, dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_mdp_terms.restype = C.c_int
@@ -372,6 +374,12 @@ def dz_count() -> int:
 def set_self_jitter(eps: float, seed: int = 0):
     """Test hook: jitter every self-contact capsule end point by uniform +-eps m per coordinate (0 = exact)."""
     lib().orc_set_self_jitter(float(eps), int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def set_threshold_jitter(lim_eps: float, contact_eps: float, seed: int = 0):
+    """Test hook: decide every joint-limit / ground-contact switch with the limit (rad) / depth (m) shifted by a fresh
+    uniform +-eps (0, 0 = exact; oracle/h12_oracle.c "test hooks")."""
+    lib().orc_set_threshold_jitter(float(lim_eps), float(contact_eps), int(seed) & 0xFFFFFFFFFFFFFFFF)
 
 
 def ground(cfg, x, y):

@@ -54,7 +54,7 @@ AMPLIFY_EPS = 3e-6
 # wrenches are pinned directly (tests/test_gpu_selfcollision.py, h12env_eval_self_contacts: 99 % of envs within
 # 1.5e-4 relative).  An env-step off tolerance whose step the self-contacts act in (the oracle with
 # self_collision off lands elsewhere) is therefore re-run with the oracle's capsule end points jittered
-# independently at the fp32 scale of those points (oracle set_self_jitter, SELF_JITTER metres; positions stay
+# independently at the fp32 scale of those points (oracle set_self_jitter, JITTER metres; positions stay
 # within ~30 m of the origin, ulp <= 2e-6 m): threshold-sensitive when a jittered run reproduces the GPU's result,
 # or when a jitter <= SELF_AMPLIFY moves the oracle itself as far.  What is still not explained is counted
 # separately and allowed at a rate of SELF_RATE: the count must stay within the 99.9 % Poisson quantile of
@@ -64,8 +64,16 @@ AMPLIFY_EPS = 3e-6
 # the env's world position), and no unexplained self-contact env-step is allowed any more (SELF_RATE = 0: the
 # jittered re-runs below must explain every one).
 SELF_RATE = 0.0
-SELF_JITTER = (1e-7,) * 32 + (1e-6,) * 64 + (3e-6,) * 64
+JITTER = (1e-7,) * 32 + (1e-6,) * 64 + (3e-6,) * 64
 SELF_AMPLIFY = 1e-6
+# Switching thresholds (round 3): a joint pressed against its limit is pinned by the stiff implicit limit spring
+# (1e6 N m/rad) ONTO its activation surface, q + h qd = q_upper to ~1e-9 rad (tools and numbers: DESIGN.md section 4);
+# the kernel's fp32 evaluation of that test (ulp(q) ~3e-8 rad) decides either way, and a perturbation of the step's
+# initial state is contracted away by the same spring before the deciding substep.  Likewise a lightly loaded sole
+# point at the contact activation depth.  Every env-step that the state perturbations above do not explain is
+# re-run with those decisions themselves jittered (oracle set_threshold_jitter: limits by at most LIMIT_JITTER_MAX
+# rad, contact depths by eps m); it counts as explained by the same reproduce / ill-conditioned rules.
+LIMIT_JITTER_MAX = 1e-6
 PERTURBS = (1e-7,) * 16 + (1e-6,) * 32 + (3e-6,) * 64 + (1e-5,) * 128
 PHYS = ("POS", "QUAT", "VLIN", "WANG", "Q", "QD")
 TERMS = ("EPSUM", "EPSUM2", "METRIC")  # episode sums of the 20 kernel reward terms (12 Flat + 8 Rsl), command metrics
@@ -167,7 +175,7 @@ class ForcedParity:
         self.bad_counts = {c: 0 for c in CRITERIA}
         self.unexplained = []
         self.self_unexplained = []  # unexplained env-steps in which the self-contacts act (see SELF_RATE)
-        self.self_explained = 0  # ... explained by a jittered self-contact geometry (SELF_JITTER)
+        self.self_explained = 0  # ... of them self-contact steps explained by a jittered re-run (JITTER)
         self.explained = 0
         self.tiers: dict[str, int] = {}  # explained env-steps per (rule, perturbation) tier
         self.dump = [] if os.environ.get("H12_FORCED_DUMP") else None
@@ -213,11 +221,12 @@ class ForcedParity:
                 if self._reproduced(e, F0, I0, obs0, a_np, t, g, o):
                     self.explained += 1
                     continue
-                if self._self_contact_step(e, F0, I0, obs0, a_np, t, o):
-                    if self._reproduced_self(e, F0, I0, obs0, a_np, t, g, o):
-                        self.explained += 1
-                        self.self_explained += 1
-                        continue
+                self_step = self._self_contact_step(e, F0, I0, obs0, a_np, t, o)
+                if self._reproduced_jitter(e, F0, I0, obs0, a_np, t, g, o, self_step):
+                    self.explained += 1
+                    self.self_explained += int(self_step)
+                    continue
+                if self_step:
                     self.self_unexplained.append((t, int(e), {c: round(float(worst[c][e]), 3) for c in worst}))
                     self._dump(t, e, F0, I0, obs0, a_np, g, o)
                     continue
@@ -260,19 +269,22 @@ class ForcedParity:
     def _tier(self, k):
         self.tiers[k] = self.tiers.get(k, 0) + 1
 
-    def _reproduced_self(self, e, F0, I0, obs0, a_np, t, g, o):
-        """True when the oracle, re-run for env e from its exact pre-step state with the self-contact capsule end
-        points jittered by SELF_JITTER, reproduces the GPU's result (same rule as _reproduced), or when a jitter
-        <= SELF_AMPLIFY moves the oracle itself at least half as far (ill-conditioned at the fp32 scale)."""
+    def _reproduced_jitter(self, e, F0, I0, obs0, a_np, t, g, o, self_step):
+        """True when the oracle, re-run for env e with its switching decisions jittered at the fp32 scale by JITTER
+        (joint-limit and ground-contact thresholds, min(eps, LIMIT_JITTER_MAX) rad / eps m; in a self-contact step
+        also the capsule end points, eps m), reproduces the GPU's result (same rule as _reproduced), or when a
+        jitter <= SELF_AMPLIFY moves the oracle itself at least half as far (ill-conditioned at the fp32 scale)."""
         ref = O.OracleEnv(self.env._model, self.env._ccfg, 1, self.env.env_offset + int(e))
         o_e = tuple(x[:, e:e + 1] if x.ndim == 2 and x.shape[-1] == self.env.num_envs else x[e:e + 1] for x in o[:6])
         g_e = tuple(x[:, e:e + 1] if x.ndim == 2 and x.shape[-1] == self.env.num_envs else x[e:e + 1] for x in g[:6])
         f0 = F0[:, e:e + 1]
         d_og = _distance(f0, g_e, o_e, exact=False)
+        tag = "self-jitter" if self_step else "switch-jitter"
         try:
-            for k, eps in enumerate(SELF_JITTER):
+            for k, eps in enumerate(JITTER):
                 O.set_dz_count(self._dz0)
-                O.set_self_jitter(eps, int(self.rng.integers(1 << 62)))
+                O.set_self_jitter(eps if self_step else 0.0, int(self.rng.integers(1 << 62)))
+                O.set_threshold_jitter(min(eps, LIMIT_JITTER_MAX), eps, int(self.rng.integers(1 << 62)))
                 # every other draw also perturbs the state at the fp32 scale: a self-contact step can flip a ground
                 # contact or slip decision as well, which neither perturbation reproduces alone
                 fs = f0 if k % 2 == 0 else perturbed(self.rng, f0, min(eps, 1e-6))
@@ -280,13 +292,14 @@ class ForcedParity:
                 po, pr, pt, ptr, _ = ref.step(a_np[e:e + 1], t)
                 p_e = (ref.F.copy(), ref.I.copy(), po, pr, pt, ptr)
                 if _distance(f0, g_e, p_e, o_e) <= 0.5 * d_og:
-                    self._tier(f"self-jitter-reproduced@{eps:g}")
+                    self._tier(f"{tag}-reproduced@{eps:g}")
                     return True
                 if eps <= SELF_AMPLIFY and _distance(f0, p_e, o_e, exact=False) >= 0.5 * d_og:
-                    self._tier(f"self-jitter-ill-conditioned@{eps:g}")
+                    self._tier(f"{tag}-ill-conditioned@{eps:g}")
                     return True
         finally:
             O.set_self_jitter(0.0)
+            O.set_threshold_jitter(0.0, 0.0)
         return False
 
     def _self_contact_step(self, e, F0, I0, obs0, a_np, t, o):
@@ -307,7 +320,7 @@ class ForcedParity:
     def report(self) -> str:
         frac = {c: self.bad_counts[c] / max(1, self.env_steps) for c in CRITERIA}
         return (f"steps {self.steps} x {self.env.num_envs} envs; failing env-steps per criterion {frac}; worst "
-                f"passing error / tolerance {self.worst}; threshold-sensitive (explained) env-steps {self.explained} (of which by self-contact jitter {self.self_explained}; per tier {dict(sorted(self.tiers.items()))}); unexplained (not threshold-sensitive) "
+                f"passing error / tolerance {self.worst}; threshold-sensitive (explained) env-steps {self.explained} (of which self-contact steps {self.self_explained}; per tier {dict(sorted(self.tiers.items()))}); unexplained (not threshold-sensitive) "
                 f"{len(self.unexplained)}: {self.unexplained[:8]}; self-contact steps off the oracle "
                 f"{len(self.self_unexplained)} (allowed at a rate of {SELF_RATE:g} of env-steps, 99.9 % Poisson quantile): "
                 f"{self.self_unexplained[:4]}")

@@ -1,11 +1,16 @@
 #!/bin/bash
-# One GPU-box pass for a round checkpoint: -m gpu tests, the default bench line, rocprofv3 stats + PMC.
-# Usage (from the repo root, on the GPU box): bash tools/gpu_round.sh <tag>
-set -o pipefail
-TAG=${1:-latest}
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gputest_$TAG.txt 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gputest_$TAG.txt; exit 1; }
-tail -1 gpurun_out/gputest_$TAG.txt
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.log; exit 1; }
-tail -1 gpurun_out/bench_$TAG.log
-bash tools/profile.sh "$TAG"
+# GPU box: the -m gpu suite (forced-parity dumps + per-check log) then the default bench line.  Stops after anything
+# other than a normal pytest pass / fail (a fault, abort or time limit).
+set -u
+tag=${1:-r3}
+mkdir -p gpurun_out/dumps_$tag
+export H12_FORCED_DUMP=gpurun_out/dumps_$tag H12_FORCED_LOG=gpurun_out/${tag}_forced.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread -rf > gpurun_out/${tag}_gputest.txt 2>&1
+rc=$?
+echo "pytest rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
+rc2=$?
+echo "bench rc=$rc2"
+tail -c 3000 gpurun_out/${tag}_bench.json
+exit $rc2
