@@ -747,30 +747,70 @@ H12_DEV void sole_impl_force_flat(const float* a, const float R[3][3], const Sol
 //    by the single wave's instruction stream), and each lane reads back its own knee / foot wrench.
 // Real (un-mirrored) coordinates throughout; the pair force acts +F on the left body, -F on the right one.
 
-// closest points of segments p1-q1 and p2-q2 (the construction of the oracle's seg_closest)
-H12_DEV void seg_closest(const float* p1, const float* q1, const float* p2, const float* q2, float* c1, float* c2) {
+// Contact points of two capsule axes p1-q1, p2-q2 (the oracle's seg_points): general pairs (sin^2 of the angle
+// >= 1e-3) one closest point, with the normal from d1 x d2 when both parameters are interior (well-conditioned where
+// the axes nearly intersect); nearly parallel pairs a line contact, two points at the ends of the overlap along the
+// first segment with half weight each (one point, the nearest ends, without overlap).  Parameters only: the
+// points are p + d s, and the caller loops over them.
+struct SegPts {
+  float d1[3], d2[3], s0, s1, t0, t1, ncx, ncy, ncz, w;
+  int n;
+  bool has_nc;
+};
+H12_DEV void seg_points(const float* p1, const float* q1, const float* p2, const float* q2, SegPts& o) {
+  // branch-free (every field written once, from selects: per-branch stores let the compiler re-form the two
+  // points into a scratch array)
+  float r[3];
+  for (int a = 0; a < 3; ++a) { o.d1[a] = q1[a] - p1[a]; o.d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
+  const float A = dot3(o.d1, o.d1), E = dot3(o.d2, o.d2), F = dot3(o.d2, r), C = dot3(o.d1, r), B = dot3(o.d1, o.d2);
+  const float den = A * E - B * B, iA = frcp(A), iE = frcp(E);
+  const bool par = !(den > 1e-3f * A * E);
+  // nearly parallel: segment 2's ends projected onto segment 1; the overlap [lo, hi]
+  const float u0 = -C * iA, u1 = (B - C) * iA;
+  const float lo = fmaxf(0.f, fminf(u0, u1)), hi = fminf(1.f, fmaxf(u0, u1));
+  const bool line = par && hi > lo;
+  // one point: the clamped closest-point construction (from the unconstrained s, or for parallel axes without
+  // overlap from the middle of the empty overlap = the nearest ends)
+  float s = par ? fminf(fmaxf(0.5f * (lo + hi), 0.f), 1.f) : fminf(fmaxf((B * F - C * E) * frcp(den), 0.f), 1.f);
+  float t = (B * s + F) * iE;
+  const bool tlo = t < 0.f, thi = t > 1.f;
+  s = tlo ? fminf(fmaxf(u0, 0.f), 1.f) : (thi ? fminf(fmaxf(u1, 0.f), 1.f) : s);
+  t = fminf(fmaxf(t, 0.f), 1.f);
+  o.has_nc = !par && !tlo && !thi && s > 0.f && s < 1.f;
+  float c[3];
+  cross(o.d1, o.d2, c);
+  const float cn = o.has_nc ? __builtin_amdgcn_rsqf(dot3(c, c)) : 0.f;
+  o.ncx = c[0] * cn; o.ncy = c[1] * cn; o.ncz = c[2] * cn;
+  o.n = line ? 2 : 1;
+  o.w = line ? 0.5f : 1.f;
+  o.s0 = line ? lo : s;
+  o.t0 = line ? fminf(fmaxf((B * lo + F) * iE, 0.f), 1.f) : t;
+  o.s1 = hi;
+  o.t1 = fminf(fmaxf((B * hi + F) * iE, 0.f), 1.f);
+}
+// broad phase: true when the capsules' axes may come within rr.  The segment distance is Lipschitz in the first
+// segment's parameter with constant |d1| sin(angle) (while the second's stays interior), so for nearly parallel
+// axes the midpoint of the overlap bounds the minimum from below by half the overlap's length times that constant
+H12_DEV bool capsules_near(const float* p1, const float* q1, const float* p2, const float* q2, float rr) {
   float d1[3], d2[3], r[3];
   for (int a = 0; a < 3; ++a) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
   const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
   const float den = A * E - B * B, iA = frcp(A);
-  float s;
+  float s, slack = 0.f;
   if (den > 1e-3f * A * E) {
     s = fminf(fmaxf((B * F - C * E) * frcp(den), 0.f), 1.f);
-  } else {  // nearly parallel (sin^2 < 1e-3): middle of the overlap along the first segment (oracle seg_closest)
+  } else {
     const float t0 = -C * iA, t1 = (B - C) * iA;
     const float lo = fmaxf(0.f, fminf(t0, t1)), hi = fminf(1.f, fmaxf(t0, t1));
     s = fminf(fmaxf(0.5f * (lo + hi), 0.f), 1.f);
+    slack = 0.5f * fmaxf(hi - lo, 0.f) * fsqrt(fmaxf(den, 0.f) * frcp(E)) + 1e-4f;
   }
   float t = (B * s + F) * frcp(E);
   if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-C * iA, 0.f), 1.f); }
   else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((B - C) * iA, 0.f), 1.f); }
-  for (int a = 0; a < 3; ++a) { c1[a] = p1[a] + d1[a] * s; c2[a] = p2[a] + d2[a] * t; }
-}
-H12_DEV bool capsules_near(const float* p1, const float* q1, const float* p2, const float* q2, float rr) {
-  float c1[3], c2[3];
-  seg_closest(p1, q1, p2, q2, c1, c2);
-  const float d[3] = {c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]};
-  return dot3(d, d) < rr * rr;
+  const float dv[3] = {r[0] + d1[0] * s - d2[0] * t, r[1] + d1[1] * s - d2[1] * t, r[2] + d1[2] * s - d2[2] * t};
+  const float reach = rr + slack;
+  return dot3(dv, dv) < reach * reach;
 }
 // real-frame point of a lane-frame body point: M (Rb pl + pb), M = diag(1, sg, 1)
 H12_DEV void body_point_real(const float Rb[3][3], const float* pb, const float* pl, float sg, float* out) {
@@ -895,37 +935,46 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
     const float4 ra = gr[j == 0 ? SG_KNEE : SG_ROD + 2 * (j - 1)], rb = gr[j == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (j - 1) + 1];
     const float pa[3] = {la.x, la.y, la.z}, pb[3] = {lb.x, lb.y, lb.z}, qa[3] = {ra.x, ra.y, ra.z}, qb[3] = {rb.x, rb.y, rb.z};
     const float rs = (i == 0 ? h12m::KNEE_R : h12m::FOOT_R) + (j == 0 ? h12m::KNEE_R : h12m::FOOT_R);
-    float cA[3], cB[3];
-    seg_closest(pa, pb, qa, qb, cA, cB);
-    const float dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
-    const float d2 = dot3(dv, dv);
-    if (!(d2 < rs * rs) || !(d2 > 1e-18f)) continue;
-    const float d = fsqrt(d2), depth = rs - d, id = frcp(d);
-    const float n[3] = {dv[0] * id, dv[1] * id, dv[2] * id};
-    const float x[3] = {0.5f * (cA[0] + cB[0]), 0.5f * (cA[1] + cB[1]), 0.5f * (cA[2] + cB[2])};
+    SegPts sp;
+    seg_points(pa, pb, qa, qb, sp);
     const float4* kl = gl + (i == 0 ? SG_KKIN : SG_FKIN);
     const float4* kr = gr + (j == 0 ? SG_KKIN : SG_FKIN);
     const float4 wl = kl[0], vl = kl[1], ol = kl[2], wr = kr[0], vr_ = kr[1], orr = kr[2];
-    const float rl_[3] = {x[0] - ol.x, x[1] - ol.y, x[2] - ol.z}, rr_[3] = {x[0] - orr.x, x[1] - orr.y, x[2] - orr.z};
-    const float WL[3] = {wl.x, wl.y, wl.z}, WR[3] = {wr.x, wr.y, wr.z};
-    float ul[3], ur[3];
-    cross(WL, rl_, ul);
-    cross(WR, rr_, ur);
-    const float vrel[3] = {vl.x + ul[0] - vr_.x - ur[0], vl.y + ul[1] - vr_.y - ur[1], vl.z + ul[2] - vr_.z - ur[2]};
-    const float vn = dot3(vrel, n), fn = P.sk * depth - P.sc * vn;
-    if (!(fn > 0.f)) continue;
-    float F[3];
-    for (int a = 0; a < 3; ++a) F[a] = -P.sct * (vrel[a] - vn * n[a]);
-    const float ftn2 = dot3(F, F), cap = P.smu * fn;
-    if (ftn2 > cap * cap) { const float sc = cap * __builtin_amdgcn_rsqf(ftn2); F[0] *= sc; F[1] *= sc; F[2] *= sc; }
-    for (int a = 0; a < 3; ++a) F[a] += fn * n[a];
-    float m[3];
-    cross(x, F, m);
     float* al = L.acc[e][0][i > 0];
     float* ar = L.acc[e][1][j > 0];
-    for (int a = 0; a < 3; ++a) {
-      atomicAdd(&al[a], F[a]); atomicAdd(&al[4 + a], m[a]);
-      atomicAdd(&ar[a], -F[a]); atomicAdd(&ar[4 + a], -m[a]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // unrolled: sp's arrays stay in registers
+      if (q >= sp.n) break;
+      float cA[3], cB[3];
+      const float sq = q ? sp.s1 : sp.s0, tq = q ? sp.t1 : sp.t0;
+      for (int a = 0; a < 3; ++a) { cA[a] = pa[a] + sp.d1[a] * sq; cB[a] = qa[a] + sp.d2[a] * tq; }
+      const float dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
+      const float d2 = dot3(dv, dv);
+      if (!(d2 < rs * rs) || !(d2 > 1e-18f)) continue;
+      const float d = fsqrt(d2), depth = rs - d, id = frcp(d);
+      const float sgn = dv[0] * sp.ncx + dv[1] * sp.ncy + dv[2] * sp.ncz < 0.f ? -1.f : 1.f;
+      const float n[3] = {sp.has_nc ? sgn * sp.ncx : dv[0] * id, sp.has_nc ? sgn * sp.ncy : dv[1] * id,
+                          sp.has_nc ? sgn * sp.ncz : dv[2] * id};
+      const float x[3] = {0.5f * (cA[0] + cB[0]), 0.5f * (cA[1] + cB[1]), 0.5f * (cA[2] + cB[2])};
+      const float rl_[3] = {x[0] - ol.x, x[1] - ol.y, x[2] - ol.z}, rr_[3] = {x[0] - orr.x, x[1] - orr.y, x[2] - orr.z};
+      const float WL[3] = {wl.x, wl.y, wl.z}, WR[3] = {wr.x, wr.y, wr.z};
+      float ul[3], ur[3];
+      cross(WL, rl_, ul);
+      cross(WR, rr_, ur);
+      const float vrel[3] = {vl.x + ul[0] - vr_.x - ur[0], vl.y + ul[1] - vr_.y - ur[1], vl.z + ul[2] - vr_.z - ur[2]};
+      const float vn = dot3(vrel, n), fn = sp.w * (P.sk * depth - P.sc * vn);
+      if (!(fn > 0.f)) continue;
+      float F[3];
+      for (int a = 0; a < 3; ++a) F[a] = -sp.w * P.sct * (vrel[a] - vn * n[a]);
+      const float ftn2 = dot3(F, F), cap = P.smu * fn;
+      if (ftn2 > cap * cap) { const float sc = cap * __builtin_amdgcn_rsqf(ftn2); F[0] *= sc; F[1] *= sc; F[2] *= sc; }
+      for (int a = 0; a < 3; ++a) F[a] += fn * n[a];
+      float m[3];
+      cross(x, F, m);
+      for (int a = 0; a < 3; ++a) {
+        atomicAdd(&al[a], F[a]); atomicAdd(&al[4 + a], m[a]);
+        atomicAdd(&ar[a], -F[a]); atomicAdd(&ar[4 + a], -m[a]);
+      }
     }
   }
   wave_sync();

@@ -416,28 +416,65 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
  * jointed parent/child pairs; within one leg no knee/foot pair can touch (shank 0.4 m), so every left/right
  * pair is tested.  Generic restatement (world frame, every pair, fp64); the kernel mirrors it per lane pair. */
 
-/* closest points of segments p1-q1 and p2-q2 (the standard clamped-parameter construction); nearly parallel
- * segments (sin^2 of the angle < 1e-3, ~1.8 deg) take the middle of their overlap along the first segment: a line
- * contact's centre, and well-conditioned in fp32 (den = |d1|^2 |d2|^2 sin^2 loses ~log10(1/sin^2) digits
- * to cancellation; the parallel side rods of two feet side by side sit right there) */
-static void seg_closest(const double p1[3], const double q1[3], const double p2[3], const double q2[3], double c1[3],
-                        double c2[3]) {
+/* Contact points of two capsule axes p1-q1 and p2-q2 (the self-contact model; the kernel's seg_points restates it):
+ * * general (sin^2 of the angle between the axes >= 1e-3): the closest points (the standard clamped-parameter
+ *   construction), one point.  When both parameters are interior the closest-point difference is along d1 x d2, and
+ *   the contact normal is taken from that cross product (sign: the difference's side): the same direction, but
+ *   well-conditioned where the axes nearly intersect (rods pressed through each other to their axes), where the
+ *   difference itself is a few fp32 ulps long and its direction is noise;
+ * * nearly parallel (sin^2 < 1e-3, 1.8 deg): a LINE contact -- two points, at the two ends of the overlap of the
+ *   segments along the first one, each with half the pair's stiffness and damping (a uniformly pressed parallel pair
+ *   gets the one-point law; a tilted one is pressed at its closer end).  Without overlap: the nearest ends, one point.
+ * Returns the number of points; w: the per-point weight; nc: the cross-product normal (unit, from segment 2 towards
+ * segment 1) when has_nc. */
+typedef struct seg_pts {
+  int n, has_nc;
+  double w, c1[2][3], c2[2][3], nc[3];
+} seg_pts;
+static double seg_t(double B, double F, double E, double s) { return clampd((B * s + F) / E, 0.0, 1.0); }
+static void seg_points(const double p1[3], const double q1[3], const double p2[3], const double q2[3], seg_pts* o) {
   double d1[3], d2[3], r[3];
   for (int a = 0; a < 3; ++a) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
   const double A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
   const double den = A * E - B * B;
-  double s;
+  double sp[2], tp[2];
+  o->n = 1;
+  o->w = 1.0;
+  o->has_nc = 0;
+  o->nc[0] = o->nc[1] = o->nc[2] = 0.0;
   if (den > 1e-3 * A * E) {
-    s = clampd((B * F - C * E) / den, 0.0, 1.0);
+    double s = clampd((B * F - C * E) / den, 0.0, 1.0), t = (B * s + F) / E;
+    if (t < 0.0) { t = 0.0; s = clampd(-C / A, 0.0, 1.0); }
+    else if (t > 1.0) { t = 1.0; s = clampd((B - C) / A, 0.0, 1.0); }
+    else if (s > 0.0 && s < 1.0) {
+      double c[3];
+      cross3(d1, d2, c);
+      const double cn = 1.0 / sqrt(dot3(c, c));
+      for (int a = 0; a < 3; ++a) o->nc[a] = c[a] * cn;
+      o->has_nc = 1;
+    }
+    sp[0] = s;
+    tp[0] = t;
   } else {
-    const double t0 = -C / A, t1 = (B - C) / A;
+    const double t0 = -C / A, t1 = (B - C) / A; /* segment 2's ends projected onto segment 1 */
     const double lo = fmax(0.0, fmin(t0, t1)), hi = fmin(1.0, fmax(t0, t1));
-    s = clampd(0.5 * (lo + hi), 0.0, 1.0);
+    if (hi > lo) {
+      o->n = 2;
+      o->w = 0.5;
+      sp[0] = lo;
+      sp[1] = hi;
+      tp[0] = seg_t(B, F, E, lo);
+      tp[1] = seg_t(B, F, E, hi);
+    } else { /* end to end: the nearest ends */
+      double s = clampd(0.5 * (lo + hi), 0.0, 1.0), t = (B * s + F) / E;
+      if (t < 0.0) { t = 0.0; s = clampd(-C / A, 0.0, 1.0); }
+      else if (t > 1.0) { t = 1.0; s = clampd((B - C) / A, 0.0, 1.0); }
+      sp[0] = s;
+      tp[0] = t;
+    }
   }
-  double t = (B * s + F) / E;
-  if (t < 0.0) { t = 0.0; s = clampd(-C / A, 0.0, 1.0); }
-  else if (t > 1.0) { t = 1.0; s = clampd((B - C) / A, 0.0, 1.0); }
-  for (int a = 0; a < 3; ++a) { c1[a] = p1[a] + d1[a] * s; c2[a] = p2[a] + d2[a] * t; }
+  for (int k = 0; k < o->n; ++k)
+    for (int a = 0; a < 3; ++a) { o->c1[k][a] = p1[a] + d1[a] * sp[k]; o->c2[k][a] = p2[a] + d2[a] * tp[k]; }
 }
 
 typedef struct capsule_w {
@@ -506,29 +543,33 @@ static void self_contacts(const h12env_model* m, const h12env_config* c, const k
   for (int i = 0; i < 5; ++i)
     for (int j = 0; j < 5; ++j) {
       const capsule_w *A = &cap[0][i], *Bc = &cap[1][j];
-      double cA[3], cB[3];
-      seg_closest(A->p0, A->p1, Bc->p0, Bc->p1, cA, cB);
-      double dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
-      const double d = sqrt(dot3(dv, dv)), depth = A->r + Bc->r - d;
-      if (!(depth > 0.0) || d < 1e-9) continue;
-      double n[3], x[3], va[3], vb[3], vr[3];
-      for (int a = 0; a < 3; ++a) { n[a] = dv[a] / d; x[a] = 0.5 * (cA[a] + cB[a]); }
-      point_vel(k, A->b, x, va);
-      point_vel(k, Bc->b, x, vb);
-      for (int a = 0; a < 3; ++a) vr[a] = va[a] - vb[a];
-      const double vn = dot3(vr, n), fn = c->self_k * depth - c->self_c * vn;
-      if (!(fn > 0.0)) continue;
-      double ft[3];
-      for (int a = 0; a < 3; ++a) ft[a] = -c->self_ct * (vr[a] - vn * n[a]);
-      const double ftn = sqrt(dot3(ft, ft)), cap_t = c->self_mu * fn;
-      if (ftn > cap_t) for (int a = 0; a < 3; ++a) ft[a] *= cap_t / ftn;
-      double F[3], Fm[3];
-      for (int a = 0; a < 3; ++a) { F[a] = fn * n[a] + ft[a]; Fm[a] = -F[a]; }
-      apply_world_force(k, A->b, x, F, fext);
-      apply_world_force(k, Bc->b, x, Fm, fext);
-      double* ra = i == 0 ? rr->knee_force[0] : rr->foot_force[0];
-      double* rb = j == 0 ? rr->knee_force[1] : rr->foot_force[1];
-      for (int a = 0; a < 3; ++a) { ra[a] += F[a]; rb[a] -= F[a]; }
+      seg_pts sp;
+      seg_points(A->p0, A->p1, Bc->p0, Bc->p1, &sp);
+      for (int q = 0; q < sp.n; ++q) {
+        const double *cA = sp.c1[q], *cB = sp.c2[q];
+        double dv[3] = {cA[0] - cB[0], cA[1] - cB[1], cA[2] - cB[2]};
+        const double d = sqrt(dot3(dv, dv)), depth = A->r + Bc->r - d;
+        if (!(depth > 0.0) || d < 1e-9) continue;
+        double n[3], x[3], va[3], vb[3], vr[3];
+        const double sgn = dot3(dv, sp.nc) < 0.0 ? -1.0 : 1.0;
+        for (int a = 0; a < 3; ++a) { n[a] = sp.has_nc ? sgn * sp.nc[a] : dv[a] / d; x[a] = 0.5 * (cA[a] + cB[a]); }
+        point_vel(k, A->b, x, va);
+        point_vel(k, Bc->b, x, vb);
+        for (int a = 0; a < 3; ++a) vr[a] = va[a] - vb[a];
+        const double vn = dot3(vr, n), fn = sp.w * (c->self_k * depth - c->self_c * vn);
+        if (!(fn > 0.0)) continue;
+        double ft[3];
+        for (int a = 0; a < 3; ++a) ft[a] = -sp.w * c->self_ct * (vr[a] - vn * n[a]);
+        const double ftn = sqrt(dot3(ft, ft)), cap_t = c->self_mu * fn;
+        if (ftn > cap_t) for (int a = 0; a < 3; ++a) ft[a] *= cap_t / ftn;
+        double F[3], Fm[3];
+        for (int a = 0; a < 3; ++a) { F[a] = fn * n[a] + ft[a]; Fm[a] = -F[a]; }
+        apply_world_force(k, A->b, x, F, fext);
+        apply_world_force(k, Bc->b, x, Fm, fext);
+        double* ra = i == 0 ? rr->knee_force[0] : rr->foot_force[0];
+        double* rb = j == 0 ? rr->knee_force[1] : rr->foot_force[1];
+        for (int a = 0; a < 3; ++a) { ra[a] += F[a]; rb[a] -= F[a]; }
+      }
     }
 }
 
