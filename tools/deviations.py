@@ -6,11 +6,12 @@ MJCF for the pelvis body's own inertial): a random-action Flat rollout, then per
      keeping torso_link as a separate body; the build's definition since round 2) vs the composite base COM
      (pelvis + the 40 welded upper-body bodies; the round-1 definition): |dv_xy| and the change of the
      track_lin_vel_xy_exp reward term between the two -- why the definition matters;
-  2. joint limits: penalty limits (1000 N m/rad) instead of PhysX's hard limits -- how often and how far a joint
-     sits beyond its range;
+  2. joint limits: a stiff implicit limit spring (1e6 N m/rad on the predicted end-of-step position) plus the
+     0.01 rad hard-limit projection instead of PhysX's hard limits -- how often and how far a joint sits beyond its
+     range (all joint-env-steps, and the ones beyond);
   3. contact stiffness: sole-sphere penetration depth of the penalty springs (PhysX: rigid, ~0).
 
-    python tools/deviations.py [--envs 1024] [--steps 300]
+    python tools/deviations.py [--envs 1024] [--steps 300] [--out profiles/r3_deviations.json]
 """
 from __future__ import annotations
 
@@ -38,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--out", type=str, default=None)
+    ap.add_argument("--contact-k", type=float, default=None, help="experiment: ground contact stiffness override")
     a = ap.parse_args()
     import oracle as O
     from gen_model import inertial_of
@@ -50,6 +53,8 @@ def main():
     model = build_model()
     c_comp = np.asarray(model.base_com, dtype=np.float64)  # composite (model.root_com: the pelvis body)
     cfg = H12FlatEnvCfg()
+    if a.contact_k:
+        cfg.sim.contact_k = a.contact_k
     n = a.envs
     env = O.OracleEnv(model, cfg.to_c(), n)
     env.reset()
@@ -102,11 +107,17 @@ def main():
         "track_lin_vel_xy_exp_abs_change": {"median": float(np.median(dr)), "p95": float(np.percentile(dr, 95))},
         "joint_env_steps_beyond_limit_fraction": float((excess > 0).mean()),
         "joint_limit_excess_rad": {"p99": float(np.percentile(excess, 99)), "max": float(excess.max())},
+        "joint_limit_excess_rad_beyond_only": {"median": float(np.median(excess[excess > 0])) if (excess > 0).any() else 0.0,
+                                               "p99": float(np.percentile(excess[excess > 0], 99)) if (excess > 0).any() else 0.0},
+        "sim": {"contact_k": cfg.sim.contact_k, "limit_k": cfg.sim.limit_k, "limit_projection": cfg.sim.limit_projection,
+                "max_depenetration_velocity": cfg.sim.max_depenetration_velocity},
     }
     if depth:
         d = np.asarray(depth)
         out["sole_penetration_mm_in_contact"] = {"median": float(1e3 * np.median(d)), "p95": float(1e3 * np.percentile(d, 95))}
     print(json.dumps(out, indent=1))
+    if a.out:
+        Path(a.out).write_text(json.dumps(out, indent=1) + "\n")
 
 
 if __name__ == "__main__":
