@@ -9,11 +9,11 @@ integration step each, delayed PD, contact, sensor, rewards, terminations, reset
 450-float observations).  Actions ~ N(0,1) are pre-generated and resident in HBM before timing.
 Envs shard across ranks (4096 per GPU, weak scaling, RNG keyed by global env id).  With N > 1 the
 timed region is BASELINE config C4: every rank records its shard's rollout compactly (per env-step
-the new observation frame, action, reward, done flags: h12env.rollout), all-gathers it over RCCL in
-chunks of --gather-every steps on a side stream while it keeps stepping, and decodes the global
-(T = 24, N_global, 450) observation rows a PPO learner consumes; the line's c4_rollout_allgather
-splits env / all-gather / decode time.  N = 1 is config C2 (no collective; --rollout on forces the
-record + copy + decode path on one GPU).
+the new observation frame, action, reward, done flags: h12env.rollout) and all-gathers it over RCCL,
+asynchronously on RCCL's stream, once per rollout of T = 24 steps (--gather-every: smaller chunks)
+while it steps the next rollout; --rollout-decode also rebuilds the global (T, N_global, 450)
+observation rows on every rank.  The line's c4_rollout_allgather splits env / all-gather / decode
+time.  N = 1 is config C2 (no collective; --rollout on records on one GPU).
 
 Steady state: episode_length_buf is randomised first (rsl_rl's init_at_random_ep_len) and a fixed
 burn-in (--burn-in, untimed, on top of --warmup) lets falls and time-outs reach their steady rate, so
@@ -75,12 +75,12 @@ def parse():
     p.add_argument("--no-self-collision", action="store_true", help="experiment: legs do not collide (not the metric)")
     p.add_argument("--rollout", choices=("auto", "on", "off"), default="auto",
                    help="BASELINE config C4: record the compact rollout (frame, action, reward, dones per env-step) and "
-                        "all-gather it over the ranks every --gather-every steps on a side stream, decoding the full "
-                        "(T, N_global, 450) observation rows on every rank, inside the timed region (auto: on when "
-                        "N > 1; N = 1 is config C2, the plain rollout)")
+                        "all-gather it over the ranks (asynchronous RCCL collective per rollout, or per --gather-every "
+                        "steps) inside the timed region (auto: on when N > 1; N = 1 is config C2, the plain rollout)")
     p.add_argument("--rollout-steps", type=int, default=24,
                    help="rollout length T (num_steps_per_env, C12/agents/rsl_rl_ppo_cfg.py:12)")
-    p.add_argument("--gather-every", type=int, default=4, help="all-gather chunk length G in env steps (C4)")
+    p.add_argument("--gather-every", type=int, default=None,
+                   help="all-gather chunk length G in env steps (C4; default: the rollout length)")
     p.add_argument("--rollout-decode", action="store_true",
                    help="C4: also rebuild the global (T, N_global, 450) observation rows on every rank after each "
                         "gathered chunk (off: the gathered records are handed over; a learner rebuilds its minibatch rows)")
@@ -322,19 +322,22 @@ def main():
             D.all_gather_into_tensor(tail, env.get_observations()["policy"].contiguous())
         else:
             tail.copy_(env.get_observations()["policy"])
-        rg = RolloutGather(rec, world, args.gather_every, tail, timing=True, decode=args.rollout_decode)
+        # no timing events inside the timed window (each event record costs host time comparable to a step); the
+        # all-gather / decode split is measured in an untimed pass right after it
+        rg = RolloutGather(rec, world, args.gather_every, tail, timing=False, decode=args.rollout_decode)
+        pool_off = B + W  # actions[pool_off + i] is the action of timed step i
         env.bind_rollout(rec)
 
-        def put_actions(i0):
-            def f(t0, t1):  # the chunk's actions (pool slices) into the records, one copy when contiguous
-                a0 = i0 % pool
-                span = t1 - t0
+        def put_actions(i_end):
+            def f(s0, s1):  # the chunk's actions (pool slices) into ring slots [s0, s1), one copy when contiguous
+                span = s1 - s0
+                a0 = (i_end - span) % pool
                 if a0 + span <= pool:
-                    rec.actions[t0:t1].copy_(actions[a0:a0 + span])
+                    rec.actions[s0:s1].copy_(actions[a0:a0 + span])
                 else:
                     k = pool - a0
-                    rec.actions[t0:t0 + k].copy_(actions[a0:])
-                    rec.actions[t0 + k:t1].copy_(actions[:span - k])
+                    rec.actions[s0:s0 + k].copy_(actions[a0:])
+                    rec.actions[s0 + k:s1].copy_(actions[:span - k])
             return f
 
     barrier()
@@ -348,11 +351,10 @@ def main():
             continue
         rg.before_step()
         tc = rec.t
-        env.step(actions[(B + W + i) % pool])
-        rg.after_step(tc, put_actions(B + W + i - (tc - rg.chunk_of(tc)[1])))
-    if rg is not None:
-        tc = rec.t
-        rg.flush(tc if tc else 0, put_actions(B + W + K - (tc - rg.chunk_of(max(tc - 1, 0))[1])) if tc else None)
+        env.step(actions[(pool_off + i) % pool])
+        rg.after_step(tc, put_actions(pool_off + i + 1))
+    if rg is not None and K > 0:
+        rg.flush(rec.t, put_actions(pool_off + K))
     ev_c[1].record()
     if rg is not None:
         rg.wait()
@@ -372,36 +374,51 @@ def main():
         if not args.rollout_decode:  # the check rebuilds the rows of the gathered records once, untimed
             from h12env.rollout import decode as _decode
 
-            _decode(rg.gathered, world, n, te, rg.G, rec.history, 0, te, rg.tail, rg.obs[:te])
-        np.savez(args.dump_rollout, obs=rg.obs[:te].cpu().numpy(), gathered=rg.gathered.cpu().numpy(),
+            _decode(rg.records(0), world, n, te, rg.G, rec.history, 0, te, rg.tail, rg.obs[:te])
+        np.savez(args.dump_rollout, obs=rg.obs[:te].cpu().numpy(), gathered=rg.records(0).cpu().numpy(),
                  tail=rg.tail.cpu().numpy(), off=np.array(rec.off), step_bytes=rec.step_bytes, T=te, G=rg.G,
                  n=n, world=world, burn_in=B, warmup=W, steps=K, pool=pool)
-    if rg is not None:
+    final_obs = env.get_observations()["policy"].clone()
+    if rg is not None and not args.profile_only:
+        # the split pass (untimed, after the window): two more rollouts with an event pair around every chunk's
+        # gather and decode on the comm stream
+        chunks_timed = rg.seq
+        rg.timing = True
+        for i in range(2 * args.rollout_steps):
+            rg.before_step()
+            tc = rec.t
+            env.step(actions[(pool_off + K + i) % pool])
+            rg.after_step(tc, put_actions(pool_off + K + i + 1))
+        rg.wait()
         st = rg.stats()
+        split_iters = 2
         env_span = ev_c[0].elapsed_time(ev_c[1])
         iters = K / args.rollout_steps
         rec_b = rec.step_bytes
-        recv = st["gathered_bytes"] * (world - 1) / world  # bytes each rank receives from the others
-        c4 = {"rollout_steps": args.rollout_steps, "gather_every": rg.G, "chunks": st["chunks"],
+        recv = st["gathered_bytes"] / split_iters * (world - 1) / world  # bytes each rank receives from the others
+        c4 = {"rollout_steps": args.rollout_steps, "gather_every": rg.G, "chunks": chunks_timed,
+              "split_pass_chunks": st["chunks"],
               "record_bytes_per_env_step": rec_b / n, "full_row_bytes_per_env_step": (env.obs_dim + 12 + 2) * 4,
-              "gathered_bytes": st["gathered_bytes"], "received_bytes_per_rank": recv,
-              "env_stream_ms_per_iter": env_span / iters, "allgather_ms_per_iter": st["gather_ms"] / iters,
-              "decode_ms_per_iter": st["decode_ms"] / iters, "ms_per_iter": 1e3 * dt / iters,
+              "gathered_bytes_per_iter": st["gathered_bytes"] / split_iters, "received_bytes_per_rank_per_iter": recv,
+              "env_stream_ms_per_iter": env_span / iters, "allgather_ms_per_iter": st["gather_ms"] / split_iters,
+              "decode_ms_per_iter": st["decode_ms"] / split_iters, "ms_per_iter": 1e3 * dt / iters,
               "allgather_algbw_gbs": st["gathered_bytes"] / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] else None,
-              "allgather_busbw_gbs": recv / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] and world > 1 else None,
+              "allgather_busbw_gbs": recv * split_iters / (st["gather_ms"] * 1e-3) / 1e9 if st["gather_ms"] and world > 1 else None,
               "rows_rebuilt": bool(args.rollout_decode),
               "decoded_rows_bytes_per_iter": args.rollout_steps * world * n * env.obs_dim * 4 if args.rollout_decode else 0,
               "decode_gbs": (args.rollout_decode and st["chunks"] and st["decode_ms"] and
                              rg.G * world * n * env.obs_dim * 4 * st["chunks"] / (st["decode_ms"] * 1e-3) / 1e9) or None,
-              "overlap": "gathers (+ row rebuilds) on a side stream ordered by signal-memory fences, concurrent with "
-                         "the next chunk's env steps",
-              "backend": (args.dist_backend if world > 1 else "copy (N = 1)")}
+              "overlap": "one asynchronous RCCL all-gather per chunk (default: per rollout) on RCCL's stream, concurrent "
+                         "with the next rollout's env steps into the other half of a 2T-record ring; the split above "
+                         "comes from an untimed pass that serialises each gather between an event pair",
+              "backend": (args.dist_backend if world > 1 else "none (N = 1: the records are read in place)")}
+        if world == 1:  # nothing is gathered: no all-gather time or bandwidth to report
+            c4.update(allgather_ms_per_iter=None, allgather_algbw_gbs=None, gathered_bytes_per_iter=0)
         env.unbind_rollout()
     if args.profile_only:
         if rank == 0:
             print(json.dumps({"profile_only": True, "ms_per_step": 1e3 * dt / K}))
         return
-    final_obs = env.get_observations()["policy"].clone()
 
     # replay of the timed window from the snapshot: count its resets and time each launch with HIP
     # events bound to the dispatches (kernel begin / end, as rocprofv3 reports them); the replay must

@@ -72,13 +72,15 @@ def broadcast(t: torch.Tensor, src: int = 0) -> None:
         dist.broadcast(t, src=src)
 
 
-def all_gather_into_tensor(out: torch.Tensor, x: torch.Tensor) -> None:
+def all_gather_into_tensor(out: torch.Tensor, x: torch.Tensor, async_op: bool = False):
+    """async_op (RCCL): returns the collective's Work -- ``work.wait()`` makes the CURRENT stream wait for it (a
+    device-side wait, the host does not block); staged (gloo) it completes before returning (None)."""
     if _staged() and x.is_cuda:
         h = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(h, x.cpu())
         out.copy_(h)
-    else:
-        dist.all_gather_into_tensor(out, x)
+        return None
+    return dist.all_gather_into_tensor(out, x, async_op=async_op)
 
 
 def allgather_envs(x: torch.Tensor, shard: Shard, env_dim: int = 0) -> torch.Tensor:

@@ -546,7 +546,7 @@ class H12VelocityEnv:
             o.rew, o.terminated, o.truncated, o.frame_out = self._rollout_ptrs[t]
             self.reward_buf, self.reset_terminated, self.reset_time_outs = self._rollout_views[t]
             self.reset_buf = self.reset_terminated
-            rec.t = t + 1 if t + 1 < rec.T else 0
+            rec.t = t + 1 if t + 1 < rec.slots else 0
         o.log_acc = self._log_ptr + slot * (NLOG * 4)
         rc = self._lib.h12env_step(self._h, a.data_ptr(), prev.data_ptr(), o_ref, self.common_step_counter,
                                    _raw_stream(self._dev_index))
@@ -564,7 +564,7 @@ class H12VelocityEnv:
     def bind_rollout(self, rec):
         """Record every following step into the compact rollout ``rec`` (h12env.rollout.RolloutRecorder; BASELINE
         config C4): the step's reward, terminated / truncated flags and new observation frame (as it enters the
-        history) are written by the kernels straight into step record ``rec.t``, which then advances (mod T); the
+        history) are written by the kernels straight into ring slot ``rec.t``, which then advances (mod rec.slots); the
         returned reward / flag tensors are views of that record.  Flat observation layout only (the frames rebuild
         the history rows)."""
         if self.obs_dim == NOBS_ROUGH or self._cat:
@@ -573,8 +573,8 @@ class H12VelocityEnv:
             raise ValueError("rollout recorder was built for another env shape")
         self._rollout_saved = (self.reward_buf, self.reset_terminated, self.reset_time_outs)
         self._rollout_ptrs = [(rec.rewards[t].data_ptr(), rec.terminated[t].data_ptr(), rec.truncated[t].data_ptr(),
-                               rec.frames[t].data_ptr()) for t in range(rec.T)]
-        self._rollout_views = [(rec.rewards[t], rec.terminated[t], rec.truncated[t]) for t in range(rec.T)]
+                               rec.frames[t].data_ptr()) for t in range(rec.slots)]
+        self._rollout_views = [(rec.rewards[t], rec.terminated[t], rec.truncated[t]) for t in range(rec.slots)]
         self._rollout_outs = []
         for k in range(2):
             o = H12StepOut()

@@ -4,9 +4,10 @@ rsl_rl's RolloutStorage (rsl-rl-lib 2.3.3) keeps per iteration (T, N, 450) obser
 (C12/agents/rsl_rl_ppo_cfg.py:12).  A 450-float row is 10 frames of 45 floats (CircularBuffer, term-major,
 T/utils/history/circular_buffer.py:79-170), nine of which the previous row already holds.  So a shard records, per
 env-step, only the new frame exactly as it enters the history (h12env_step_out.frame_out: noise and term scales
-applied), the action, the reward and the two done flags -- 238 B instead of 1856 B -- the shards' records are
-all-gathered in chunks of G steps on a side stream while the env keeps stepping, and every rank rebuilds the full
-(T, N_global, 450) rows with ``h12env_rollout_decode`` (HIP), bit-identical to the rows the envs returned.
+applied), the action, the reward and the two done flags -- 234 B instead of 1856 B -- the shards' records are
+all-gathered (one RCCL collective per rollout by default, asynchronous on RCCL's stream) while the env steps the next
+rollout into the other half of a ring of 2T records, and every rank can rebuild the full (T, N_global, 450) rows
+with ``h12env_rollout_decode`` (HIP), bit-identical to the rows the envs returned.
 
 Layouts are the C library's (include/h12env.h, h12env_rollout_layout): a step record of one shard is
 frames f32 [n][45] | actions f32 [n][12] | rewards f32 [n] | terminated u8 [n] | truncated u8 [n] (256-B aligned
@@ -16,7 +17,6 @@ step.
 from __future__ import annotations
 
 import ctypes as C
-import time
 
 import torch
 
@@ -34,33 +34,40 @@ def record_layout(n: int):
 
 
 class RolloutRecorder:
-    """Device-resident compact rollout of one shard: T step records of n envs (one uint8 buffer).
+    """Device-resident compact rollout of one shard: a ring of nbuf x T step records of n envs (one uint8 buffer).
 
     ``H12VelocityEnv.bind_rollout(rec)`` makes every env.step write its reward, done flags and new observation frame
-    straight into step record ``rec.t`` (no extra copies) and advance the cursor; the caller writes the actions
-    (``rec.actions[t]``), as a PPO runner stores its own actions."""
+    straight into ring slot ``rec.t`` (no extra copies) and advance the cursor (mod nbuf T); the caller writes the
+    actions (``rec.actions[slot]``), as a PPO runner stores its own actions.  Rollout k occupies slots
+    [(k mod nbuf) T, (k mod nbuf + 1) T): with nbuf = 2 the all-gather of one rollout has the whole next rollout to
+    complete before its records are rewritten."""
 
-    def __init__(self, num_envs: int, T: int, device, history: int):
-        self.n, self.T, self.history = int(num_envs), int(T), int(history)
+    def __init__(self, num_envs: int, T: int, device, history: int, nbuf: int = 2):
+        self.n, self.T, self.history, self.nbuf = int(num_envs), int(T), int(history), int(nbuf)
+        self.slots = self.nbuf * self.T
         self.off, self.step_bytes = record_layout(self.n)
-        self.record = torch.zeros(self.T * self.step_bytes, dtype=torch.uint8, device=device)
-        steps = self.record.view(self.T, self.step_bytes)
+        self.record = torch.zeros(self.slots * self.step_bytes, dtype=torch.uint8, device=device)
+        steps = self.record.view(self.slots, self.step_bytes)
         n, o = self.n, self.off
 
         def sec(i, count, dtype, shape):
             nb = count * torch.tensor([], dtype=dtype).element_size()
-            return steps[:, o[i]:o[i] + nb].view(dtype).view(self.T, *shape)
+            return steps[:, o[i]:o[i] + nb].view(dtype).view(self.slots, *shape)
 
         self.frames = sec(0, n * OBS_FRAME, torch.float32, (n, OBS_FRAME))
         self.actions = sec(1, n * NJ, torch.float32, (n, NJ))
         self.rewards = sec(2, n, torch.float32, (n,))
         self.terminated = sec(3, n, torch.bool, (n,))
         self.truncated = sec(4, n, torch.bool, (n,))
-        self.t = 0  # next step record env.step writes
+        self.t = 0  # next ring slot env.step writes
 
-    def chunk_bytes(self, t0: int, t1: int) -> torch.Tensor:
-        """The shard's records of steps [t0, t1) (contiguous)."""
-        return self.record[t0 * self.step_bytes:t1 * self.step_bytes]
+    def chunk_bytes(self, s0: int, s1: int) -> torch.Tensor:
+        """The shard's records of ring slots [s0, s1) (contiguous)."""
+        return self.record[s0 * self.step_bytes:s1 * self.step_bytes]
+
+    def rollout_bytes(self, buf: int) -> torch.Tensor:
+        """The records of the rollout in ring half ``buf`` (T step records)."""
+        return self.chunk_bytes(buf * self.T, (buf + 1) * self.T)
 
 
 def decode(records: torch.Tensor, n_shards: int, n: int, T: int, G: int, history: int, t0: int, t1: int,
@@ -112,138 +119,120 @@ class StreamFence:
 
 
 class RolloutGather:
-    """Chunked all-gather of the shards' rollout records on a side stream, each chunk decoded into the global
-    (T, N_global, 45H) observation rows right after it arrives -- while the env keeps stepping on its own stream.
+    """All-gather of the shards' rollout records, one collective per chunk of G steps (default G = T: one per
+    rollout), issued asynchronously on RCCL's own stream right after the chunk's last step, so it runs while the env
+    steps the next chunk into the other half of the recorder's ring; optionally every chunk's global
+    (T, N_global, 45H) observation rows are rebuilt right after it arrives (``h12env_rollout_decode``).
 
-    Per chunk of G steps: the compute stream records an event after the chunk's last step; the comm stream waits
-    on it, all-gathers the chunk's bytes of every shard (one ``all_gather_into_tensor``) and decodes the chunk's
-    rows.  Before the env writes a step record of the next iteration, the compute stream waits for the gather of
-    that chunk (``before_step``), so the records are double-use safe with one buffer.  world == 1: the gather is a
-    device copy (same code path, no collective)."""
+    Ordering uses the collectives' own stream semantics (torch.distributed Work): before the env rewrites a ring
+    chunk, ``before_step`` makes the compute stream wait for that chunk's previous gather (``work.wait()``, a device-side
+    wait; with the 2T ring it completed a whole rollout earlier).  world == 1: nothing to gather -- the records are
+    read in place."""
 
-    def __init__(self, rec: RolloutRecorder, world: int, G: int, tail: torch.Tensor, timing: bool = False,
-                 sync: str = "fence", decode: bool = True):
-        self.rec, self.world, self.G = rec, int(world), max(1, min(int(G), rec.T))
+    def __init__(self, rec: RolloutRecorder, world: int, G: int | None = None, tail: torch.Tensor | None = None,
+                 timing: bool = False, decode: bool = True):
+        self.rec, self.world = rec, int(world)
+        self.G = max(1, min(int(G or rec.T), rec.T))
         dev = rec.record.device
-        self.gathered = torch.empty(self.world * rec.record.numel(), dtype=torch.uint8, device=dev)
+        S = rec.step_bytes
+        self.gathered = (torch.empty(rec.nbuf * self.world * rec.T * S, dtype=torch.uint8, device=dev)
+                         if self.world > 1 else None)
         ng, row = self.world * rec.n, OBS_FRAME * rec.history
-        self.obs = torch.empty(rec.T, ng, row, device=dev)  # the decoded rollout rows handed to PPO
-        if tail.shape != (ng, row):
+        self.obs = torch.empty(rec.T, ng, row, device=dev)  # the rebuilt rows of the latest rollout
+        if tail is None or tail.shape != (ng, row):
             raise ValueError(f"tail must be ({ng}, {row})")
-        self.tail = tail.contiguous().clone()   # rows before step 0 of the first iteration (all envs)
-        self.comm = torch.cuda.Stream(device=dev)
-        self.compute = torch.cuda.current_stream(dev)  # the stream the env steps on
-        nchunks = (rec.T + self.G - 1) // self.G
-        self.done_ev = [None] * nchunks          # per chunk: gathered (the records may be rewritten)
-        self._ev = [(torch.cuda.Event(), torch.cuda.Event()) for _ in range(nchunks)]  # (ready, done), reused
-        self._last_row = self.obs[rec.T - 1]     # the next iteration's tail
-        self.prof = None                         # diagnostics: host seconds per _launch segment (dict)
-        # stream ordering: "fence" (signal-memory counters: slot 0 = chunks recorded, slot 1 = chunks gathered) or
-        # "event" (HIP events; ~100 us of host time per hand-off on this stack, tools/stream_diag.py)
-        self.sync = sync
-        self.fence = StreamFence(dev, 2) if sync == "fence" else None
-        self.seq = 0                              # chunks launched so far
-        self.chunk_seq = [0] * nchunks            # per chunk index: sequence number of its last gather
+        self.tail = tail.contiguous().clone()   # rows before step 0 of the first rollout (all envs)
+        self._last_row = self.obs[rec.T - 1]     # the next rollout's tail
+        self._work = {}                          # (ring half, chunk) -> outstanding collective
         self.timing = timing
-        self.times: list[tuple] = []             # (chunk bytes, gather event pair, decode event pair)
+        self.times: list[tuple] = []             # (gathered bytes, (start, gathered, decoded) events)
         self.iterations = 0
+        self.seq = 0                             # chunks launched so far
         # decode=False: the gathered records are the product (a PPO learner rebuilds the rows of each minibatch it
         # draws; the full (T, N_global, 45H) rebuild is then never needed)
         self.decode_off = not decode
 
     def chunk_of(self, t: int) -> tuple[int, int, int]:
+        """(chunk, first step, end step) of rollout step t."""
         c = t // self.G
         return c, c * self.G, min((c + 1) * self.G, self.rec.T)
 
-    def before_step(self):
-        """Call before env.step: the step record about to be written must have left in the previous gather."""
-        t = self.rec.t
-        c, t0, _ = self.chunk_of(t)
-        if t != t0:
-            return
-        if self.fence is not None:
-            if self.chunk_seq[c]:
-                self.fence.wait(1, self.chunk_seq[c], self.compute)
-        elif self.done_ev[c] is not None:
-            self.compute.wait_event(self.done_ev[c])
+    def records(self, buf: int) -> torch.Tensor:
+        """Every shard's records of the rollout in ring half ``buf``, chunk-major / shard / step."""
+        if self.world == 1:
+            return self.rec.rollout_bytes(buf)
+        n = self.world * self.rec.T * self.rec.step_bytes
+        return self.gathered[buf * n:(buf + 1) * n]
 
-    def after_step(self, t: int, actions=None):
-        """Call after env.step wrote step record t: at a chunk's end, gather and decode it on the comm stream.
-        actions: optional callable (t0, t1) -> None that writes the chunk's actions into rec.actions[t0:t1] (on the
-        compute stream, before the gather)."""
+    def before_step(self):
+        """Call before env.step: a chunk's ring slots are rewritten only after their previous gather."""
+        buf, t = divmod(self.rec.t, self.rec.T)
+        c, t0, _ = self.chunk_of(t)
+        if t == t0:
+            w = self._work.pop((buf, c), None)
+            if w is not None:
+                w.wait()
+
+    def after_step(self, slot: int, actions=None):
+        """Call after env.step wrote ring slot ``slot``: at a chunk's end, gather it (and rebuild its rows).
+        actions: optional callable (s0, s1) -> None writing the chunk's actions into rec.actions[s0:s1] first."""
+        buf, t = divmod(slot, self.rec.T)
         c, t0, t1 = self.chunk_of(t)
         if t + 1 != t1:
             return
-        self._launch(c, t0, t1, self.rec.T, actions)
+        self._launch(buf, c, t0, t1, self.rec.T, actions)
         if t1 == self.rec.T:
             self.iterations += 1
 
-    def flush(self, t_end: int, actions=None):
-        """Gather and decode the records of an unfinished chunk [chunk start, t_end) (end of a measurement window):
-        decoded as a rollout of t_end steps (rows [0, t_end) of self.obs)."""
-        if t_end <= 0:
-            return
-        c, t0, t1 = self.chunk_of(t_end - 1)
-        if t_end == t1:
+    def flush(self, slot_end: int, actions=None):
+        """Gather (and rebuild) an unfinished chunk ending before ring slot ``slot_end`` (the cursor after the last
+        step of a measurement window), as a rollout of that many steps."""
+        s = (slot_end - 1) % self.rec.slots
+        buf, t = divmod(s, self.rec.T)
+        c, t0, t1 = self.chunk_of(t)
+        if t + 1 == t1:
             return  # the chunk was complete (after_step gathered it)
-        self._launch(c, t0, t_end, t_end, actions)
+        self._launch(buf, c, t0, t + 1, t + 1, actions)
 
-    def _launch(self, c: int, t0: int, t1: int, T_eff: int, actions):
+    def _launch(self, buf: int, c: int, t0: int, t1: int, T_eff: int, actions):
         rec = self.rec
-        prof = self.prof
-        if prof is not None:
-            p0 = time.perf_counter()
+        T, S = rec.T, rec.step_bytes
         if actions is not None:
-            actions(t0, t1)
+            actions(buf * T + t0, buf * T + t1)
         self.seq += 1
-        seq = self.seq
-        ready, done = self._ev[c]
-        if self.fence is not None:
-            self.fence.signal(0, seq, self.compute)
-            self.fence.wait(0, seq, self.comm)
-        else:
-            ready.record(self.compute)
-            self.comm.wait_event(ready)
-        if prof is not None:
-            p1 = time.perf_counter()
-        gc = t1 - t0
-        S = rec.step_bytes
-        out = self.gathered[t0 * self.world * S:(t0 + gc) * self.world * S]
-        src = rec.record[t0 * S:t1 * S]
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if self.timing else None
-        with torch.cuda.stream(self.comm):
-            if ev:
-                ev[0].record(self.comm)
-            if self.world > 1:
-                Dist.all_gather_into_tensor(out, src)
-            else:
-                out.copy_(src)
-            if ev:
-                ev[1].record(self.comm)
-            if self.fence is not None:  # the records of this chunk may be rewritten from here on
-                self.fence.signal(1, seq, self.comm)
-                self.chunk_seq[c] = seq
-            if prof is not None:
-                p2 = time.perf_counter()
+        if ev:
+            ev[0].record()
+        work = None
+        nbytes = (t1 - t0) * S
+        if self.world > 1:
+            base = buf * self.world * T * S
+            out = self.gathered[base + t0 * self.world * S:base + t1 * self.world * S]
+            work = Dist.all_gather_into_tensor(out, rec.chunk_bytes(buf * T + t0, buf * T + t1), async_op=True)
+            nbytes *= self.world
+        if ev:  # timing pass: the compute stream waits for the gather so that the event pair brackets it
+            if work is not None:
+                work.wait()
+                work = None
+            ev[1].record()
+        if not self.decode_off:
+            if work is not None:
+                work.wait()
+                work = None
             tail = self.tail if self.iterations == 0 else self._last_row
-            if not self.decode_off:
-                decode(self.gathered, self.world, rec.n, T_eff, self.G, rec.history, t0, t1, tail,
-                       self.obs if T_eff == rec.T else self.obs[:T_eff], stream=self.comm)
-            if ev:
-                ev[2].record(self.comm)
-                self.times.append((out.numel(), ev))
-            if self.fence is None:
-                done.record(self.comm)
-        if self.fence is None:
-            self.done_ev[c] = done
-        if prof is not None:
-            p3 = time.perf_counter()
-            for k, v in (("actions+events", p1 - p0), ("gather", p2 - p1), ("decode+done", p3 - p2)):
-                prof[k] = prof.get(k, 0.0) + v
-            prof["chunks"] = prof.get("chunks", 0) + 1
+            decode(self.records(buf), self.world, rec.n, T_eff, self.G, rec.history, t0, t1, tail,
+                   self.obs if T_eff == T else self.obs[:T_eff])
+        if ev:
+            ev[2].record()
+            self.times.append((nbytes, ev))
+        if work is not None:
+            self._work[(buf, c)] = work
 
     def wait(self):
-        torch.cuda.current_stream(self.rec.record.device).wait_stream(self.comm)
+        """The compute stream waits for every outstanding gather."""
+        for w in self._work.values():
+            w.wait()
+        self._work.clear()
 
     def stats(self) -> dict:
         """Summed gather / decode milliseconds and gathered bytes of the timed chunks (synchronises)."""

@@ -1,9 +1,9 @@
 """GPU: the compact rollout records and their all-gather (BASELINE config C4; h12env.rollout, include/h12env.h
 "Rollout records").
 
-* single process (world 1, the gather is a device copy): the HIP row rebuild (h12env_rollout_decode) reproduces
+* single process (world 1: the records are read in place): the HIP row rebuild (h12env_rollout_decode) reproduces
   every observation row the env returned, bit for bit, over two whole iterations (the second one's tail aliases
-  the first one's last row) and a flushed partial chunk; Flat (history 10) and Rsl (history 6), ragged env counts
+  the first one's last row; the two halves of the recorder's ring) and a flushed partial chunk; Flat (history 10) and Rsl (history 6), ragged env counts
   (37: rows not float4-aligned) and a chunk length that does not divide T; the frames in the records are the newest
   slots of the returned rows, and the reward / done tensors the step returned are the records themselves;
 * two ranks of bench.py's N > 1 path (child processes, both on cuda:0, gloo: RCCL refuses two ranks on one device):
@@ -59,7 +59,7 @@ def test_decoded_rows_equal_env_rows(gpu, task, n):
         for t in range(steps):
             rg.before_step()
             tc = rec.t
-            assert tc == t
+            assert tc == (it % 2) * T + t  # the recorder's ring of 2T slots
             a = torch.randn(n, 12, generator=gen).to(gpu)
             obs, rew, term, trunc, _ = env.step(a)
             rec.actions[tc].copy_(a)
@@ -120,8 +120,8 @@ def test_two_rank_bench_rollout_allgather(tmp_path):
     out = json.loads(line)
     c4 = out["c4_rollout_allgather"]
     assert out["n_gpus"] == world and c4["chunks"] == 6 and c4["gather_every"] == 4
-    for k in ("env_stream_ms_per_iter", "allgather_ms_per_iter", "decode_ms_per_iter", "gathered_bytes",
-              "received_bytes_per_rank"):
+    for k in ("env_stream_ms_per_iter", "allgather_ms_per_iter", "decode_ms_per_iter", "gathered_bytes_per_iter",
+              "received_bytes_per_rank_per_iter"):
         assert c4[k] is not None and c4[k] > 0, k
     assert "all-gather" in out["config"]["parallelism"]
 

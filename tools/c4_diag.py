@@ -3,8 +3,8 @@
 
     python tools/c4_diag.py [--envs 4096] [--steps 240] [--gather-every 4]
 
-Modes: plain steps; steps recording into a bound RolloutRecorder; + the per-chunk device copy ("gather" at
-world 1); + the decode.  For each: wall ms per step after a final sync, and the host-side ms per step of the
+Modes: plain steps; steps recording into a bound RolloutRecorder; + the chunk's actions copied into the records;
++ the row rebuild (decode) per chunk.  For each: wall ms per step after a final sync, and the host-side ms per step of the
 loop alone (launch-bound if it approaches the wall time)."""
 import argparse
 import sys
@@ -43,16 +43,13 @@ def main():
         rec = rg = None
         if mode != "plain":
             rec = RolloutRecorder(n, 24, dev, 10)
-            rg = RolloutGather(rec, 1, a.gather_every, env.get_observations()["policy"].clone(),
-                               sync="event" if mode.endswith("-ev") else "fence")
+            rg = RolloutGather(rec, 1, a.gather_every, env.get_observations()["policy"].clone())
             mode_base = mode.split("-")[0]
             env.bind_rollout(rec)
             if mode_base == "record":
                 rg = None
-            elif mode_base == "copy":
+            elif mode_base == "acts":
                 rg.decode_off = True
-            if rg is not None:
-                rg.prof = {}
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
@@ -61,7 +58,10 @@ def main():
             tc = rec.t if rec is not None else 0
             env.step(acts[i % 64])
             if rg is not None:
-                rg.after_step(tc)
+                if mode.startswith("acts"):  # + the chunk's actions copied into the records (bench.py's put_actions)
+                    rg.after_step(tc, lambda s0, s1: rec.actions[s0:s1].copy_(acts[:s1 - s0]))
+                else:
+                    rg.after_step(tc)
         th = time.perf_counter() - t0
         if rg is not None:
             rg.wait()
@@ -69,12 +69,9 @@ def main():
         tw = time.perf_counter() - t0
         if rec is not None:
             env.unbind_rollout()
-        if rg is not None and rg.prof:
-            c = rg.prof.pop("chunks")
-            print("   host us per chunk:", {k: round(1e6 * v / c, 1) for k, v in rg.prof.items()}, flush=True)
         print(f"{mode:8s} wall {1e3 * tw / a.steps:.4f} ms/step   host loop {1e3 * th / a.steps:.4f} ms/step", flush=True)
 
-    for mode in ("plain", "record", "copy-ev", "copy", "decode-ev", "decode", "plain"):
+    for mode in ("plain", "record", "acts", "decode", "plain"):
         run(mode)
     # the decode kernel alone: one chunk and one whole iteration of rows, back to back
     rec = RolloutRecorder(n, 24, dev, 10)
