@@ -105,6 +105,19 @@ def load_pmc(path):
                                   f"per MI355X_MICROARCH.md; SQ_INSTS_VALU / SQ_WAVES)")
 
 
+def load_isa():
+    """tools/kernel_isa.py --json summary (physics-wave loop VALU count, registers) if it was made from the current
+    kernel source."""
+    import hashlib
+    p = ROOT / "profiles" / "latest_isa.json"
+    if not p.exists():
+        return {}, None
+    d = json.loads(p.read_text())
+    if d.get("source_sha256") != hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest():
+        return {}, f"{p.name}: stale (kernel source changed)"
+    return d, f"{p.relative_to(ROOT)} (static ISA, tools/kernel_isa.py --json)"
+
+
 def cpu_model() -> str:
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -458,15 +471,23 @@ def main():
         # 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost', one wave's stream on one SIMD), so
         # the kernel's floor is (VALU instructions per wave) x 4 cycles at the 2.4 GHz max clock
         sq = pmc.get("step_kernel", {}).get("SQ", {})
+        isa, isa_src = load_isa()
         issue = None
-        if sq.get("SQ_WAVES") and sq.get("SQ_INSTS_VALU") and args.task == "flat" and n == 4096:
-            per_wave = sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]
-            floor_ms = per_wave * 4.0 / (CLOCK_GHZ * 1e9) * 1e3
-            issue = {"bound": "valu-issue, one wave per SIMD", "valu_insts_per_wave": per_wave,
-                     "waves": sq["SQ_WAVES"], "simds_in_use_frac": sq["SQ_WAVES"] / N_SIMD,
-                     "floor_ms": floor_ms, "frac": floor_ms / kern_ms_avg,
-                     "wait_frac": sq.get("SQ_WAIT_ANY", 0.0) / sq.get("SQ_WAVE_CYCLES", 1.0),
-                     "source": pmc_src}
+        if isa and args.task == "flat" and n == 4096 and not (args.no_self_collision or args.decimation
+                                                                or args.inner_steps or args.explicit_penalty):
+            # the step time is the PHYSICS wave's serial chain (the helper / self-contact waves of a block finish
+            # inside its window): its physics-step loop runs decimation x inner_steps times per env step
+            # (tools/kernel_isa.py --json, static ISA of this kernel source); the loads / rewards / reset / stores
+            # around the loop are not counted, so the floor is a lower bound
+            per_step = isa["physics_step_loop"]["valu"] * cfg.decimation * cfg.sim.inner_steps
+            floor_ms = per_step * 4.0 / (CLOCK_GHZ * 1e9) * 1e3
+            issue = {"bound": "valu-issue, one wave per SIMD (the physics wave's chain)",
+                     "physics_wave_loop_valu_per_env_step": per_step,
+                     "floor_ms": floor_ms, "frac": floor_ms / kern_ms_avg, "isa_source": isa_src}
+            if sq.get("SQ_WAVES") and sq.get("SQ_INSTS_VALU"):  # PMC: all three waves of every block averaged
+                issue.update(pmc_valu_insts_per_wave_all_roles=sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"],
+                             waves=sq["SQ_WAVES"], simds_in_use_frac=sq["SQ_WAVES"] / N_SIMD,
+                             wait_frac=sq.get("SQ_WAIT_ANY", 0.0) / sq.get("SQ_WAVE_CYCLES", 1.0), pmc_source=pmc_src)
         metric, workload = METRIC, "Isaac-Velocity-Flat-H12_12dof-v0 random-action rollout, 4096 envs per MI355X"
         if args.task in ("rsl", "cat"):
             tid = {"rsl": "Rsl-H12_12dof", "cat": "CaT-Flat-H12_12dof"}[args.task]

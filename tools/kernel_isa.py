@@ -2,7 +2,7 @@
 """Static ISA report of libh12env's kernels (gfx950): register allocation from the code-object metadata and
 instruction counts from the compiler's own assembly.
 
-    python tools/kernel_isa.py [kernel-name-substring ...]
+    python tools/kernel_isa.py [kernel-name-substring ...] [--json profiles/latest_isa.json]
 
 Builds csrc/h12env.hip with -save-temps into a temp dir (same flags as h12env.build), then for each kernel
 prints .vgpr_count / .agpr_count / .sgpr_count / scratch, the instruction mix (VALU, v_accvgpr moves, SALU,
@@ -81,11 +81,43 @@ def report(text: str, name: str) -> dict:
     return r
 
 
+def physics_wave_json(text: str, meta: dict, out: Path) -> None:
+    """profiles/latest_isa.json for bench.py's issue roofline: the Flat step_kernel's register allocation and the
+    VALU count of its physics wave's physics-step loop (the largest loop: the physics wave's chain; the helper and
+    self-contact waves run other, shorter loops), keyed by the kernel source's sha256 like latest_pmc.json."""
+    import hashlib
+    import json
+
+    name = next(k for k in meta if "step_kernelILi0E" in k)
+    g, r = meta[name], report(text, name)
+    top = max(r["loops"], key=lambda x: x[2])
+    res = {"source_sha256": hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest(),
+           "kernel": name,
+           "registers": {"vgpr_count_total": g.get("vgpr_count"), "agpr_count": g.get("agpr_count"),
+                         "arch_vgpr": (g.get("vgpr_count") or 0) - (g.get("agpr_count") or 0),
+                         "sgpr_count": g.get("sgpr_count"), "scratch_bytes": g.get("private_segment_fixed_size"),
+                         "note": "gfx950 unified file: .vgpr_count is arch + acc registers; rocprofv3's VGPR_Count "
+                                 "column decodes the descriptor's granulated field with a granule of 4 instead of 8 "
+                                 "(half the allocated count)"},
+           "physics_step_loop": {"label": top[0], "instructions": top[1], "valu": top[2], "v_accvgpr": top[3]},
+           "valu_total_static": r["valu"]}
+    out.write_text(json.dumps(res, indent=1) + "\n")
+    print("wrote", out)
+
+
 def main():
-    subs = sys.argv[1:] or ["step_kernelILi0E", "obs_assemble_kernelILi10E"]
+    args = sys.argv[1:]
+    js = None
+    if "--json" in args:
+        i = args.index("--json")
+        js = Path(args[i + 1])
+        del args[i:i + 2]
+    subs = args or ["step_kernelILi0E", "obs_assemble_kernelILi10E"]
     with tempfile.TemporaryDirectory() as td:
         text = build_asm(Path(td)).read_text()
     meta = metadata(text)
+    if js is not None:
+        physics_wave_json(text, meta, js)
     for name, g in sorted(meta.items()):
         if not any(s in name for s in subs):
             continue
