@@ -1221,7 +1221,11 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
 // range of envs -- each XCD's state loads / stores are contiguous runs of every field instead of 128-B chunks
 // 1 KB apart (the round-robin order put the tail of the waves on some XCDs 2 us behind the others)
 H12_DEV int xcd_block(int b, int nb);
+#ifdef H12_EXP_PLAIN_MAP  // experiment builds only: env chunk = block index (chunks interleaved over the XCDs)
+H12_DEV int step_block() { return blockIdx.x; }
+#else
 H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
+#endif
 
 template <int K>
 H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi) {
@@ -1375,6 +1379,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   PHX(10);
   if constexpr (HW) {
     __syncthreads();  // R1
+    PHX(8);
     float jt[36];
     get4(help_lds().jt, threadIdx.x, jt, 9);
     // tq includes the delayed PD (computed by the helper wave); tau_pd receives the PD torque alone
@@ -1397,7 +1402,6 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   link_ia<2>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
   link_ia<1>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
   link_ia<0>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
-  PHX(12);
   // ---- the contact-independent forces: bias forces, self-contact wrenches (helper wave)
   if constexpr (HW) {  // the inertia chain stays ahead of R2 (else the compiler sinks most of it past the barrier)
     for (int i = 0; i < 6; ++i) { pin(IA.A[i]); pin(IA.C[i]); }
@@ -1406,11 +1410,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     for (int k = 0; k < NL; ++k)
       for (int i = 0; i < 6; ++i) pin(Ic[k][i]);
   }
+  PHX(12);
   float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float pbase[6];  // base body bias force (lane 0; 0 on lane 1)
   AInertia Rg;     // base body inertia (lane 0)
   if constexpr (HW) {
     __syncthreads();  // R2
+    PHX(9);
     float o[44];
     get4(help_lds().bias, threadIdx.x, o, 11);
     for (int k = 0; k < NL; ++k)
@@ -2567,7 +2573,9 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
           const HelpLds& H = help_lds();
           float acc = 0.f;
           for (int j = 0; j < ne; ++j) acc += H.logv[v][j];
+#ifndef H12_EXP_NO_LOG_ATOMICS  // experiment builds only: the per-block episode-log partials dropped
           if (acc != 0.f) atomicAdd(A.log_part + (size_t)v * gridDim.x + blockIdx.x, acc);
+#endif
         }
       }
     } else {

@@ -8,9 +8,9 @@ The variant library records, per main (physics) wave and lane 0, the cycles betw
 csrc/h12env.hip into 16 global counters (h12env_phase_profile); printed here as cycles per wave and env
 step.  Slots: 0 state loads, 1 physics loop, 2 contact-sensor replay, 3 rewards / terminations, 4 outputs +
 episode log, 5 reset + commands + events, 6 observation frame, 7 state stores; inside each inner step
-(summed over the step's inner steps): 10 pass 1 and the ground contacts, 11 the wait for the helper wave's
-joint terms, 12 the articulated-inertia chain, 13 the wait for its bias forces / self-contact wrenches, 14 the
-rest (bias-force chain, base solve, pass 3, integration, next state to the helper).  The marks' own atomics add a few hundred cycles per step.  Not the product
+(summed over the step's inner steps): 10 pass 1 and the ground contacts, 8 the barrier R1 itself, 11 reading the
+helper wave's joint terms, 12 the articulated-inertia chain, 9 the barrier R2 itself, 13 reading its bias forces /
+self-contact wrenches, 14 the rest (bias-force chain, base solve, pass 3, integration, next state to the helper).  The marks' own atomics add a few hundred cycles per step.  Not the product
 library: the variant is loaded through H12ENV_LIB and never built by __graft_entry__.
 """
 from __future__ import annotations
@@ -27,8 +27,10 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 VARIANTS = ROOT / "tools" / "_variants"
 SLOTS = {0: "loads", 1: "physics", 2: "sensor", 3: "rewards", 4: "outputs+log", 5: "reset+cmd", 6: "frame",
-         7: "stores", 10: "inner: pass 1 + ground contacts", 11: "inner: wait R1 (joint terms)",
-         12: "inner: inertia chain", 13: "inner: wait R2 (bias, self-contacts)", 14: "inner: bias chain .. integration + S"}
+         7: "stores", 10: "inner: pass 1 + ground contacts", 8: "inner: barrier R1 (waiting for the helpers)",
+         11: "inner: joint terms from LDS", 12: "inner: inertia chain (pinned ahead of R2)",
+         9: "inner: barrier R2 (waiting for the helpers)", 13: "inner: bias forces / self wrenches from LDS",
+         14: "inner: bias chain .. integration + S"}
 
 
 def build(tag: str, flags: list[str], plain: bool = False) -> Path:
