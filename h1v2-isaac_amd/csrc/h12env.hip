@@ -63,7 +63,7 @@ template <int K> struct Feat {
 // over waves (lane 0), read back with h12env_phase_profile.  Not part of the product library.
 #ifdef H12_PHASE_PROFILE
 __device__ unsigned long long g_phase[16];
-__device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, [4]: after reset + command, [5]: spare  // per physics wave of the last launch: realtime start, end, end after waitcnt
+__device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, [4]: after reset + command, [5]: XCC id  // per physics wave of the last launch: realtime start, end, end after waitcnt
 #define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter(); \
   const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime()
 #define PH_WAVE_END()                                                          \
@@ -71,8 +71,11 @@ __device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, 
     const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();           \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
     const unsigned long long _r2 = __builtin_amdgcn_s_memrealtime();           \
+    unsigned _xcc;                                                             \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));        \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                        \
       g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
+      g_wave[blockIdx.x][5] = _xcc & 15u;                                      \
     }                                                                          \
   } while (0)
 #define PH(i)                                                                       \

@@ -89,8 +89,10 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             env.step(acts[t])
             torch.cuda.synchronize()
             lib.h12env_wave_times(wt, waves)
-            a = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 6).astype(np.int64)[:, :5]
+            full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 6).astype(np.int64)
+            a = full[:, :5].copy()
             a -= a[:, 0].min()
+            a = np.concatenate([a, full[:, 5:6]], axis=1)  # column 5: the wave's XCC id (s_getreg HW_REG_XCC_ID)
             raw.append(a.copy())
             rs = (env.reset_terminated | env.reset_time_outs).view(-1, 32).sum(1).cpu().numpy()
             rsets.append(rs)
