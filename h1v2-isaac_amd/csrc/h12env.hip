@@ -2052,6 +2052,9 @@ H12_DEV void cmd_metrics(const KParams& P, EnvSt& s) {
 // first (48 rows), then base position (3) and yaw cos / sin (2) for the height scan.
 template <int K>
 H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, float* frame) {
+#ifdef H12_EXP_NO_FRAME  // experiment builds only: the frame is not written (timing of the store tail)
+  return;
+#endif
   const float sg = leg ? -1.f : 1.f;
   const int o = (Feat<K>::ext && P.task == H12_TASK_ROUGH) ? 3 : 0;
   if (leg == 0) {
