@@ -84,6 +84,9 @@ def parse():
     p.add_argument("--rollout-decode", action="store_true",
                    help="C4: also rebuild the global (T, N_global, 450) observation rows on every rank after each "
                         "gathered chunk (off: the gathered records are handed over; a learner rebuilds its minibatch rows)")
+    p.add_argument("--force-collective", action="store_true",
+                   help="test hook: with --rollout on, issue the rollout all-gather even on one rank (a one-rank "
+                        "process group, launched by torch.distributed.run): exercises the RCCL code path on one GPU")
     p.add_argument("--dump-rollout", type=str, default=None,
                    help="test hook: rank 0 saves the decoded rows and the gathered records of the timed window (.npz)")
     return p.parse_args()
@@ -267,7 +270,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
-    if world > 1:
+    if world > 1 or args.force_collective:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -337,7 +340,8 @@ def main():
             tail.copy_(env.get_observations()["policy"])
         # no timing events inside the timed window (each event record costs host time comparable to a step); the
         # all-gather / decode split is measured in an untimed pass right after it
-        rg = RolloutGather(rec, world, args.gather_every, tail, timing=False, decode=args.rollout_decode)
+        rg = RolloutGather(rec, world, args.gather_every, tail, timing=False, decode=args.rollout_decode,
+                           collective=args.force_collective)
         pool_off = B + W  # actions[pool_off + i] is the action of timed step i
         env.bind_rollout(rec)
 
@@ -353,11 +357,14 @@ def main():
                     rec.actions[s0 + k:s1].copy_(actions[:span - k])
             return f
 
+    snap = env.snapshot()  # replayed below (reset count + kernel timing of the same window); copied before the barrier
     barrier()
-    snap = env.snapshot()  # replayed below (reset count + kernel timing of the same window)
-    ev_c = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    # the env-stream span of the rollout path (C4 split); no event records in the plain timed window (each costs
+    # host time, which a 20-step window does not amortise)
+    ev_c = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] if rg is not None else None
     t0 = time.perf_counter()
-    ev_c[0].record()
+    if ev_c:
+        ev_c[0].record()
     for i in range(K):
         if rg is None:
             env.step(actions[(B + W + i) % pool])
@@ -368,7 +375,8 @@ def main():
         rg.after_step(tc, put_actions(pool_off + i + 1))
     if rg is not None and K > 0:
         rg.flush(rec.t, put_actions(pool_off + K))
-    ev_c[1].record()
+    if ev_c:
+        ev_c[1].record()
     if rg is not None:
         rg.wait()
     barrier()
@@ -425,7 +433,7 @@ def main():
                          "with the next rollout's env steps into the other half of a 2T-record ring; the split above "
                          "comes from an untimed pass that serialises each gather between an event pair",
               "backend": (args.dist_backend if world > 1 else "none (N = 1: the records are read in place)")}
-        if world == 1:  # nothing is gathered: no all-gather time or bandwidth to report
+        if not rg.coll:  # nothing is gathered: no all-gather time or bandwidth to report
             c4.update(allgather_ms_per_iter=None, allgather_algbw_gbs=None, gathered_bytes_per_iter=0)
         env.unbind_rollout()
     if args.profile_only:
@@ -562,7 +570,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if world > 1 or args.force_collective:
         dist.barrier()
         dist.destroy_process_group()
 

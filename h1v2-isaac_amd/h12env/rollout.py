@@ -130,13 +130,15 @@ class RolloutGather:
     read in place."""
 
     def __init__(self, rec: RolloutRecorder, world: int, G: int | None = None, tail: torch.Tensor | None = None,
-                 timing: bool = False, decode: bool = True):
+                 timing: bool = False, decode: bool = True, collective: bool = False):
         self.rec, self.world = rec, int(world)
+        # collective: issue the all-gather even at world 1 (a one-rank process group; exercises the RCCL path)
+        self.coll = self.world > 1 or collective
         self.G = max(1, min(int(G or rec.T), rec.T))
         dev = rec.record.device
         S = rec.step_bytes
         self.gathered = (torch.empty(rec.nbuf * self.world * rec.T * S, dtype=torch.uint8, device=dev)
-                         if self.world > 1 else None)
+                         if self.coll else None)
         ng, row = self.world * rec.n, OBS_FRAME * rec.history
         self.obs = torch.empty(rec.T, ng, row, device=dev)  # the rebuilt rows of the latest rollout
         if tail is None or tail.shape != (ng, row):
@@ -159,7 +161,7 @@ class RolloutGather:
 
     def records(self, buf: int) -> torch.Tensor:
         """Every shard's records of the rollout in ring half ``buf``, chunk-major / shard / step."""
-        if self.world == 1:
+        if not self.coll:
             return self.rec.rollout_bytes(buf)
         n = self.world * self.rec.T * self.rec.step_bytes
         return self.gathered[buf * n:(buf + 1) * n]
@@ -205,7 +207,7 @@ class RolloutGather:
             ev[0].record()
         work = None
         nbytes = (t1 - t0) * S
-        if self.world > 1:
+        if self.coll:
             base = buf * self.world * T * S
             out = self.gathered[base + t0 * self.world * S:base + t1 * self.world * S]
             work = Dist.all_gather_into_tensor(out, rec.chunk_bytes(buf * T + t0, buf * T + t1), async_op=True)
