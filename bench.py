@@ -432,7 +432,7 @@ def main():
               "overlap": "one asynchronous RCCL all-gather per chunk (default: per rollout) on RCCL's stream, concurrent "
                          "with the next rollout's env steps into the other half of a 2T-record ring; the split above "
                          "comes from an untimed pass that serialises each gather between an event pair",
-              "backend": (args.dist_backend if world > 1 else "none (N = 1: the records are read in place)")}
+              "backend": (args.dist_backend if rg.coll else "none (N = 1: the records are read in place)")}
         if not rg.coll:  # nothing is gathered: no all-gather time or bandwidth to report
             c4.update(allgather_ms_per_iter=None, allgather_algbw_gbs=None, gathered_bytes_per_iter=0)
         env.unbind_rollout()

@@ -168,3 +168,29 @@ def test_two_rank_bench_rollout_allgather(tmp_path):
     np.testing.assert_array_equal(decode_ref(g["frames"], done, d["tail"], 10), d["obs"])
     assert done.any()
     env.close()
+
+
+@pytest.mark.timeout(400)
+def test_rccl_rollout_allgather_one_rank(tmp_path):
+    """The RCCL code path of the rollout all-gather (asynchronous all_gather_into_tensor on RCCL's stream, work.wait
+    before a ring half is rewritten), on a one-rank NCCL process group (bench.py --force-collective): the 8-GPU run
+    is the driver's, this keeps the same calls exercised on one GPU.  The line must carry the split, the window must
+    replay bit-exactly, and the gathered records of the first rollout must rebuild the rows the env returned."""
+    port = _free_port()
+    dump = tmp_path / "rollout.npz"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "1", "--rollout", "on",
+           "--force-collective", "--envs", "64", "--steps", "30", "--warmup", "3", "--burn-in", "20",
+           "--gather-every", "8", "--no-cpu-baseline", "--dump-rollout", str(dump)]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, env=env, cwd=str(ROOT), capture_output=True, text=True, timeout=360)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c4 = out["c4_rollout_allgather"]
+    assert out["replay_bit_exact"] and c4["backend"] == "nccl"
+    assert c4["allgather_ms_per_iter"] is not None and c4["allgather_ms_per_iter"] > 0
+    assert c4["gathered_bytes_per_iter"] > 0 and c4["chunks"] == 4
+    d = np.load(dump)
+    g = unpack(d["gathered"], 1, 64, int(d["T"]), int(d["G"]), list(d["off"]), int(d["step_bytes"]))
+    done = g["terminated"] | g["truncated"]
+    np.testing.assert_array_equal(decode_ref(g["frames"], done, d["tail"], 10), d["obs"])
