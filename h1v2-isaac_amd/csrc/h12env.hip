@@ -1035,6 +1035,78 @@ H12_DEV HelpLds& help_lds() {
   __shared__ HelpLds H;
   return H;
 }
+#ifndef H12_OBS_POL
+#define H12_OBS_POL 0  // cache policy bits of the observation-row stores (buffer store aux: 1 sc0, 2 nt, 16 sc1)
+#endif
+// one float4 of an observation row (16-byte aligned rows) at float4 index j of dst
+H12_DEV void st_row4(float* dst, int j, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
+                                         H12_OBS_POL);
+}
+// ---- Fused observation assembly (step path; Flat / Rsl history layouts without CaT: StepArgs.fuse).  The rows
+// obs_assemble_kernel would write are stored by step_kernel's helper waves instead, mostly while the physics wave
+// integrates: a row is 90 % shifted history (obs[e, slot h] = obs_prev[e, slot h + 1]), which this step's physics
+// does not change.  After the first physics step's R2 barrier the helper waves LDS-DMA the block's 32 rows of
+// obs_prev (drained before the next R2); after each later R2 -- the physics wave's pass 2 / 3 and integration, where
+// they would idle -- each lane stores its share of the shifted rows as float4s (fuse_early).  At the end of the step
+// only the newest slot (45 floats per row, the noisy scaled frame the physics wave leaves in LDS), the rows of
+// resetting envs (the frame in every slot) and frame_out are written (fuse_late, after barrier F).  Spreading the
+// 57.6 KB per block over the physics loop matters: the same stores issued after the loop cost ~6.6 us per step
+// (128 CUs at ~9 GB/s each), more than the separate kernel over all 256 CUs.  Bit-identical to the two-kernel path:
+// the same copies and the same float operations.
+constexpr int FUSE_ROWS = ENVS_PER_BLOCK;
+struct FuseLds {
+  float hist[FUSE_ROWS * H12_OBS_FRAME * (H12_NHIST + 1)];  // the rows (45 hist floats each), then frames [row][45]
+  float noise[FUSE_ROWS][33];  // noise values of the row's 30 noisy components (padded row: conflict-free)
+  int fill[FUSE_ROWS];         // the row restarts its history (terminated | truncated)
+};
+extern __shared__ float4 h12_dyn_lds[];
+H12_DEV FuseLds& fuse_lds() { return *reinterpret_cast<FuseLds*>(h12_dyn_lds); }
+struct FuseCtx {
+  const float* src;  // the block's first row of obs_prev
+  float* dst;        // ... of obs
+  int row;           // floats per row (45 x history)
+  int on;            // whole block, 16-byte aligned, >= 2 physics steps: the spread path; else fuse_late alone
+};
+// helper-wave lane t of nt, after the R2 barrier of inner step it (n_steps in the env step)
+H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
+  if (!f.on) return;
+  FuseLds& F = fuse_lds();
+  const int f4 = FUSE_ROWS * f.row / 4;
+  if (it == 0) {  // rows -> LDS: 1 KB LDS-DMA chunks, drained before the next R2 (fuse_drain)
+    const int w = t >> 6, lane = t & 63, nw = nt >> 6, nch = (f4 + 63) / 64;
+    for (int ch = w; ch < nch; ch += nw)
+      if (ch * 64 + lane < f4)
+        __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(F.hist + ch * 256), 16, 0, 0);
+    return;
+  }
+  // this lane's float4s j = t + k nt, k in its share of the remaining inner steps; every float gets the next-newer
+  // slot (+3 in the 3-wide terms, +12 in the 12-wide ones); the newest slot's floats get a placeholder that
+  // fuse_late overwrites (same block, after barrier F: every early store has completed by then)
+  const int kmax = (f4 + nt - 1) / nt;
+  const int k0 = (it - 1) * kmax / (n_steps - 1), k1 = it * kmax / (n_steps - 1);
+  const int h9 = f.row / 5;  // 9 x history: the 3-wide terms' columns
+  const uint32_t mrow = 0xFFFFFFFFu / (uint32_t)f.row + 1u;  // p / row = umulhi(p, mrow) for p < 2^16
+  for (int k = k0; k < k1; ++k) {
+    const int j = t + k * nt;
+    if (j >= f4) break;
+    const int p0 = 4 * j, col0 = p0 - (int)__umulhi((uint32_t)p0, mrow) * f.row;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = col0 + q - (col0 + q >= f.row ? f.row : 0);
+      v[q] = F.hist[p0 + q + (col < h9 ? 3 : 12)];
+    }
+    st_row4(f.dst, j, make_float4(v[0], v[1], v[2], v[3]));
+  }
+}
+// before the R2 barrier of inner step 1: this wave's LDS-DMA has landed (the other waves' reads follow R2)
+H12_DEV void fuse_drain(const FuseCtx& f, int it) {
+  if (f.on && it == 1) __builtin_amdgcn_s_waitcnt(0);
+}
+
 // CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the joint-term
 // hand-off array (free once the last inner step has read it; the LDS footprint stays the three-wave block's)
 typedef float CatLds[H12_NCSTR_COLS + 1][ENVS_PER_BLOCK];
@@ -1231,7 +1303,7 @@ H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
 #endif
 
 template <int K>
-H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi) {
+H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi, const FuseCtx& fc) {
   const int l = threadIdx.x - BLOCK;
   const int leg = l & 1;
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
@@ -1298,12 +1370,14 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
       }
       put4(H.torso, l, t, 4);
     }
+    fuse_drain(fc, it);
     __syncthreads();  // R2: bias forces, torso contact
+    fuse_early(fc, it, n_steps, l, blockDim.x - BLOCK);
   }
 }
 
 template <int K>
-H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
+H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) {
   const int l = threadIdx.x - 2 * BLOCK;
   const int leg = l & 1;
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
@@ -1328,7 +1402,9 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps) {
       self_finish(P, leg, act, Rk, pk, R, p, w, w + 6, fr);
       put4(H.selfw, l, w, 3);
     }
+    fuse_drain(fc, it);
     __syncthreads();  // R2: self-contact wrenches
+    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, blockDim.x - BLOCK);
   }
 }
 
@@ -2200,22 +2276,23 @@ H12_DEV bool asm_row_written(const AsmArgs& A, int e, bool& fill) {
 // column table entry of row-local column col of a 45 x NH row (term-major blocks of 3NH, 3NH, 3NH, 12NH,
 // 12NH, 12NH floats, oldest slot first): frame component c (bits 0-7), history shift d (bits 8-15),
 // newest-slot flag (bit 16)
-template <int NH>
-H12_DEV uint32_t asm_col_entry(int col) {
+H12_DEV uint32_t hist_col_entry(int col, int nh) {
   int c, hh, d;
-  if (col < 9 * NH) {
-    int t = col / (3 * NH), r = col - 3 * NH * t;
+  if (col < 9 * nh) {
+    int t = col / (3 * nh), r = col - 3 * nh * t;
     hh = r / 3;
     c = 3 * t + (r - 3 * hh);
     d = 3;
   } else {
-    int k = col - 9 * NH, t = k / (12 * NH), r = k - 12 * NH * t;
+    int k = col - 9 * nh, t = k / (12 * nh), r = k - 12 * nh * t;
     hh = r / 12;
     c = 9 + 12 * t + (r - 12 * hh);
     d = 12;
   }
-  return (uint32_t)c | ((uint32_t)d << 8) | (hh == NH - 1 ? (1u << 16) : 0u);
+  return (uint32_t)c | ((uint32_t)d << 8) | (hh == nh - 1 ? (1u << 16) : 0u);
 }
+template <int NH>
+H12_DEV uint32_t asm_col_entry(int col) { return hist_col_entry(col, NH); }
 
 // NH: history length (10 Flat, 6 Rsl); the row is 45 * NH floats
 template <int NH>
@@ -2328,8 +2405,8 @@ H12_DEV void obs_assemble_body(const KParams& P, const AsmArgs& A) {
       if (j < ASM_F4) {
         const float* pb = s_hist + 4 * j;
         const uint2 t = gt[u];
-        reinterpret_cast<float4*>(dst)[j] = make_float4(pb[0 + (int)(int16_t)(t.x & 0xFFFFu)], pb[1 + ((int)t.x >> 16)],
-                                                        pb[2 + (int)(int16_t)(t.y & 0xFFFFu)], pb[3 + ((int)t.y >> 16)]);
+        st_row4(dst, j, make_float4(pb[0 + (int)(int16_t)(t.x & 0xFFFFu)], pb[1 + ((int)t.x >> 16)],
+                                    pb[2 + (int)(int16_t)(t.y & 0xFFFFu)], pb[3 + ((int)t.y >> 16)]));
       }
     }
     return;
@@ -2359,6 +2436,27 @@ H12_DEV void obs_assemble_body(const KParams& P, const AsmArgs& A) {
       if (s_write[row]) dst[pp] = value(row, col);
     }
   }
+}
+// Deferred episode-log folds (fused step path): block (v, k) folds value v of pending step k -- the same per-lane
+// sums and shuffle tree as log_load / log_fold_one, so the accumulators are bit-identical to the immediate fold.
+// One block per (value, step) and no two pending steps share an accumulator (h12env_step flushes first), so every
+// accumulator word has one writer.
+constexpr int LOG_RING = 64;  // partial sets (steps) the handle holds; a full ring is folded by the next step
+struct FoldArgs {
+  float* part;  // the handle's ring: [LOG_RING][LOG_NPART][nb]
+  int nb;
+  int slot[LOG_RING];
+  float* acc[LOG_RING];
+};
+__global__ void __launch_bounds__(64) log_flush_kernel(FoldArgs F) {
+  const int v = blockIdx.x, k = blockIdx.y;
+  float* q = F.part + ((size_t)F.slot[k] * LOG_NPART + v) * F.nb;
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < F.nb; b += 64) acc += q[b];
+  for (int b = threadIdx.x; b < F.nb; b += 64) q[b] = 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (threadIdx.x == 0 && acc != 0.f) F.acc[k][log_slot(v)] += acc;
 }
 template <int NH>
 __global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
@@ -2540,15 +2638,105 @@ struct StepArgs {
   uint32_t lo, hi;
   int n_substeps;
   int dz_slot;  // deadzone counter read this step (P.dz_cnt[dz_slot]); +1 is counted into, +2 zeroed
+  int fuse;     // the observation rows are assembled inside step_kernel (FuseCtx; dynamic LDS)
+  float* frame_out;         // (n, 45) noisy scaled frames as they enter the history (fused path), or null
 };
+
+// helper waves (lane t of nt), before barrier L: the rows' noise blocks (and, off the spread path, the rows -> LDS)
+H12_DEV void fuse_stage(const KParams& P, const StepArgs& A, const FuseCtx& fc, int n, int t, int nt) {
+  FuseLds& F = fuse_lds();
+  const int e0 = step_block() * FUSE_ROWS, ne = min(FUSE_ROWS, n - e0);
+  if (!fc.on)
+    for (int j = t; j < ne * fc.row; j += nt) F.hist[j] = fc.src[j];  // plain copies (ragged block / 1 physics step)
+  for (int w = t; w < 8 * ne; w += nt) {
+    const int r = w >> 3, blk = w & 7;
+    uint32_t q[4];
+    philox(P.seed_lo, P.seed_hi, (uint32_t)(A.env_offset + e0 + r), A.lo, ((uint32_t)ST_OBS << 16) | (uint32_t)blk,
+           A.hi, q);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      if (4 * blk + a < 30) F.noise[r][4 * blk + a] = noise_of(P, 4 * blk + a, q[a]);
+  }
+}
+
+// column of frame component c's newest slot in a row of history nh (term-major blocks, oldest slot first)
+H12_DEV int newest_col(int c, int nh) {
+  if (c < 9) return (c / 3) * 3 * nh + 3 * (nh - 1) + c % 3;
+  const int k = c - 9;
+  return 9 * nh + (k / 12) * 12 * nh + 12 * (nh - 1) + k % 12;
+}
+
+// helper waves, after barrier F: the newest slots, the refilled rows and frame_out (spread path), or whole rows
+H12_DEV void fuse_late(const KParams& P, const StepArgs& A, const FuseCtx& fc, int n, int t, int nt) {
+  const FuseLds& F = fuse_lds();
+  const int e0 = step_block() * FUSE_ROWS, ne = min(FUSE_ROWS, n - e0);
+  const int row = fc.row, nh = P.hist;
+  const float* fr = F.hist + FUSE_ROWS * row;
+  if (A.frame_out)  // the block's frames are one contiguous run of ne x 45 floats
+    for (int k = t; k < ne * H12_OBS_FRAME; k += nt) A.frame_out[(size_t)e0 * H12_OBS_FRAME + k] = fr[k];
+  if (fc.on) {
+    for (int w = t; w < FUSE_ROWS * H12_OBS_FRAME; w += nt) {
+      const int r = w / H12_OBS_FRAME, c = w - r * H12_OBS_FRAME;
+      fc.dst[r * row + newest_col(c, nh)] = fr[w];
+    }
+    // a resetting env's row restarts its history: the frame in every slot
+    uint32_t fm = (uint32_t)__ballot(F.fill[threadIdx.x & (FUSE_ROWS - 1)] != 0);  // wave-uniform
+    while (fm) {
+      const int r = __builtin_ctz(fm);
+      fm &= fm - 1u;
+      for (int col = t; col < row; col += nt)
+        fc.dst[r * row + col] = fr[H12_OBS_FRAME * r + (int)(hist_col_entry(col, nh) & 0xFFu)];
+    }
+    return;
+  }
+  for (int p = t; p < ne * row; p += nt) {
+    const int r = p / row, col = p - r * row;
+    const uint32_t te = hist_col_entry(col, nh);
+    fc.dst[p] = (F.fill[r] || (te >> 16)) ? fr[H12_OBS_FRAME * r + (int)(te & 0xFFu)] : F.hist[p + (int)((te >> 8) & 0xFFu)];
+  }
+}
+
+// physics wave, fused path: obs_frame's values (Flat layout) with the noise (drawn by fuse_stage) and the term
+// scale applied as obs_assemble_body does, into the block's LDS frame row r; and the row's refill flag
+H12_DEV void obs_frame_fused(const KParams& P, const EnvSt& s, int leg, int r, bool fill) {
+  FuseLds& F = fuse_lds();
+  float* fr = F.hist + FUSE_ROWS * H12_OBS_FRAME * P.hist + H12_OBS_FRAME * r;
+  const float* nz = F.noise[r];
+  const float sg = leg ? -1.f : 1.f;
+  if (leg == 0) {
+    float R[3][3];
+    quat_R(s.b.quat, R);
+    for (int a = 0; a < 3; ++a) fr[a] = (s.b.wang[a] + nz[a]) * P.oscale[0];
+    for (int a = 0; a < 3; ++a) fr[3 + a] = (-R[2][a] + nz[3 + a]) * P.oscale[1];
+    for (int a = 0; a < 3; ++a) fr[6 + a] = s.cmd[a] * P.oscale[2];
+    F.fill[r] = fill ? 1 : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int j = NL * leg + k;
+    const float js = jsign(k, sg);
+    fr[9 + j] = (js * (s.lg.q[k] - h12m::Q0[k]) + nz[6 + j]) * P.oscale[3];
+    fr[21 + j] = (js * s.lg.qd[k] + nz[18 + j]) * P.oscale[4];
+    fr[33 + j] = js * s.act[k] * P.oscale[5];
+  }
+}
 
 template <int K>
 __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
+    const int nsteps = P.decimation * P.inner;
+    FuseCtx fc = {};
+    if (A.fuse) {
+      const int e0 = step_block() * ENVS_PER_BLOCK, row = H12_OBS_FRAME * P.hist;
+      fc = {A.obs_prev + (size_t)e0 * row, A.obs + (size_t)e0 * row, row, e0 + ENVS_PER_BLOCK <= W.n && nsteps >= 2};
+    }
+    const int ft = threadIdx.x - BLOCK, fnt = blockDim.x - BLOCK;  // lane among the helper waves
     if (threadIdx.x < 2 * BLOCK) {
-      helper_wave<K>(P, W.n, P.decimation * P.inner,
-                     (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi);
-      if (A.log_part || (Feat<K>::ext && P.cat)) {
+      helper_wave<K>(P, W.n, nsteps,
+                     (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi,
+                     fc);
+      if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
+      if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) {
         __syncthreads();  // L: the physics wave's episode-log values (and CaT constraint values)
         if (Feat<K>::ext && P.cat) {
           // CaT: this block's column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs
@@ -2584,9 +2772,20 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
 #endif
         }
       }
+      if (A.fuse) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's shifted-row stores have completed (fuse_late rewrites some)
+        __syncthreads();                // F: the physics wave's noisy frames and refill flags
+        fuse_late(P, A, fc, W.n, ft, fnt);
+      }
     } else {
-      self_wave<K>(P, W.n, P.decimation * P.inner);
-      if (A.log_part || (Feat<K>::ext && P.cat)) __syncthreads();  // L
+      self_wave<K>(P, W.n, nsteps, fc);
+      if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
+      if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) __syncthreads();  // L
+      if (A.fuse) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();  // F
+        fuse_late(P, A, fc, W.n, ft, fnt);
+      }
     }
     return;
   }
@@ -2699,7 +2898,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     // the same L2 lines: +4.2 us per step).  In this wave the wave-reduced atomics cost a resetting wave ~0.5 us,
     // and the step time is the slowest wave's.  The assembly kernel that follows folds the partials into log_acc
     // (log_load / log_fold).
-    if (A.log_part || (Feat<K>::ext && P.cat)) {
+    if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) {
       if (A.log_part && leg == 0) {
         float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
         for (int t = 0; t < NT; ++t) L[t][lane_pair] = reset ? s.epsum[t] : 0.f;
@@ -2738,7 +2937,12 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     push_event<K>(P, s, g, A.lo, A.hi);
     // ---- observation frame (after reset: ObservationManager.compute, cat_env.py:190)
     PH(5);
-    obs_frame<K>(P, s, leg, e, W.n, A.frame);
+    if (A.fuse) {
+      obs_frame_fused(P, s, leg, lane_pair, term || tout);
+      __syncthreads();  // F: the helper waves assemble and store the block's rows
+    } else {
+      obs_frame<K>(P, s, leg, e, W.n, A.frame);
+    }
     PH(6);
 #ifndef H12_EXP_NO_STORE  // experiment builds only (knock-out timing)
     store_env<K>(P, W, e, leg, s);
@@ -3158,7 +3362,12 @@ struct Handle {
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
   int16_t* asm_tab = nullptr;  // obs_assemble_kernel gather table for P.hist (Flat / Rsl layouts)
-  float* log_part = nullptr;   // [LOG_NPART][step blocks] episode-log partials (step_kernel -> assembly kernel)
+  bool fuse = false;           // step_kernel assembles the observation rows itself (FuseCtx; else obs_assemble_kernel)
+  float* log_part = nullptr;   // ring of LOG_RING [LOG_NPART][step blocks] episode-log partial sets (step_kernel ->
+                               // the assembly kernel's immediate fold, or log_flush_kernel for fused steps)
+  int log_pos = 0;             // ring slot of the next step with a log
+  int n_pend = 0;              // fused steps whose partials await log_flush_kernel (ring slots log_pos - n_pend ..)
+  float* pend_acc[LOG_RING] = {};
   // kernel timing: 4 events per timed step bound to the launches themselves (hipExtLaunchKernelGGL:
   // the events take the dispatch packet's begin / end timestamps, as rocprofv3's kernel trace does) --
   // step_kernel begin / end, observation kernel begin / end
@@ -3168,7 +3377,8 @@ struct Handle {
 
 constexpr size_t MAX_TIMED_STEPS = 4096;
 
-// the event pair of kernel k (0 = env kernel, 1 = observation kernel) of the current timed step, or nulls
+// the event pair of kernel k (0 = env kernel, 1 = the step's second kernel: assembly or log fold) of the current
+// timed step, or nulls; timing_next moves on to the next step
 bool timing_events(Handle* h, int k, hipEvent_t* e0, hipEvent_t* e1) {
   *e0 = *e1 = nullptr;
   if (!h->timing || h->n_timed >= MAX_TIMED_STEPS) return false;
@@ -3180,8 +3390,10 @@ bool timing_events(Handle* h, int k, hipEvent_t* e0, hipEvent_t* e1) {
   }
   *e0 = h->ev[i];
   *e1 = h->ev[i + 1];
-  if (k == 1) h->n_timed++;
   return true;
+}
+void timing_next(Handle* h) {
+  if (h->timing && h->n_timed < MAX_TIMED_STEPS) h->n_timed++;
 }
 
 bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
@@ -3415,10 +3627,10 @@ int feature_level(const KParams& P) {
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
                     hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, float* log_acc = nullptr,
-                    float* frame_out = nullptr) {
+                    float* frame_out = nullptr, float* log_part = nullptr) {
   AsmArgs A = {};
   A.frame_out = frame_out;
-  A.log_part = h->log_part;
+  A.log_part = log_part;
   A.log_acc = log_acc;
   A.log_nb = n_blocks(h);
   A.obs_prev = obs_prev;
@@ -3609,7 +3821,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   }
   e = hipMalloc(&h->dz_cnt, 3 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(h->dz_cnt, 0, 3 * sizeof(int));
-  const size_t log_bytes = sizeof(float) * LOG_NPART * (size_t)((n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK);
+  const size_t log_bytes = sizeof(float) * LOG_RING * LOG_NPART * (size_t)((n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK);
   if (e == hipSuccess) e = hipMalloc(&h->log_part, log_bytes);
   if (e == hipSuccess) e = hipMemset(h->log_part, 0, log_bytes);
   if (e != hipSuccess) {
@@ -3649,6 +3861,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
       h12env_destroy((h12env*)h);
       return set_err(H12_E_ALLOC, "gather table: %s", hipGetErrorString(e));
     }
+    // the step path assembles the rows inside step_kernel (fuse_stage / fuse_store) unless CaT rewrites the done
+    // flags after it (cat_prob_kernel) or H12_FUSE_OBS=0 asks for the two-kernel path
+    const char* fz = getenv("H12_FUSE_OBS");
+    h->fuse = !h->P.cat && !(fz && fz[0] == '0');
   }
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -3694,6 +3910,22 @@ int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
   return launch_assemble(h, nullptr, obs, nullptr, nullptr, mask, 1, A.lo, A.hi, (hipStream_t)stream);
 }
 
+// the pending fused steps' log folds, in one launch (log_flush_kernel), on the stream the steps ran on
+int flush_logs(Handle* h, hipStream_t stream, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+  if (!h->n_pend) return 0;
+  FoldArgs F = {};
+  F.part = h->log_part;
+  F.nb = n_blocks(h);
+  for (int k = 0; k < h->n_pend; ++k) {
+    F.slot[k] = (h->log_pos - h->n_pend + k + LOG_RING) % LOG_RING;
+    F.acc[k] = h->pend_acc[k];
+  }
+  hipExtLaunchKernelGGL(log_flush_kernel, dim3(LOG_NPART, h->n_pend), dim3(64), 0, stream, e0, e1, 0, F);
+  h->n_pend = 0;
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h12env_step_out* out,
                 int64_t step_index, void* stream) {
   Handle* h = (Handle*)hh;
@@ -3710,7 +3942,22 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.rew = out->rew;
   A.term = out->terminated;
   A.trunc = out->truncated;
-  A.log_part = out->log_acc ? h->log_part : nullptr;
+  // this step's partial set in the ring; a pending fold into the same accumulator, or a full ring, is folded first
+  // (stream order keeps every accumulator's additions in step order)
+  hipStream_t st = (hipStream_t)stream;
+  hipEvent_t t0, t1;
+  bool flushed = false;
+  if (out->log_acc && h->n_pend) {
+    bool dup = h->n_pend == LOG_RING;
+    for (int k = 0; k < h->n_pend && !dup; ++k) dup = h->pend_acc[k] == out->log_acc;
+    if (dup) {
+      timing_events(h, 1, &t0, &t1);  // the fold is this step's second kernel
+      if (int rc = flush_logs(h, st, t0, t1)) return rc;
+      flushed = true;
+    }
+  }
+  float* part = out->log_acc ? h->log_part + (size_t)h->log_pos * LOG_NPART * n_blocks(h) : nullptr;
+  A.log_part = part;
   A.applied_torque = out->applied_torque;
   A.foot_force = out->foot_force;
   A.env_offset = h->env_offset;
@@ -3718,26 +3965,44 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.hi = (uint32_t)((uint64_t)step_index >> 32);
   A.frame = h->frame;
   A.dz_slot = (int)(h->dz_step++ % 3);
-  hipEvent_t t0, t1;
-  timing_events(h, 0, &t0, &t1);
+  // fused assembly: whole 16-byte aligned rows (the LDS-DMA); otherwise obs_assemble_kernel follows
+  A.fuse = h->fuse && ((((uintptr_t)obs_prev | (uintptr_t)out->obs) & 15u) == 0);
+  A.frame_out = out->frame_out;
+  // timing: pair 0 = step_kernel, pair 1 = the second kernel (a flushed fold above, the assembly kernel below, or
+  // an empty pair)
+  hipEvent_t k0, k1;
+  timing_events(h, 0, &k0, &k1);
   // every block carries a helper wave and, with self-collision, a self-contact wave (helper_wave, self_wave)
-  LAUNCH_KT(step_kernel, t0, t1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 3 : 2) * BLOCK), 0, (hipStream_t)stream,
-            h->P, h->W, A);
+  LAUNCH_KT(step_kernel, k0, k1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 3 : 2) * BLOCK),
+            A.fuse ? sizeof(FuseLds) : 0, st, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
+  if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
+  if (A.fuse) {
+    // the rows are stored; the log partials are folded later (log_flush_kernel: a full ring, a reused accumulator,
+    // h12env_flush_log)
+    if (out->log_acc) h->pend_acc[h->n_pend++] = out->log_acc;
+    if (!flushed && timing_events(h, 1, &t0, &t1)) {  // no second kernel: an empty pair
+      HIP_TRY(hipEventRecord(t0, st));
+      HIP_TRY(hipEventRecord(t1, st));
+    }
+    timing_next(h);
+    return 0;
+  }
   if (h->P.cat) {
     hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
     HIP_TRY(hipGetLastError());
     static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
-    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, out->log_acc ? h->log_part : nullptr,
-                 n_blocks(h)};
+    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
     hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0,
                        (hipStream_t)stream, h->P, h->W, C);
     HIP_TRY(hipGetLastError());
   }
-  timing_events(h, 1, &t0, &t1);
+  t0 = t1 = nullptr;
+  if (!flushed) timing_events(h, 1, &t0, &t1);
+  timing_next(h);
   // fill = terminated | truncated: the envs reset inside the step restart their history
-  return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi,
-                         (hipStream_t)stream, t0, t1, out->log_acc, out->frame_out);
+  return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi, st, t0, t1,
+                         out->log_acc, out->frame_out, part);
 }
 
 int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t* fill_mask, void* stream) {
@@ -3991,6 +4256,12 @@ int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_
   if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * fr;
   if (flops_per_env) *flops_per_env = f0 + f1;
   return 0;
+}
+
+int h12env_flush_log(h12env* hh, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  return flush_logs(h, (hipStream_t)stream);
 }
 
 int h12env_set_kernel_timing(h12env* hh, int enable) {

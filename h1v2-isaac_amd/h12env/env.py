@@ -61,8 +61,9 @@ class _LazyLog(dict):
     nothing is kept alive or computed per step for logs nobody reads)."""
 
     def __init__(self, ring: torch.Tensor, slot: int, max_episode_length_s: float, terms: list, term_map: torch.Tensor,
-                 cstr: list | None = None, extra: dict | None = None, lookback: int = 1):
+                 cstr: list | None = None, extra: dict | None = None, lookback: int = 1, flush=None):
         super().__init__()
+        self._flush = flush  # completes the library's deferred accumulator additions (h12env_flush_log)
         self._ring = ring
         self._slot = slot
         self._lookback = lookback
@@ -88,6 +89,8 @@ class _LazyLog(dict):
     def _fill(self):
         if self._done:
             return
+        if self._flush is not None:
+            self._flush()
         ring = self._ring
         idx = (self._slot - torch.arange(self._lookback, device=ring.device)) % ring.shape[0]
         k = torch.argmax((ring[idx, NREW] > 0).to(torch.int32)).view(1)  # first slot counting a reset (0 if none)
@@ -535,6 +538,7 @@ class H12VelocityEnv:
                 elif t0 <= c - _LOG_RING + _LOG_CHUNK + _LOG_LOOKBACK - 2:
                     log._fill()
                     del self._live_logs[t0]
+            self._flush_log()  # no deferred fold may land in the recycled slots after the zeroing
             self._log_ring[slot:slot + _LOG_CHUNK].zero_()
         # the output pointers are fixed per observation buffer (built once, _step_outs); only the log slot moves
         rec = self._rollout
@@ -553,7 +557,7 @@ class H12VelocityEnv:
         if rc:
             check(self._lib, rc, "h12env_step")
         log = _LazyLog(self._log_ring, slot, self.max_episode_length_s, self._reward_terms, self._reward_map,
-                       self._cstr_terms, self._log_extra, _LOG_LOOKBACK)
+                       self._cstr_terms, self._log_extra, _LOG_LOOKBACK, self._flush_log)
         self._live_logs[self.common_step_counter] = weakref.ref(log)
         self.extras = {"log": log, "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
@@ -646,6 +650,7 @@ class H12VelocityEnv:
                 "counter": self.common_step_counter}
 
     def restore(self, snap: dict):
+        self._flush_log()  # folds of steps before the restore land in their own slots first
         self._state.copy_(snap["state"])
         for o, s in zip(self._obs, snap["obs"]):
             o.copy_(s)
@@ -655,8 +660,13 @@ class H12VelocityEnv:
     def render(self, recompute: bool = False):
         return None
 
+    def _flush_log(self):
+        if not self._closed:
+            check(self._lib, self._lib.h12env_flush_log(self._h, _raw_stream(self._dev_index)), "h12env_flush_log")
+
     def close(self):
         if not self._closed:
+            self._flush_log()  # logs still referenced (extras) stay complete
             torch.cuda.synchronize(self.device)
             self._lib.h12env_destroy(self._h)
             self._closed = True

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define H12ENV_ABI_VERSION 8
+#define H12ENV_ABI_VERSION 9
 #define H12_NJ 12          /* actuated joints (L leg 6, R leg 6; MJCF depth-first order) */
 #define H12_NHIST 10       /* observation history length of the Flat task (flat_env_cfg.py:26); max */
 #define H12_OBS_FRAME 45   /* ang_vel 3, gravity 3, command 3, q-q0 12, qd 12, action 12 */
@@ -309,7 +309,10 @@ typedef struct h12env_step_out {
   float* rew;              /* N       (required) */
   uint8_t* terminated;     /* N       (required) */
   uint8_t* truncated;      /* N       (required) */
-  float* log_acc;          /* H12_NLOG floats, accumulated with atomics (caller zeroes) */
+  float* log_acc;          /* H12_NLOG floats, accumulated into (caller zeroes).  (ABI 9) The step's additions may
+                              be deferred: they are complete, in step order, once h12env_flush_log has run on the
+                              stream (later steps flush by themselves when 64 steps are pending or an accumulator
+                              is reused) */
   float* applied_torque;   /* N x 12, last physics step (ArticulationData.applied_torque) */
   float* foot_force;       /* N x 2,  |net contact force| of the feet, last physics step */
   float* cstr_prob;        /* N, CaT task: the dones CaTEnv.step returns (constraint termination probability,
@@ -336,6 +339,9 @@ int h12env_reset(h12env* h, const uint8_t* mask, float* obs, void* stream);
  * out->obs.  step_index: common_step_counter after increment (>= 1). */
 int h12env_step(h12env* h, const float* actions, const float* obs_prev, const h12env_step_out* out,
                 int64_t step_index, void* stream);
+/* (ABI 9) Complete every deferred episode-log addition of earlier h12env_step calls (one kernel on stream; nothing
+ * when none is pending).  Call it before reading a step's log_acc. */
+int h12env_flush_log(h12env* h, void* stream);
 /* ObservationManager.compute() outside step(): appends one frame of the current state to every
  * env's history (obs_prev -> obs, may alias); fill_mask[i] != 0 fills env i's history with the frame
  * (the first push after a reset).  fill_mask may be NULL. */

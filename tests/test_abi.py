@@ -38,7 +38,7 @@ def test_struct_sizes_match():
 
 def test_state_bytes_and_abi():
     lib = load_library()
-    assert lib.h12env_abi_version() == 8
+    assert lib.h12env_abi_version() == 9
     assert lib.h12env_state_bytes(0) == 0
     assert lib.h12env_state_bytes(4096) == (143 + 3) * 4 * 4096
 

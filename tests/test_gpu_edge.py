@@ -160,7 +160,7 @@ def test_ragged_env_counts_rsl_cat(gpu, task, n):
 def test_episode_log_fold_ragged(gpu, task, n):
     """The episode log (reward sums, reset / time-out / base-contact counts, command metrics and, for CaT, the
     constraint statistics) goes through per-block partial slots folded by the assembly kernel (log_load /
-    log_fold): compare the step's accumulator with the oracle's on steps with forced time-outs, including grids
+    log_fold; CaT) or, on the fused Flat path, by log_flush_kernel (deferred, h12env_flush_log): compare the step's accumulator with the oracle's on steps with forced time-outs, including grids
     smaller than the number of log values (n = 1, 37)."""
     from h12env._abi import F as FIELDS, LOG_METRIC, NLOG, NREW
     from h12env.cfg import H12CaTEnvCfg
@@ -193,6 +193,7 @@ def test_episode_log_fold_ragged(gpu, task, n):
         env.step(torch.from_numpy(a).cuda())
         ref.F[:], ref.I[:] = F0, I0  # teacher-forced: the oracle steps from the GPU's state
         _, _, r_term, r_trunc, info = ref.step(a, t)
+        env._flush_log()  # the fused step path defers its fold (h12env_flush_log)
         acc = env._log_ring[env.common_step_counter % len(env._log_ring)].cpu().numpy()
         lo = info["log"]
         if (r_term | r_trunc).any():

@@ -57,6 +57,7 @@ def test_teacher_forced_flat_4096x1100(gpu):
         done_any = done | tg | trg  # envs resetting in either run (a threshold-sensitive flip resets one only)
         if done.any() and ok[done_any].all():
             # log accumulator of this step's resetting envs (episode sums, count, time-out / base-contact counts)
+            env._flush_log()  # the fused step path defers its fold (h12env_flush_log)
             acc = env._log_ring[env.common_step_counter % len(env._log_ring)].cpu().numpy()
             lo = info["log"]
             k = list(range(NREW + 3)) + [LOG_METRIC, LOG_METRIC + 1]  # + the command metrics (ABI 7)
