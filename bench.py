@@ -474,7 +474,11 @@ def main():
                 or args.inner_steps is not None or args.explicit_penalty):  # tools/profile.sh: the default workload
             pmc, pmc_src = {}, "not collected for this workload (tools/profile.sh profiles the default flat line)"
         traffic = pmc.get("step_kernel", {}).get("hbm_bytes_per_launch")
-        obs_traffic = pmc.get("obs_assemble_kernel", {}).get("hbm_bytes_per_launch")
+        # kernel 1 of the timing / cost pairs: the observation assembly kernel, or -- when step_kernel assembles the
+        # rows itself (env.obs_fused) -- the deferred episode-log fold, launched once per <= 32 steps
+        fused = env.obs_fused
+        sec_kernel = "log_flush_kernel" if fused else "obs_assemble_kernel"
+        obs_traffic = None if fused else pmc.get(sec_kernel, {}).get("hbm_bytes_per_launch")
         # VALU issue roofline of step_kernel: one wave per SIMD issues at most one VALU instruction per
         # 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost', one wave's stream on one SIMD), so
         # the kernel's floor is (VALU instructions per wave) x 4 cycles at the 2.4 GHz max clock
@@ -553,12 +557,15 @@ def main():
                 "valu_flops_per_env_step": flops_env,
                 "valu_tflops": flops_env * n / (kern_ms_avg * 1e-3) / 1e12,
                 "valu_frac": flops_env * n / (kern_ms_avg * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                "obs_assembly": "fused into step_kernel" if fused else "obs_assemble_kernel",
                 "secondary": {
-                    "kernel": "obs_assemble_kernel",
+                    "kernel": sec_kernel,
                     "bound": "hbm",
                     "kernel_ms_avg": obs_ms_avg,
-                    "achieved": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9,
-                    "frac": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "timing": ("per env step: the launches' time summed over the window / steps (one launch folds "
+                               "the steps since the last one)") if fused else "per launch (one per env step)",
+                    "achieved": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9 if obs_ms_avg > 0 else None,
+                    "frac": obs_bytes_env * n / (obs_ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if obs_ms_avg > 0 else None,
                     "traffic": obs_traffic,
                 },
                 "step_bytes_per_env": step_bytes_env,

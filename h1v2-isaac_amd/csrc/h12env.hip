@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/h12env.h"
@@ -1056,8 +1057,12 @@ H12_DEV void st_row4(float* dst, int j, float4 v) {
 // (128 CUs at ~9 GB/s each), more than the separate kernel over all 256 CUs.  Bit-identical to the two-kernel path:
 // the same copies and the same float operations.
 constexpr int FUSE_ROWS = ENVS_PER_BLOCK;
+constexpr int FUSE_F4_MAX = FUSE_ROWS * H12_OBS_FRAME * H12_NHIST / 4;  // float4s of a block's rows (history 10)
+constexpr int FUSE_CODE_BYTES = (FUSE_F4_MAX + H12_OBS_FRAME * H12_NHIST + 1023) / 1024 * 1024;  // 1 KB DMA chunks
 struct FuseLds {
   float hist[FUSE_ROWS * H12_OBS_FRAME * (H12_NHIST + 1)];  // the rows (45 hist floats each), then frames [row][45]
+  uint8_t code[FUSE_CODE_BYTES];  // fuse_code_table: per float4 of the rows bit q = float q's shift is 12 (else 3);
+                                  // from FUSE_F4_MAX on, per row column its frame component
   float noise[FUSE_ROWS][33];  // noise values of the row's 30 noisy components (padded row: conflict-free)
   int fill[FUSE_ROWS];         // the row restarts its history (terminated | truncated)
 };
@@ -1066,6 +1071,7 @@ H12_DEV FuseLds& fuse_lds() { return *reinterpret_cast<FuseLds*>(h12_dyn_lds); }
 struct FuseCtx {
   const float* src;  // the block's first row of obs_prev
   float* dst;        // ... of obs
+  const uint8_t* code;  // fuse_code_table (device, FUSE_CODE_BYTES)
   int row;           // floats per row (45 x history)
   int on;            // whole block, 16-byte aligned, >= 2 physics steps: the spread path; else fuse_late alone
 };
@@ -1080,26 +1086,27 @@ H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
       if (ch * 64 + lane < f4)
         __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane),
                                          (__attribute__((address_space(3))) void*)(F.hist + ch * 256), 16, 0, 0);
+    for (int ch = w; ch < FUSE_CODE_BYTES / 1024; ch += nw)
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint4*>(f.code) + ch * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(F.code + ch * 1024), 16, 0, 0);
     return;
   }
-  // this lane's float4s j = t + k nt, k in its share of the remaining inner steps; every float gets the next-newer
-  // slot (+3 in the 3-wide terms, +12 in the 12-wide ones); the newest slot's floats get a placeholder that
-  // fuse_late overwrites (same block, after barrier F: every early store has completed by then)
+  // this lane's float4s j = t + k nt, k in its share of the remaining inner steps: every float gets the next-newer
+  // slot (+3 in the 3-wide terms, +12 in the 12-wide ones, fuse_code_table); the newest slot's floats get a
+  // placeholder that fuse_late overwrites, as it rewrites the rows of resetting envs (after barrier F, when every
+  // early store has completed)
   const int kmax = (f4 + nt - 1) / nt;
   const int k0 = (it - 1) * kmax / (n_steps - 1), k1 = it * kmax / (n_steps - 1);
-  const int h9 = f.row / 5;  // 9 x history: the 3-wide terms' columns
-  const uint32_t mrow = 0xFFFFFFFFu / (uint32_t)f.row + 1u;  // p / row = umulhi(p, mrow) for p < 2^16
+#ifdef H12_EXP_FUSE_NO_EARLY  // experiment builds only: the shifted-row stores dropped
+  return;
+#endif
   for (int k = k0; k < k1; ++k) {
     const int j = t + k * nt;
     if (j >= f4) break;
-    const int p0 = 4 * j, col0 = p0 - (int)__umulhi((uint32_t)p0, mrow) * f.row;
-    float v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int col = col0 + q - (col0 + q >= f.row ? f.row : 0);
-      v[q] = F.hist[p0 + q + (col < h9 ? 3 : 12)];
-    }
-    st_row4(f.dst, j, make_float4(v[0], v[1], v[2], v[3]));
+    const uint32_t cd = F.code[j];
+    const float* pb = F.hist + 4 * j;
+    st_row4(f.dst, j, make_float4(pb[0 + ((cd & 1u) ? 12 : 3)], pb[1 + ((cd & 2u) ? 12 : 3)],
+                                  pb[2 + ((cd & 4u) ? 12 : 3)], pb[3 + ((cd & 8u) ? 12 : 3)]));
   }
 }
 // before the R2 barrier of inner step 1: this wave's LDS-DMA has landed (the other waves' reads follow R2)
@@ -2639,6 +2646,7 @@ struct StepArgs {
   int n_substeps;
   int dz_slot;  // deadzone counter read this step (P.dz_cnt[dz_slot]); +1 is counted into, +2 zeroed
   int fuse;     // the observation rows are assembled inside step_kernel (FuseCtx; dynamic LDS)
+  const uint8_t* fuse_code;  // fuse_code_table of the handle's history length
   float* frame_out;         // (n, 45) noisy scaled frames as they enter the history (fused path), or null
 };
 
@@ -2672,9 +2680,24 @@ H12_DEV void fuse_late(const KParams& P, const StepArgs& A, const FuseCtx& fc, i
   const int e0 = step_block() * FUSE_ROWS, ne = min(FUSE_ROWS, n - e0);
   const int row = fc.row, nh = P.hist;
   const float* fr = F.hist + FUSE_ROWS * row;
-  if (A.frame_out)  // the block's frames are one contiguous run of ne x 45 floats
-    for (int k = t; k < ne * H12_OBS_FRAME; k += nt) A.frame_out[(size_t)e0 * H12_OBS_FRAME + k] = fr[k];
+  if (A.frame_out) {  // the block's frames are one contiguous run of ne x 45 floats
+    float* fo = A.frame_out + (size_t)e0 * H12_OBS_FRAME;
+    if (ne == FUSE_ROWS && ((uintptr_t)fo & 15u) == 0) {  // 360 float4s, reads before stores
+      constexpr int NF4 = FUSE_ROWS * H12_OBS_FRAME / 4, FMAX = (NF4 + 63) / 64;
+      float4 fv[FMAX];
+#pragma unroll
+      for (int k = 0; k < FMAX; ++k) fv[k] = reinterpret_cast<const float4*>(fr)[min(t + k * nt, NF4 - 1)];
+#pragma unroll
+      for (int k = 0; k < FMAX; ++k)
+        if (t + k * nt < NF4) reinterpret_cast<float4*>(fo)[t + k * nt] = fv[k];
+    } else {
+      for (int k = t; k < ne * H12_OBS_FRAME; k += nt) fo[k] = fr[k];
+    }
+  }
   if (fc.on) {
+#ifdef H12_EXP_FUSE_NO_LATE  // experiment builds only: the newest-slot / refill stores dropped
+    return;
+#endif
     for (int w = t; w < FUSE_ROWS * H12_OBS_FRAME; w += nt) {
       const int r = w / H12_OBS_FRAME, c = w - r * H12_OBS_FRAME;
       fc.dst[r * row + newest_col(c, nh)] = fr[w];
@@ -2684,8 +2707,7 @@ H12_DEV void fuse_late(const KParams& P, const StepArgs& A, const FuseCtx& fc, i
     while (fm) {
       const int r = __builtin_ctz(fm);
       fm &= fm - 1u;
-      for (int col = t; col < row; col += nt)
-        fc.dst[r * row + col] = fr[H12_OBS_FRAME * r + (int)(hist_col_entry(col, nh) & 0xFFu)];
+      for (int col = t; col < row; col += nt) fc.dst[r * row + col] = fr[H12_OBS_FRAME * r + F.code[FUSE_F4_MAX + col]];
     }
     return;
   }
@@ -2728,7 +2750,8 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     FuseCtx fc = {};
     if (A.fuse) {
       const int e0 = step_block() * ENVS_PER_BLOCK, row = H12_OBS_FRAME * P.hist;
-      fc = {A.obs_prev + (size_t)e0 * row, A.obs + (size_t)e0 * row, row, e0 + ENVS_PER_BLOCK <= W.n && nsteps >= 2};
+      fc = {A.obs_prev + (size_t)e0 * row, A.obs + (size_t)e0 * row, A.fuse_code, row,
+            e0 + ENVS_PER_BLOCK <= W.n && nsteps >= 2};
     }
     const int ft = threadIdx.x - BLOCK, fnt = blockDim.x - BLOCK;  // lane among the helper waves
     if (threadIdx.x < 2 * BLOCK) {
@@ -2757,26 +2780,26 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
           }
         }
       }
-      if (A.log_part) {
-        // lane v sums value v over the block's envs and adds it to this block's partial slot (one atomic per
-        // value and block; the slots are value-major [LOG_NPART][blocks], no two blocks share an address)
-        const int v = threadIdx.x - BLOCK;
-        constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+      // lane v: value v summed over the block's envs, stored into this block's partial slot (value-major
+      // [LOG_NPART][blocks]: each block owns its slots, so a plain store of every used value, zeros included); on
+      // the fused path after the rows, off barrier F's path
+      float lacc = 0.f;
+      const int v = threadIdx.x - BLOCK;
+      constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+      const bool lv = A.log_part && v < LOG_NSTEP && (v < NT || v >= H12_NREW);
+      if (lv) {
         const int ne = min(ENVS_PER_BLOCK, W.n - step_block() * ENVS_PER_BLOCK);
-        if (v < LOG_NSTEP && (v < NT || v >= H12_NREW)) {
-          const HelpLds& H = help_lds();
-          float acc = 0.f;
-          for (int j = 0; j < ne; ++j) acc += H.logv[v][j];
-#ifndef H12_EXP_NO_LOG_ATOMICS  // experiment builds only: the per-block episode-log partials dropped
-          if (acc != 0.f) atomicAdd(A.log_part + (size_t)v * gridDim.x + blockIdx.x, acc);
-#endif
-        }
+        const HelpLds& H = help_lds();
+        for (int j = 0; j < ne; ++j) lacc += H.logv[v][j];
       }
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's shifted-row stores have completed (fuse_late rewrites some)
         __syncthreads();                // F: the physics wave's noisy frames and refill flags
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
+#ifndef H12_EXP_NO_LOG_ATOMICS  // experiment builds only: the per-block episode-log partials dropped
+      if (lv) A.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;
+#endif
     } else {
       self_wave<K>(P, W.n, nsteps, fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
@@ -3363,6 +3386,7 @@ struct Handle {
   bool timing = false;
   int16_t* asm_tab = nullptr;  // obs_assemble_kernel gather table for P.hist (Flat / Rsl layouts)
   bool fuse = false;           // step_kernel assembles the observation rows itself (FuseCtx; else obs_assemble_kernel)
+  uint8_t* fuse_code = nullptr;  // fuse_code_table(P.hist) on the device
   float* log_part = nullptr;   // ring of LOG_RING [LOG_NPART][step blocks] episode-log partial sets (step_kernel ->
                                // the assembly kernel's immediate fold, or log_flush_kernel for fused steps)
   int log_pos = 0;             // ring slot of the next step with a log
@@ -3372,6 +3396,7 @@ struct Handle {
   // the events take the dispatch packet's begin / end timestamps, as rocprofv3's kernel trace does) --
   // step_kernel begin / end, observation kernel begin / end
   std::vector<hipEvent_t> ev;
+  std::vector<uint8_t> ev_k1;  // per timed step: its pair 1 was recorded (a fused step without a flush has none)
   size_t n_timed = 0;
 };
 
@@ -3390,10 +3415,16 @@ bool timing_events(Handle* h, int k, hipEvent_t* e0, hipEvent_t* e1) {
   }
   *e0 = h->ev[i];
   *e1 = h->ev[i + 1];
+  if (h->ev_k1.size() <= h->n_timed) h->ev_k1.resize(h->n_timed + 1, 0);
+  if (k == 1) h->ev_k1[h->n_timed] = 1;
   return true;
 }
+// the current timed step's pair 1 is already in use (a log fold flushed ahead of it)
+bool pair1_taken(const Handle* h) { return h->n_timed < h->ev_k1.size() && h->ev_k1[h->n_timed]; }
 void timing_next(Handle* h) {
-  if (h->timing && h->n_timed < MAX_TIMED_STEPS) h->n_timed++;
+  if (!h->timing || h->n_timed >= MAX_TIMED_STEPS) return;
+  h->n_timed++;
+  if (h->ev_k1.size() > h->n_timed) h->ev_k1[h->n_timed] = 0;
 }
 
 bool close(float a, float b) { return fabsf(a - b) <= 1e-6f * (1.f + fabsf(a) + fabsf(b)); }
@@ -3595,6 +3626,27 @@ std::vector<int16_t> asm_gather_table(int nh) {
       d = 12;
     }
     t[(size_t)p] = (int16_t)(hh == nh - 1 ? nf + H12_OBS_FRAME * r + c - p : d);
+  }
+  return t;
+}
+
+// fused assembly: one code byte per float4 of a block's 32 rows of history nh (the same for every block) -- bit q:
+// float q's next-newer slot is 12 floats on (the 12-wide terms; else 3) -- then, from byte FUSE_F4_MAX, one byte per
+// row column: its frame component (a refilled row holds the frame in every slot)
+std::vector<uint8_t> fuse_code_table(int nh) {
+  const int row = H12_OBS_FRAME * nh, f4 = ENVS_PER_BLOCK * row / 4;
+  std::vector<uint8_t> t((size_t)FUSE_CODE_BYTES, 0);
+  for (int j = 0; j < f4; ++j) {
+    uint8_t c = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int col = (4 * j + q) % row;
+      if (col >= 9 * nh) c |= (uint8_t)(1u << q);
+    }
+    t[(size_t)j] = c;
+  }
+  for (int col = 0; col < row; ++col) {
+    const int k = col < 9 * nh ? col : col - 9 * nh, w = col < 9 * nh ? 3 : 12;
+    t[(size_t)FUSE_F4_MAX + col] = (uint8_t)((col < 9 * nh ? 0 : 9) + w * (k / (w * nh)) + k % w);
   }
   return t;
 }
@@ -3865,6 +3917,15 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     // flags after it (cat_prob_kernel) or H12_FUSE_OBS=0 asks for the two-kernel path
     const char* fz = getenv("H12_FUSE_OBS");
     h->fuse = !h->P.cat && !(fz && fz[0] == '0');
+    if (h->fuse) {
+      const std::vector<uint8_t> c = fuse_code_table(h->P.hist);
+      e = hipMalloc(&h->fuse_code, c.size());
+      if (e == hipSuccess) e = hipMemcpy(h->fuse_code, c.data(), c.size(), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        h12env_destroy((h12env*)h);
+        return set_err(H12_E_ALLOC, "fused-assembly code table: %s", hipGetErrorString(e));
+      }
+    }
   }
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -3888,6 +3949,7 @@ void h12env_destroy(h12env* hh) {
   if (h->log_part) (void)hipFree(h->log_part);
   if (h->cat_mem) (void)hipFree(h->cat_mem);
   if (h->asm_tab) (void)hipFree(h->asm_tab);
+  if (h->fuse_code) (void)hipFree(h->fuse_code);
   for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
   delete h;
 }
@@ -3951,7 +4013,8 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
     bool dup = h->n_pend == LOG_RING;
     for (int k = 0; k < h->n_pend && !dup; ++k) dup = h->pend_acc[k] == out->log_acc;
     if (dup) {
-      timing_events(h, 1, &t0, &t1);  // the fold is this step's second kernel
+      t0 = t1 = nullptr;
+      if (!pair1_taken(h)) timing_events(h, 1, &t0, &t1);  // this step's second kernel
       if (int rc = flush_logs(h, st, t0, t1)) return rc;
       flushed = true;
     }
@@ -3968,6 +4031,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   // fused assembly: whole 16-byte aligned rows (the LDS-DMA); otherwise obs_assemble_kernel follows
   A.fuse = h->fuse && ((((uintptr_t)obs_prev | (uintptr_t)out->obs) & 15u) == 0);
   A.frame_out = out->frame_out;
+  A.fuse_code = h->fuse_code;
   // timing: pair 0 = step_kernel, pair 1 = the second kernel (a flushed fold above, the assembly kernel below, or
   // an empty pair)
   hipEvent_t k0, k1;
@@ -3981,11 +4045,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
     // the rows are stored; the log partials are folded later (log_flush_kernel: a full ring, a reused accumulator,
     // h12env_flush_log)
     if (out->log_acc) h->pend_acc[h->n_pend++] = out->log_acc;
-    if (!flushed && timing_events(h, 1, &t0, &t1)) {  // no second kernel: an empty pair
-      HIP_TRY(hipEventRecord(t0, st));
-      HIP_TRY(hipEventRecord(t1, st));
-    }
-    timing_next(h);
+    timing_next(h);  // no second kernel unless a fold was flushed above
     return 0;
   }
   if (h->P.cat) {
@@ -3998,7 +4058,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
     HIP_TRY(hipGetLastError());
   }
   t0 = t1 = nullptr;
-  if (!flushed) timing_events(h, 1, &t0, &t1);
+  if (!flushed && !pair1_taken(h)) timing_events(h, 1, &t0, &t1);
   timing_next(h);
   // fill = terminated | truncated: the envs reset inside the step restart their history
   return launch_assemble(h, obs_prev, out->obs, out->terminated, out->truncated, nullptr, 0, A.lo, A.hi, st, t0, t1,
@@ -4225,11 +4285,20 @@ int h12env_kernel_cost(const h12env* hh, int kernel, double* bytes_per_env, doub
                     (P.rsl ? 8.0 : 0.0) + (P.push ? 1.0 : 0.0) + (P.cat ? 22.0 : 0.0);
     // CaT: the constraint scratch written and read back, the no_move list entry, reward and dones rewritten
     const double cat_bytes = P.cat ? (double)CAT_ROWS * 4.0 * 2.0 + 4.0 + 4.0 * 2.0 + 4.0 : 0.0;
-    bytes = fields * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 + (double)H12_NJ * 4.0 + 2.0 * 4.0 +
-            (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0 + cat_bytes;
-    flops = h->flops_per_env;
+    bytes = fields * 4.0 * 2.0 + (double)H12_NJ * 4.0 + 4.0 + 2.0 + (double)H12_NJ * 4.0 + 2.0 * 4.0 + cat_bytes;
+    if (h->fuse) {  // the observation row: H-1 old frames read, H frames written (H = 10 Flat, 6 Rsl)
+      const double row = (double)H12_OBS_FRAME * P.hist;
+      bytes += (row - H12_OBS_FRAME) * 4.0 + row * 4.0;
+    } else {
+      bytes += (rough ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;  // the frame scratch
+    }
+    flops = h->flops_per_env + (h->fuse ? 30.0 * 3.0 + 45.0 + 8.0 * 10.0 * 6.0 : 0.0);
   } else if (kernel == 1) {
-    if (rough) {
+    if (h->fuse) {
+      // log_flush_kernel, per step and env: the block's partial slots read and zeroed
+      bytes = (double)LOG_NPART * 4.0 * 2.0 / ENVS_PER_BLOCK;
+      flops = (double)LOG_NPART / ENVS_PER_BLOCK;
+    } else if (rough) {
       // frame read, one height sample per ray, the 235-float row written
       bytes = (double)FRAME_ROWS * 4.0 + (double)H12_NSCAN * 4.0 + (double)H12_NOBS_ROUGH * 4.0;
       flops = 55.0 * 10.0 * 6.0 + (double)H12_NSCAN * 20.0;
@@ -4251,17 +4320,26 @@ int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_
   double b0, f0, b1, f1;
   if (int rc = h12env_kernel_cost(hh, 0, &b0, &f0)) return rc;
   if (int rc = h12env_kernel_cost(hh, 1, &b1, &f1)) return rc;
-  // the frame round trip between the kernels is not compulsory traffic of the step
-  const double fr = (((const Handle*)hh)->P.task == H12_TASK_ROUGH ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
+  // the frame round trip between the kernels is not compulsory traffic of the step (none on the fused path)
+  const Handle* h = (const Handle*)hh;
+  const double fr = h->fuse ? 0.0 : (h->P.task == H12_TASK_ROUGH ? (double)FRAME_ROWS : (double)H12_OBS_FRAME) * 4.0;
   if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * fr;
   if (flops_per_env) *flops_per_env = f0 + f1;
   return 0;
 }
 
+int h12env_obs_fused(const h12env* hh) {
+  const Handle* h = (const Handle*)hh;
+  return h && h->fuse ? 1 : 0;
+}
+
 int h12env_flush_log(h12env* hh, void* stream) {
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
-  return flush_logs(h, (hipStream_t)stream);
+  // kernel timing: the fold is counted as the second kernel of the next step
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (h->n_pend && !pair1_taken(h)) timing_events(h, 1, &e0, &e1);
+  return flush_logs(h, (hipStream_t)stream, e0, e1);
 }
 
 int h12env_set_kernel_timing(h12env* hh, int enable) {
@@ -4269,6 +4347,7 @@ int h12env_set_kernel_timing(h12env* hh, int enable) {
   if (!h) return set_err(H12_E_ARG, "null handle");
   h->timing = enable != 0;
   h->n_timed = 0;
+  std::fill(h->ev_k1.begin(), h->ev_k1.end(), 0);
   return 0;
 }
 
@@ -4276,11 +4355,15 @@ int h12env_kernel_times(h12env* hh, double* env_ms, double* obs_ms, int* n_steps
   Handle* h = (Handle*)hh;
   if (!h) return set_err(H12_E_ARG, "null handle");
   double a = 0.0, b = 0.0;
-  if (h->n_timed > 0) HIP_TRY(hipEventSynchronize(h->ev[4 * h->n_timed - 1]));
+  if (h->n_timed > 0) {  // the last step's kernels (its pair 1 exists only if that step had a second kernel)
+    const size_t l = h->n_timed - 1;
+    HIP_TRY(hipEventSynchronize(h->ev[4 * l + 1]));
+    if (l < h->ev_k1.size() && h->ev_k1[l]) HIP_TRY(hipEventSynchronize(h->ev[4 * l + 3]));
+  }
   for (size_t i = 0; i < h->n_timed; ++i) {
     float t0 = 0.f, t1 = 0.f;
     HIP_TRY(hipEventElapsedTime(&t0, h->ev[4 * i], h->ev[4 * i + 1]));
-    HIP_TRY(hipEventElapsedTime(&t1, h->ev[4 * i + 2], h->ev[4 * i + 3]));
+    if (i < h->ev_k1.size() && h->ev_k1[i]) HIP_TRY(hipEventElapsedTime(&t1, h->ev[4 * i + 2], h->ev[4 * i + 3]));
     a += t0;
     b += t1;
   }
@@ -4288,6 +4371,7 @@ int h12env_kernel_times(h12env* hh, double* env_ms, double* obs_ms, int* n_steps
   if (obs_ms) *obs_ms = b;
   if (n_steps) *n_steps = (int)h->n_timed;
   h->n_timed = 0;
+  std::fill(h->ev_k1.begin(), h->ev_k1.end(), 0);
   return 0;
 }
 

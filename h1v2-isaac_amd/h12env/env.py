@@ -683,8 +683,15 @@ class H12VelocityEnv:
         self._lib.h12env_step_cost(self._h, C.byref(b), C.byref(f))
         return b.value, f.value
 
+    @property
+    def obs_fused(self) -> bool:
+        """step() assembles the observation rows inside the env kernel (h12env_obs_fused); kernel 1 of the timing /
+        cost pairs is then the deferred episode-log fold, else the observation assembly kernel."""
+        return bool(self._lib.h12env_obs_fused(self._h))
+
     def kernel_cost(self, kernel: int):
-        """(compulsory HBM bytes, counted FLOPs) per env of kernel 0 (env step) or 1 (obs assembly)."""
+        """(compulsory HBM bytes, counted FLOPs) per env of kernel 0 (env step) or 1 (obs assembly, or the log fold
+        per step on the fused path)."""
         b, f = C.c_double(), C.c_double()
         check(self._lib, self._lib.h12env_kernel_cost(self._h, kernel, C.byref(b), C.byref(f)), "h12env_kernel_cost")
         return b.value, f.value
