@@ -83,14 +83,16 @@ def report(text: str, name: str) -> dict:
 
 def physics_wave_json(text: str, meta: dict, out: Path) -> None:
     """profiles/latest_isa.json for bench.py's issue roofline: the Flat step_kernel's register allocation and the
-    VALU count of its physics wave's physics-step loop (the largest loop: the physics wave's chain; the helper and
-    self-contact waves run other, shorter loops), keyed by the kernel source's sha256 like latest_pmc.json."""
+    VALU count of its physics wave's physics-step loop, keyed by the kernel source's sha256 like latest_pmc.json.
+    The physics wave is the one whose registers overflow into AGPRs, so its loop is the one with the most
+    v_accvgpr moves (largest VALU count among ties); the helper / self-contact loops use none and, with the fused
+    observation stores, the helper loop has more VALU than the physics loop."""
     import hashlib
     import json
 
     name = next(k for k in meta if "step_kernelILi0E" in k)
     g, r = meta[name], report(text, name)
-    top = max(r["loops"], key=lambda x: x[2])
+    top = max(r["loops"], key=lambda x: (x[3], x[2]))
     res = {"source_sha256": hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest(),
            "kernel": name,
            "registers": {"vgpr_count_total": g.get("vgpr_count"), "agpr_count": g.get("agpr_count"),
