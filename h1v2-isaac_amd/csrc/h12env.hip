@@ -1045,7 +1045,7 @@ H12_DEV void st_row4(float* dst, int j, float4 v) {
                                          __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
                                          H12_OBS_POL);
 }
-// ---- Fused observation assembly (step path; Flat / Rsl history layouts without CaT: StepArgs.fuse).  The rows
+// ---- Fused observation assembly (step path; the history layouts -- Flat, Rsl, CaT: StepArgs.fuse).  The rows
 // obs_assemble_kernel would write are stored by step_kernel's helper waves instead, mostly while the physics wave
 // integrates: a row is 90 % shifted history (obs[e, slot h] = obs_prev[e, slot h + 1]), which this step's physics
 // does not change.  After the first physics step's R2 barrier the helper waves LDS-DMA the block's 32 rows of
@@ -3913,10 +3913,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
       h12env_destroy((h12env*)h);
       return set_err(H12_E_ALLOC, "gather table: %s", hipGetErrorString(e));
     }
-    // the step path assembles the rows inside step_kernel (fuse_stage / fuse_store) unless CaT rewrites the done
-    // flags after it (cat_prob_kernel) or H12_FUSE_OBS=0 asks for the two-kernel path
+    // the step path assembles the rows inside step_kernel (FuseCtx) unless H12_FUSE_OBS=0 asks for the two-kernel
+    // path (CaT's kernels after step_kernel read the done flags and rescale the reward, they leave the rows alone)
     const char* fz = getenv("H12_FUSE_OBS");
-    h->fuse = !h->P.cat && !(fz && fz[0] == '0');
+    h->fuse = !(fz && fz[0] == '0');
     if (h->fuse) {
       const std::vector<uint8_t> c = fuse_code_table(h->P.hist);
       e = hipMalloc(&h->fuse_code, c.size());
@@ -4041,21 +4041,21 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
             A.fuse ? sizeof(FuseLds) : 0, st, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
+  if (h->P.cat) {
+    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, st, h->P, h->W.n);
+    HIP_TRY(hipGetLastError());
+    static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
+    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
+    hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0, st, h->P,
+                       h->W, C);
+    HIP_TRY(hipGetLastError());
+  }
   if (A.fuse) {
     // the rows are stored; the log partials are folded later (log_flush_kernel: a full ring, a reused accumulator,
     // h12env_flush_log)
     if (out->log_acc) h->pend_acc[h->n_pend++] = out->log_acc;
     timing_next(h);  // no second kernel unless a fold was flushed above
     return 0;
-  }
-  if (h->P.cat) {
-    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, (hipStream_t)stream, h->P, h->W.n);
-    HIP_TRY(hipGetLastError());
-    static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
-    CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
-    hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0,
-                       (hipStream_t)stream, h->P, h->W, C);
-    HIP_TRY(hipGetLastError());
   }
   t0 = t1 = nullptr;
   if (!flushed && !pair1_taken(h)) timing_events(h, 1, &t0, &t1);

@@ -342,8 +342,8 @@ int h12env_step(h12env* h, const float* actions, const float* obs_prev, const h1
 /* (ABI 9) Complete every deferred episode-log addition of earlier h12env_step calls (one kernel on stream; nothing
  * when none is pending).  Call it before reading a step's log_acc. */
 int h12env_flush_log(h12env* h, void* stream);
-/* (ABI 9) 1 when h12env_step assembles the observation rows inside the env kernel (Flat / Rsl layouts without CaT,
- * 16-byte aligned obs / obs_prev; environment variable H12_FUSE_OBS=0 at h12env_create selects the two-kernel
+/* (ABI 9) 1 when h12env_step assembles the observation rows inside the env kernel (history layouts -- Flat, Rsl,
+ * CaT -- with 16-byte aligned obs / obs_prev; environment variable H12_FUSE_OBS=0 at h12env_create selects the two-kernel
  * path), else 0.  Results are bit-identical either way; the kernel timing / cost pairs name different kernels. */
 int h12env_obs_fused(const h12env* h);
 /* ObservationManager.compute() outside step(): appends one frame of the current state to every

@@ -4,8 +4,9 @@ log_flush_kernel) against the two-kernel step path (obs_assemble_kernel; H12_FUS
 bit: observation rows, rewards, done flags and the episode log, over steps with resets.  Covers both fused variants --
 the spread path (whole blocks; the shifted-row stores split over the physics steps after the first: 3 of 4, and 2 of 3
 at decimation 3) and the after-the-loop path (the ragged last block of 37 / 300 envs) -- with and without the
-self-contact wave (64 or 128 helper lanes), Flat (history 10) and Rsl (history 6); logs read right after their step
-and 100+ steps later (after env.py's chunk flushes)."""
+self-contact wave (64 or 128 helper lanes), Flat (history 10), Rsl (history 6) and CaT (its kernels after step_kernel
+rescale the reward and add their constraint statistics to the same deferred log partials); logs read right after
+their step and 100+ steps later (after env.py's chunk flushes)."""
 import os
 
 import pytest
@@ -48,6 +49,7 @@ CASES = [
     ("rsl", 64, {}),
     ("flat", 96, {"self_collision": False}),
     ("flat", 64, {"decimation": 3}),
+    ("cat", 128, {}),
 ]
 
 
@@ -62,9 +64,9 @@ def _same_log(t, la, lb):
                                                   for t, n, kw in CASES])
 def test_fused_assembly_equals_two_kernel_path(gpu, task, n, kw):
     from h12env import H12FlatEnvCfg
-    from h12env.cfg import H12RslEnvCfg
+    from h12env.cfg import H12CaTEnvCfg, H12RslEnvCfg
 
-    cfg_fn = H12FlatEnvCfg if task == "flat" else H12RslEnvCfg
+    cfg_fn = {"flat": H12FlatEnvCfg, "rsl": H12RslEnvCfg, "cat": H12CaTEnvCfg}[task]
     kw = dict(kw)
     steps = kw.pop("steps", 40)
     a_env, b_env = _make(cfg_fn, n, True, **kw), _make(cfg_fn, n, False, **kw)
@@ -78,8 +80,10 @@ def test_fused_assembly_equals_two_kernel_path(gpu, task, n, kw):
         ob, rb, tb, ub, eb = b_env.step(act)
         pa, pb = oa["policy"], ob["policy"]
         assert torch.equal(pa.view(torch.int32), pb.view(torch.int32)), (t, (pa != pb).nonzero()[:5])
+        # CaT returns the constraint termination probability as its dones
         assert torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(ua, ub), t
-        resets += int((ta | ua).sum())
+        assert torch.equal(a_env.reset_terminated, b_env.reset_terminated), t
+        resets += int((a_env.reset_terminated | a_env.reset_time_outs).sum())
         logs.append((ea["log"], eb["log"]))
         if t % 10 == 9:  # read now (a flush of the pending folds), the others at the end (deferred over >= 64 steps)
             _same_log(t, *logs[-1])
