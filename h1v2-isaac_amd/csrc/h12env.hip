@@ -318,8 +318,9 @@ H12_DEV void impl_force(const float* a, const float* p, const float* u, float be
 // axes; positions are env-local on terrain, see ground_local); mus / mud: Coulomb
 // coefficients of this contact (per-env sole friction or the config's).  With P.impl, ic receives the
 // added point inertia of the contact (oracle contact_point) and f the force that cancels its weight
-// under the gravity-as-base-acceleration formulation.
-template <bool ANCHOR, bool TERRAIN>
+// under the gravity-as-base-acceleration formulation.  EXPL: the force only (its implicit part -- the added point
+// inertia and its weight -- left out; the torso face's secondary corners, torso_face).
+template <bool ANCHOR, bool TERRAIN, bool EXPL = false>
 H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
                             const float* pl, float rad, float* f, float* fw, float* anc, bool was_in, float sg,
                             const float* org, float mus, float mud, ImplC& ic) {
@@ -378,7 +379,7 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   }
   float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
   if constexpr (TERRAIN) { Fw[0] += fn * nrm[0]; Fw[1] += fn * nrm[1]; Fw[2] = fn * nrm[2]; }
-  if (P.impl) {
+  if (P.impl && !EXPL) {
     const float h = P.h;
     const float alpha = h * P.cc;
     const float beta = stick ? h * (ANCHOR ? P.fc : P.fc_v) : 0.f;
@@ -852,8 +853,8 @@ H12_DEV SelfLds& self_lds() {
 // self-contact anywhere in the wave).  Phase 2 (self_finish): the pair jobs and each lane's wrenches.  Rk/pk, vk:
 // knee pose (lane frame) and body velocity, Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP
 // swap; wave-uniform at every wave_sync.
-H12_DEV uint64_t self_stage(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
-                            const float (&Rf)[3][3], const float* pf, const float* vf) {
+H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
+                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
   SelfLds& L = self_lds();
   const float sg = leg ? -1.f : 1.f;
   // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
@@ -882,7 +883,7 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, const float (&Rk)[3][3], 
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
   {
     float4* g = L.geo[el][leg];
-    g[SG_KNEE] = make_float4(k0[0], k0[1], k0[2], 0.f);
+    g[SG_KNEE] = make_float4(k0[0], k0[1], k0[2], mu);  // w: this leg's (sole) dynamic friction coefficient
     g[SG_KNEE + 1] = make_float4(k1[0], k1[1], k1[2], 0.f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -935,6 +936,10 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
     if (!((fl >> (2 * (i > 0) + (j > 0))) & 1)) continue;
     const float4* gl = L.geo[e][0];
     const float4* gr = L.geo[e][1];
+    // Coulomb cap: material multiply combine (PhysX friction_combine_mode 'multiply').  With the startup material
+    // randomisation (randomize_rigid_body_material, C12/rsl_env_cfg.py:213-223, T/.../cat_env_cfg.py:236) it is
+    // the product of the two legs' randomised coefficients, otherwise the fixed 0.6 x 0.6 (self_mu)
+    const float smu = P.env_mu ? gl[SG_KNEE].w * gr[SG_KNEE].w : P.smu;
     const float4 la = gl[i == 0 ? SG_KNEE : SG_ROD + 2 * (i - 1)], lb = gl[i == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (i - 1) + 1];
     const float4 ra = gr[j == 0 ? SG_KNEE : SG_ROD + 2 * (j - 1)], rb = gr[j == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (j - 1) + 1];
     const float pa[3] = {la.x, la.y, la.z}, pb[3] = {lb.x, lb.y, lb.z}, qa[3] = {ra.x, ra.y, ra.z}, qb[3] = {rb.x, rb.y, rb.z};
@@ -970,7 +975,7 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
       if (!(fn > 0.f)) continue;
       float F[3];
       for (int a = 0; a < 3; ++a) F[a] = -sp.w * P.sct * (vrel[a] - vn * n[a]);
-      const float ftn2 = dot3(F, F), cap = P.smu * fn;
+      const float ftn2 = dot3(F, F), cap = smu * fn;
       if (ftn2 > cap * cap) { const float sc = cap * __builtin_amdgcn_rsqf(ftn2); F[0] *= sc; F[1] *= sc; F[2] *= sc; }
       for (int a = 0; a < 3; ++a) F[a] += fn * n[a];
       float m[3];
@@ -1000,9 +1005,10 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   wave_sync();  // the staging area is rewritten by the next physics step
 }
 
-H12_DEV void self_contacts(const KParams& P, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
-                           const float (&Rf)[3][3], const float* pf, const float* vf, float* wk, float* wf, Forces& fr) {
-  const uint64_t act = self_stage(P, leg, Rk, pk, vk, Rf, pf, vf);
+H12_DEV void self_contacts(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
+                           const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf, float* wk,
+                           float* wf, Forces& fr) {
+  const uint64_t act = self_stage(P, leg, mu, Rk, pk, vk, Rf, pf, vf);
   self_finish(P, leg, act, Rk, pk, Rf, pf, wk, wf, fr);
 }
 
@@ -1133,7 +1139,7 @@ H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
                  b.vlin[0], b.vlin[1], b.vlin[2], b.wang[0], b.wang[1], b.wang[2]};
   for (int k = 0; k < NL; ++k) { x[13 + k] = lg.q[k]; x[19 + k] = lg.qd[k]; }
   x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
-  x[28] = lg.dmass; x[29] = x[30] = x[31] = 0.f;
+  x[28] = lg.dmass; x[29] = lg.mud; x[30] = x[31] = 0.f;
   put4(help_lds().st, l, x, 8);
 }
 
@@ -1265,6 +1271,32 @@ H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], c
   contact_sphere<false, Feat<K>::terrain>(P, Rk, pk, vk, pl, h12m::KNEE_R, fext_knee, rep, dummy, false, sg, org, P.mus,
                                           P.mud, ick);
 }
+// Torso box (URDF box collider h12_12dof.urdf:387, welded to the pelvis) on the ground: the lowest corner is the
+// implicit contact (torso_corner, contact_sphere); the other three corners of the lowest face -- the face whose
+// normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso lying on a
+// face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same order).
+H12_DEV void torso_corner(const float (&R0)[3][3], float* corner) {
+  for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+}
+template <bool TERRAIN>
+H12_DEV void torso_face(const KParams& P, const float (&R0)[3][3], const float* pb0, const float* v0, const float* org,
+                        float* f, float* fw) {
+  const float z0 = fabsf(R0[2][0]), z1 = fabsf(R0[2][1]), z2 = fabsf(R0[2][2]);
+  const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
+  const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;  // the face's two in-plane axes
+  for (int k = 1; k < 4; ++k) {
+    float p[3];
+    for (int a = 0; a < 3; ++a) {
+      const bool flip = ((k & 1) && a == ab) || ((k & 2) && a == ac);
+      const bool neg = (R0[2][a] > 0.f) != flip;
+      p[a] = h12m::TORSO_C[a] + (neg ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+    }
+    ImplC dz;
+    float dummy[2];
+    contact_sphere<false, TERRAIN, true>(P, R0, pb0, v0, p, 0.f, f, fw, dummy, false, 1.f, org, P.mus, P.mud, dz);
+  }
+}
+
 // rigid body of the base (with the added torso mass): inertia Rg and bias force v x* (Rg v) (pelvis coords)
 template <int K>
 H12_DEV void base_body(const KParams& P, const Leg& lg, const float* v0, AInertia& Rg, float* pb) {
@@ -1294,6 +1326,7 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
   float x[32];
   get4(help_lds().st, l, x, 8);
   lg.dmass = x[28];
+  lg.mud = x[29];
   for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; org[i] = x[25 + i]; }
   for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
   for (int k = 0; k < NL; ++k) { lg.q[k] = x[13 + k]; lg.qd[k] = x[19 + k]; }
@@ -1367,11 +1400,12 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
       float t[16] = {};
       if (leg == 0) {
         float corner[3];
-        for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+        torso_corner(R0, corner);
         ImplC ict;
         float dummy[2];
         const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
                                                                org, P.mus, P.mud, ict);
+        torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
         t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
         t[14] = c ? 1.f : 0.f;
       }
@@ -1400,7 +1434,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       get_state(l, b, lg, org);
       float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
-      act = self_stage(P, leg, Rk, pk, v[3], R, p, v[5]);
+      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);
     }
     __syncthreads();  // R1
     if (active) {
@@ -1522,7 +1556,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       Forces fs = {};
       const float pbl[3] = {pb0[0], sg * pb0[1], pb0[2]};
       const float pkr[3] = {pk[0] - pbl[0], pk[1] - pbl[1], pk[2] - pbl[2]}, pr[3] = {p[0] - pbl[0], p[1] - pbl[1], p[2] - pbl[2]};
-      self_contacts(P, leg, Rk, pkr, v[3], R, pr, v[5], wk, wf, fs);
+      self_contacts(P, leg, lg.mud, Rk, pkr, v[3], R, pr, v[5], wk, wf, fs);
     }
   }
   PHX(13);
@@ -1551,7 +1585,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   if (leg == 0) {
     ai_add(IA, Rg);
     for (int i = 0; i < 6; ++i) pAcc[i] += pbase[i];
-    for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+    torso_corner(R0, corner);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     bool c;
     if constexpr (HW) {  // evaluated by the helper wave before R2
@@ -1565,6 +1599,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       float dummy[2];
       c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
                                                    P.mus, P.mud, ict);
+      torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
     }
     if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
@@ -3011,7 +3046,7 @@ __global__ void __launch_bounds__(BLOCK) selfc_kernel(KParams P, Workspace W, fl
   link_pass1<5>(s.lg, cs, v[4], v, R, p);
   float wk[6], wf[6];
   Forces fr = {};
-  self_contacts(P, leg, Rk, pk, v[3], R, p, v[5], wk, wf, fr);
+  self_contacts(P, leg, s.lg.mud, Rk, pk, v[3], R, p, v[5], wk, wf, fr);
   float* o = out + ((size_t)e * 2 + leg) * 12;
   for (int a = 0; a < 3; ++a) {  // lane body frame -> real body frame (force M f, moment sg M m)
     o[a] = sg * mm[a] * wk[a]; o[3 + a] = mm[a] * wk[3 + a];

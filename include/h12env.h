@@ -251,7 +251,8 @@ typedef struct h12env_config {
    * illegal knee contact). */
   int32_t self_collision;
   float self_k, self_c;        /* normal stiffness [N/m], damping [N s/m] */
-  float self_ct, self_mu;      /* tangential damping [N s/m], Coulomb cap (0.6 x 0.6, material multiply) */
+  float self_ct, self_mu;      /* tangential damping [N s/m], Coulomb cap (0.6 x 0.6, material multiply; with
+                                  per_env_friction: left x right leg H12_F_MU dynamic coefficient) */
   /* ABI 8: hard joint limits (PhysX holds the URDF ranges, A/robots/h12.py:18-35).  The stiff implicit limit spring
    * (limit_k, activated on the predicted end-of-step position) stops a joint at its range inside the solve, with
    * the reaction on the whole articulation; a joint that other forces (a foot slammed into the ground) still carry

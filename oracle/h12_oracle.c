@@ -332,6 +332,7 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   double dcap = (hi > 0 && c->max_depenetration_velocity > 0 && anc_out && !was_in) ? hi * c->max_depenetration_velocity
                                                                                      : 1e300;
   double fn = c->contact_k * (depth < dcap ? depth : dcap) - cn * vn;
+  /* Madd == NULL: the force only, without its implicit part (the torso face's secondary corners) */
   if (dj != 0.0) {
     if (c->contact_k * (depth + dj < dcap ? depth + dj : dcap) - cn * vn <= 0) return 0;
     if (fn < 0) fn = 0;
@@ -363,7 +364,7 @@ static int contact_point(const h12env_config* c, const kin_t* k, int b, const do
   }
   /* normal force along the ground normal, tangential (stiction / drag) force in world xy */
   double F[3] = {ft0 + fn * nrm[0], ft1 + fn * nrm[1], fn * nrm[2]}, fl[3], nl[3];
-  if (hi > 0) {
+  if (hi > 0 && Madd) {
     /* world mass tensor Mw = alpha n n^T + beta (I - n n^T) -> body coords Mb = R^T Mw R; point inertia at
      * pl: [[-px Mb px, px Mb], [-Mb px, Mb]].  The dynamics run with gravity as a base acceleration, which
      * would weigh the added inertia: cancel with the force g Mw e_z at the point. */
@@ -524,8 +525,12 @@ static void apply_world_force(const kin_t* k, int b, const double x[3], const do
   for (int a = 0; a < 3; ++a) { fext[b][a] += nb[a]; fext[b][3 + a] += fb[a]; }
 }
 
-static void self_contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, double fext[NB][6],
-                          orc_contact_report* rr) {
+static void self_contacts(const h12env_model* m, const h12env_config* c, const kin_t* k, const orc_phys* s,
+                          double fext[NB][6], orc_contact_report* rr) {
+  /* Coulomb cap of the leg-leg pairs: PhysX multiply combine of the two bodies' materials -- with the startup
+   * material randomisation (randomize_rigid_body_material, C12/rsl_env_cfg.py:213-223) the product of the two
+   * legs' randomised dynamic coefficients, otherwise the fixed 0.6 x 0.6 (self_mu) */
+  const double smu = (c->per_env_friction && s->env_params) ? s->mu[0][1] * s->mu[1][1] : c->self_mu;
   capsule_w cap[2][5]; /* per leg: knee, then the four sole rods */
   for (int f = 0; f < 2; ++f) {
     capsule_world(k, 6 * f + 4, m->knee_p0, m->knee_p1, m->knee_radius, &cap[f][0]);
@@ -560,7 +565,7 @@ static void self_contacts(const h12env_model* m, const h12env_config* c, const k
         if (!(fn > 0.0)) continue;
         double ft[3];
         for (int a = 0; a < 3; ++a) ft[a] = -sp.w * c->self_ct * (vr[a] - vn * n[a]);
-        const double ftn = sqrt(dot3(ft, ft)), cap_t = c->self_mu * fn;
+        const double ftn = sqrt(dot3(ft, ft)), cap_t = smu * fn;
         if (ftn > cap_t) for (int a = 0; a < 3; ++a) ft[a] *= cap_t / ftn;
         double F[3], Fm[3];
         for (int a = 0; a < 3; ++a) { F[a] = fn * n[a] + ft[a]; Fm[a] = -F[a]; }
@@ -610,7 +615,24 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
   }
   contact_point(c, k, 0, corner, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic, hi, Madd,
                 m->gravity, rec);
-  if (c->self_collision) self_contacts(m, c, k, fext, rr);
+  /* the other three corners of the lowest face (normal: the box axis closest to the vertical), explicit forces
+   * only -- a torso lying on a face or an edge rests on that face's corners (kernel torso_face, same order) */
+  {
+    const double z0 = fabs(k->R[0][2][0]), z1 = fabs(k->R[0][2][1]), z2 = fabs(k->R[0][2][2]);
+    const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
+    const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;
+    for (int q = 1; q < 4; ++q) {
+      double pc[3];
+      for (int a = 0; a < 3; ++a) {
+        const int flip = ((q & 1) && a == ab) || ((q & 2) && a == ac);
+        const int neg = (k->R[0][2][a] > 0) != flip;
+        pc[a] = m->torso_center[a] + (neg ? -1.0 : 1.0) * m->torso_half[a];
+      }
+      contact_point(c, k, 0, pc, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic, hi, NULL,
+                    m->gravity, NULL);
+    }
+  }
+  if (c->self_collision) self_contacts(m, c, k, s, fext, rr);
   if (next_mask) *next_mask = mask;
 }
 
@@ -885,7 +907,7 @@ int orc_self_contacts(const h12env_model* m, const h12env_config* c, const orc_p
   kinematics(m, s, &k);
   memset(fext, 0, sizeof(double) * NB * 6);
   memset(rep, 0, sizeof *rep);
-  self_contacts(m, c, &k, (double(*)[6])fext, rep);
+  self_contacts(m, c, &k, s, (double(*)[6])fext, rep);
   return 0;
 }
 

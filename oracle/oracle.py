@@ -284,9 +284,13 @@ def mass_matrix(model, state):
     return M
 
 
-def self_contacts(model, cfg, state):
-    """Self-contact wrenches between the legs (body-coordinate spatial forces, (13, 6)) and the report."""
+def self_contacts(model, cfg, state, mu=None):
+    """Self-contact wrenches between the legs (body-coordinate spatial forces, (13, 6)) and the report.  mu: the
+    env's randomised (static, dynamic) friction of the left and right sole (4 values; cfg.per_env_friction)."""
     s = Phys.from_numpy(state)
+    if mu is not None:
+        s.env_params = 1
+        s.mu[:] = [float(x) for x in mu]
     f = np.zeros(13 * 6)
     rep = Report()
     lib().orc_self_contacts(C.byref(model), C.byref(cfg), C.byref(s), _d(f), C.byref(rep))

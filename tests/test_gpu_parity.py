@@ -302,3 +302,49 @@ def test_episode_length_buf_writable_truncation(gpu):
     assert trunc.all()
     assert (env.episode_length_buf == 0).all()
     env.close()
+
+
+def test_torso_face_contacts_forced(gpu):
+    """Robots lying on the torso box (h12_12dof.urdf:387): pitched 70-110 deg onto the chest or the back, random
+    yaw and roll within +-20 deg, the lowest box corner 0-4 mm below the floor -- the lowest face's corners (the
+    implicit lowest corner plus the explicit others, helper wave before R2) carry the torso and trip the illegal
+    torso contact (C12/rough_env_cfg.py:95-109).  Two teacher-forced MDP steps against the oracle."""
+    from forced import ForcedParity
+
+    n = 1024
+    env = make(n, H12FlatEnvCfg())
+    env.reset()
+    rng = np.random.default_rng(77)
+    Fm = env._fstate.cpu().numpy().copy()
+    ch = np.array(env._model.torso_center, dtype=np.float64)
+    hh = np.array(env._model.torso_half, dtype=np.float64)
+    signs = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], dtype=np.float64)
+    for i in range(n):
+        pitch = rng.uniform(np.deg2rad(70), np.deg2rad(110)) * (1 if i % 2 else -1)
+        roll, yaw = rng.uniform(-0.35, 0.35), rng.uniform(-np.pi, np.pi)
+        cy, sy_, cp, sp, cr, sr = np.cos(yaw / 2), np.sin(yaw / 2), np.cos(pitch / 2), np.sin(pitch / 2), \
+            np.cos(roll / 2), np.sin(roll / 2)
+        quat = np.array([cr * cp * cy + sr * sp * sy_, sr * cp * cy - cr * sp * sy_, cr * sp * cy + sr * cp * sy_,
+                         cr * cp * sy_ - sr * sp * cy])
+        s = np.zeros(37)
+        s[3:7] = quat
+        s[13:25] = np.asarray(env._model.q_default) + rng.normal(size=12) * 0.05
+        R, p = O.body_poses(env._model, s)
+        z = (R[0] @ (ch[None] + signs * hh[None]).T)[2] + p[0][2]
+        Fm[FIELDS["POS"][0]:FIELDS["POS"][0] + 3, i] = [rng.uniform(-1, 1), rng.uniform(-1, 1),
+                                                        -z.min() - rng.uniform(0.0, 0.004)]
+        Fm[FIELDS["QUAT"][0]:FIELDS["QUAT"][0] + 4, i] = quat
+        Fm[FIELDS["VLIN"][0]:FIELDS["VLIN"][0] + 6, i] = rng.normal(size=6) * 0.1
+        Fm[FIELDS["Q"][0]:FIELDS["Q"][0] + 12, i] = s[13:25]
+        Fm[FIELDS["QD"][0]:FIELDS["QD"][0] + 12, i] = 0.0
+    env._fstate.copy_(torch.from_numpy(Fm))
+    fp = ForcedParity(env, seed=77)
+    terms = 0
+    for t in range(2):
+        a = (rng.normal(size=(n, 12)) * 0.3).astype(np.float32)
+        (_, _, _, rew, _, _), (_, _, _, _, to, _, _), _, _ = fp.step(a)
+        assert np.isfinite(rew).all()
+        terms += int(to.sum())
+    fp.check()
+    assert terms > n // 2, terms  # the torso contact is an illegal contact
+    env.close()

@@ -123,13 +123,21 @@ def test_self_collision_mdp_forced_knee_contacts_terminate(gpu):
     env.close()
 
 
-def test_self_contact_wrenches_match_oracle(gpu):
+@pytest.mark.parametrize("task", ["flat", "rsl"])
+def test_self_contact_wrenches_match_oracle(gpu, task):
     """The kernel's self-contact wrenches (h12env_eval_self_contacts) on crossed states against the oracle's
     self_contacts, body by body: no dynamics in between, so this pins the contact geometry, law and the
-    mirror-lane frame conversions directly."""
+    mirror-lane frame conversions directly.  rsl: the startup material randomisation is on
+    (C12/rsl_env_cfg.py:213-223), so each env's leg-leg Coulomb cap is the product of its two legs' randomised
+    dynamic coefficients (H12_F_MU) instead of the fixed 0.6 x 0.6."""
+    from h12env.cfg import H12RslEnvCfg
+
     n = 2048
-    env = make(n)
+    env = make(n, H12RslEnvCfg() if task == "rsl" else None)
     env.reset()
+    mu = env._fstate[FIELDS["MU"][0]:FIELDS["MU"][0] + 4].cpu().numpy().astype(np.float64) if task == "rsl" else None
+    if task == "rsl":
+        assert env._ccfg.per_env_friction == 1 and mu.std(axis=1).min() > 0.1
     rng = np.random.default_rng(43)
     Fm = crossed_states(env, rng, 1.0, roll=(-0.4, -0.1), qd=2.0)
     env._fstate.copy_(torch.from_numpy(Fm))
@@ -140,7 +148,7 @@ def test_self_contact_wrenches_match_oracle(gpu):
     for i in range(n):
         s = np.zeros(37)
         s[0:37] = Fm[0:37, i]
-        f, _ = O.self_contacts(env._model, env._ccfg, s)
+        f, _ = O.self_contacts(env._model, env._ccfg, s, None if mu is None else mu[:, i])
         hit += np.abs(f).max() > 0
         scale = max(1.0, np.abs(f).max())
         worst.append(max(np.abs(g[i, leg, b] - f[body]).max() / scale for leg, b, body in bodies))
@@ -156,7 +164,7 @@ def test_self_contact_wrenches_match_oracle(gpu):
         for k, eps in enumerate((1e-7,) * 32 + (3e-7,) * 32 + (1e-6,) * 32):
             O.set_self_jitter(eps, 1000 + k)
             try:
-                f, _ = O.self_contacts(env._model, env._ccfg, s)
+                f, _ = O.self_contacts(env._model, env._ccfg, s, None if mu is None else mu[:, i])
             finally:
                 O.set_self_jitter(0.0)
             scale = max(1.0, np.abs(f).max())

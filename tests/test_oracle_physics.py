@@ -245,3 +245,25 @@ def test_implicit_single_step_is_stable_under_random_actions(model):
         env.step(rng.normal(size=(n, 12)).astype(np.float32), t, n_threads=4)
     assert np.isfinite(env.F).all()
     assert np.abs(env.F[25:37]).max() < 200.0  # joint velocities stay physical
+
+
+def test_torso_box_rests_on_its_lowest_face(model):
+    """The torso box collider (h12_12dof.urdf:387) lying on a face is carried by the face's four corners (the
+    lowest corner through the implicit contact, the other three explicitly): with the
+    explicit integrator's forces and the robot at rest, the reported torso force is k x the summed depths of the
+    corners below the floor, and an edge (box tilted about the face's long axis) is carried by two corners."""
+    c = H12FlatEnvCfg().to_c()
+    c.self_collision = 0
+    ch, hh = np.array(model.torso_center, dtype=np.float64), np.array(model.torso_half, dtype=np.float64)
+    signs = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], dtype=np.float64)
+    for ang, n_expect in ((np.pi / 2, 4), (np.pi / 2 + 0.05, 2)):
+        s = np.zeros(37)
+        s[3:7] = [np.cos(ang / 2), 0.0, np.sin(ang / 2), 0.0]  # pitched forward onto the chest face
+        s[13:25] = np.asarray(model.q_default)
+        R, p = O.body_poses(model, s)
+        z = (R[0] @ (ch[None] + signs * hh[None]).T)[2] + p[0][2]
+        s[2] = -z.min() - 0.002  # the lowest corner 2 mm below the floor
+        depth = np.clip(-(z + s[2]), 0.0, None)
+        assert (depth > 0).sum() == n_expect
+        _, rep = O.forward_dynamics(model, c, s, np.zeros(12), algo=1, dt_impl=0.0, contact=True)
+        np.testing.assert_allclose(rep.torso_force[2], c.contact_k * depth.sum(), rtol=1e-9)

@@ -155,3 +155,26 @@ def test_self_jitter_hook(model):
     np.testing.assert_array_equal(f2, f0)
     d = np.abs(f1 - f0).max()
     assert 0.0 < d < 10 * c.self_k * 1e-6
+
+
+def test_self_friction_follows_randomised_materials(model):
+    """With the startup material randomisation (C12/rsl_env_cfg.py:213-223) the leg-leg Coulomb cap is the
+    product of the two legs' randomised dynamic coefficients (PhysX multiply combine), not the fixed 0.6 x 0.6."""
+    c = H12FlatEnvCfg().to_c()
+    s = crossed_state(model, -0.25)
+    s[13:25] += np.random.default_rng(3).normal(size=12) * 0.05  # a generic crossing (test_self_jitter_hook)
+    s[25:37] = np.random.default_rng(11).normal(size=12) * 4.0  # sliding: the tangential drag reaches its cap
+    f_fixed, _ = O.self_contacts(model, c, s)
+    assert np.abs(f_fixed).max() > 0
+    c.per_env_friction = 1
+    f_same, _ = O.self_contacts(model, c, s, mu=[0.6, 0.6, 0.6, 0.6])
+    np.testing.assert_allclose(f_same, f_fixed, rtol=1e-6, atol=1e-9)  # self_mu is the fp32 0.36
+    f_low, _ = O.self_contacts(model, c, s, mu=[0.1, 0.1, 0.2, 0.2])
+    f_nofric, _ = O.self_contacts(model, c, s, mu=[0.0, 0.0, 0.0, 0.0])
+    # the frictionless wrenches are the normal forces alone; a lower cap moves the result towards them
+    assert np.abs(f_low - f_fixed).max() > 1e-3 * np.abs(f_fixed).max()
+    assert np.abs(f_low - f_nofric).max() < np.abs(f_fixed - f_nofric).max()
+    # without the randomisation flag the per-env values are ignored
+    c.per_env_friction = 0
+    f_off, _ = O.self_contacts(model, c, s, mu=[0.1, 0.1, 0.2, 0.2])
+    np.testing.assert_array_equal(f_off, f_fixed)
