@@ -1272,9 +1272,10 @@ H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], c
                                           P.mud, ick);
 }
 // Torso box (URDF box collider h12_12dof.urdf:387, welded to the pelvis) on the ground: the lowest corner is the
-// implicit contact (torso_corner, contact_sphere); the other three corners of the lowest face -- the face whose
-// normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso lying on a
-// face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same order).
+// implicit contact (torso_corner, contact_sphere); while it touches, the other three corners of the lowest face --
+// the face whose normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso
+// lying on a face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same
+// order).  Evaluated by the helper wave before barrier R1 (helper_wave).
 H12_DEV void torso_corner(const float (&R0)[3][3], float* corner) {
   for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
 }
@@ -1284,6 +1285,8 @@ H12_DEV void torso_face(const KParams& P, const float (&R0)[3][3], const float* 
   const float z0 = fabsf(R0[2][0]), z1 = fabsf(R0[2][1]), z2 = fabsf(R0[2][2]);
   const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
   const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;  // the face's two in-plane axes
+  // not unrolled: one copy of the contact code in the helper wave's loop
+#pragma unroll 1
   for (int k = 1; k < 4; ++k) {
     float p[3];
     for (int a = 0; a < 3; ++a) {
@@ -1342,6 +1345,27 @@ H12_DEV int step_block() { return blockIdx.x; }
 H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
 #endif
 
+// The helper wave's torso-box ground contact (lane 0 of each pair): the lowest corner's implicit contact and, while it
+// touches, the face's other corners (torso_face) -> H.torso for the physics wave's base combine after R2.
+template <int K>
+H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const float* vb, const float (&R0)[3][3],
+                          const float* pb0, const float* org) {
+  float t[16] = {};
+  if (leg == 0) {
+    const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+    float corner[3];
+    torso_corner(R0, corner);
+    ImplC ict;
+    float dummy[2];
+    const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
+                                                           org, P.mus, P.mud, ict);
+    if (c) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
+    t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
+    t[14] = c ? 1.f : 0.f;
+  }
+  put4(help_lds().torso, l, t, 4);
+}
+
 template <int K>
 H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi, const FuseCtx& fc) {
   const int l = threadIdx.x - BLOCK;
@@ -1382,8 +1406,13 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
       knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt + 12, jt + 18, ick, jt[26]);
       jt[21] = ick.beta; jt[22] = ick.gamma; jt[23] = ick.u[0]; jt[24] = ick.u[1]; jt[25] = ick.u[2]; jt[27] = 0.f;
       put4(H.jt, l, jt, 9);
+      // torso-box ground contact (the base body; lane 0 of the pair) from the step's state: data-dependent work
+      // (a fallen robot's) kept off the physics wave's chain.  On terrain before R1 (the R1 -> R2 window is then the
+      // helper's critical one: its ground lookups cost Rough / C5 2.7 us per step there), on flat ground after R1
+      // (there the window before R1 is: 1.1 us per step)
+      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
     }
-    __syncthreads();  // R1: joint terms, knee contact
+    __syncthreads();  // R1: joint terms, knee contact (terrain: torso contact)
     if (active) {
       float pb[NL][6], o[44];
       leg_bias(v, pb);
@@ -1395,24 +1424,10 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
       if (leg) for (int i = 36; i < 42; ++i) o[i] = 0.f;
       o[42] = o[43] = 0.f;
       put4(H.bias, l, o, 11);
-      // torso-box corner contact (the base body; lane 0 of the pair) from the step's state: data-dependent work
-      // (a fallen robot's) kept off the physics wave's chain
-      float t[16] = {};
-      if (leg == 0) {
-        float corner[3];
-        torso_corner(R0, corner);
-        ImplC ict;
-        float dummy[2];
-        const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
-                                                               org, P.mus, P.mud, ict);
-        torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
-        t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
-        t[14] = c ? 1.f : 0.f;
-      }
-      put4(H.torso, l, t, 4);
+      if constexpr (!Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
     }
     fuse_drain(fc, it);
-    __syncthreads();  // R2: bias forces, torso contact
+    __syncthreads();  // R2: bias forces (flat: torso contact)
     fuse_early(fc, it, n_steps, l, blockDim.x - BLOCK);
   }
 }
@@ -1599,7 +1614,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       float dummy[2];
       c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
                                                    P.mus, P.mud, ict);
-      torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
+      if (c) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
     }
     if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
