@@ -1272,10 +1272,11 @@ H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], c
                                           P.mud, ick);
 }
 // Torso box (URDF box collider h12_12dof.urdf:387, welded to the pelvis) on the ground: the lowest corner is the
-// implicit contact (torso_corner, contact_sphere); while it touches, the other three corners of the lowest face --
+// implicit contact (torso_corner, contact_sphere); the other three corners of the lowest face (on terrain only while
+// the lowest corner touches: their heightfield lookups stay off a standing robot's helper wave) --
 // the face whose normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso
 // lying on a face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same
-// order).  Evaluated by the helper wave before barrier R1 (helper_wave).
+// order).  Evaluated by the helper wave (helper_torso: before R1 on terrain, between R1 and R2 on flat ground).
 H12_DEV void torso_corner(const float (&R0)[3][3], float* corner) {
   for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
 }
@@ -1285,9 +1286,7 @@ H12_DEV void torso_face(const KParams& P, const float (&R0)[3][3], const float* 
   const float z0 = fabsf(R0[2][0]), z1 = fabsf(R0[2][1]), z2 = fabsf(R0[2][2]);
   const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
   const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;  // the face's two in-plane axes
-  // not unrolled: one copy of the contact code in the helper wave's loop
-#pragma unroll 1
-  for (int k = 1; k < 4; ++k) {
+  auto corner_k = [&](int k) {
     float p[3];
     for (int a = 0; a < 3; ++a) {
       const bool flip = ((k & 1) && a == ab) || ((k & 2) && a == ac);
@@ -1297,6 +1296,13 @@ H12_DEV void torso_face(const KParams& P, const float (&R0)[3][3], const float* 
     ImplC dz;
     float dummy[2];
     contact_sphere<false, TERRAIN, true>(P, R0, pb0, v0, p, 0.f, f, fw, dummy, false, 1.f, org, P.mus, P.mud, dz);
+  };
+  if constexpr (TERRAIN) {  // one copy of the heightfield contact code in the helper wave's loop
+#pragma unroll 1
+    for (int k = 1; k < 4; ++k) corner_k(k);
+  } else {
+#pragma unroll
+    for (int k = 1; k < 4; ++k) corner_k(k);
   }
 }
 
@@ -1359,7 +1365,11 @@ H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const
     float dummy[2];
     const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
                                                            org, P.mus, P.mud, ict);
-    if (c) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
+#ifdef H12_EXP_NOGATE
+    torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
+#else
+    if (c || !Feat<K>::terrain) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
+#endif
     t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
     t[14] = c ? 1.f : 0.f;
   }
@@ -1614,7 +1624,11 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       float dummy[2];
       c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
                                                    P.mus, P.mud, ict);
-      if (c) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
+#ifdef H12_EXP_NOGATE
+      torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
+#else
+      if (c || !Feat<K>::terrain) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
+#endif
     }
     if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];

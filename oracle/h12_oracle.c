@@ -613,11 +613,12 @@ static void contacts(const h12env_model* m, const h12env_config* c, const kin_t*
     double sg = k->R[0][2][a] > 0 ? -1.0 : 1.0;
     corner[a] = m->torso_center[a] + sg * m->torso_half[a];
   }
-  /* while it touches, the other three corners of the lowest face (normal: the box axis closest to the vertical),
-   * explicit forces only -- a torso lying on a face or an edge rests on that face's corners (kernel torso_face, same
-   * gate, same order) */
-  if (contact_point(c, k, 0, corner, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic, hi, Madd,
-                    m->gravity, rec)) {
+  /* the other three corners of the lowest face (normal: the box axis closest to the vertical), explicit forces
+   * only -- a torso lying on a face or an edge rests on that face's corners (kernel torso_face, same order); on
+   * terrain only while the lowest corner touches (the kernel keeps the heightfield lookups off a standing robot) */
+  const int lowest = contact_point(c, k, 0, corner, 0.0, fext, rr->torso_force, 0, 0, 0, c->mu_static, c->mu_dynamic,
+                                   hi, Madd, m->gravity, rec);
+  if (lowest || !c->terrain) {
     const double z0 = fabs(k->R[0][2][0]), z1 = fabs(k->R[0][2][1]), z2 = fabs(k->R[0][2][2]);
     const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
     const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;
