@@ -76,7 +76,8 @@ def parse():
     p.add_argument("--rollout", choices=("auto", "on", "off"), default="auto",
                    help="BASELINE config C4: record the compact rollout (frame, action, reward, dones per env-step) and "
                         "all-gather it over the ranks (asynchronous RCCL collective per rollout, or per --gather-every "
-                        "steps) inside the timed region (auto: on when N > 1; N = 1 is config C2, the plain rollout)")
+                        "steps) inside the timed region (auto: on when N > 1 for the flat / rsl tasks, whose rows the "
+                        "records rebuild; N = 1 is config C2, the plain rollout)")
     p.add_argument("--rollout-steps", type=int, default=24,
                    help="rollout length T (num_steps_per_env, C12/agents/rsl_rl_ppo_cfg.py:12)")
     p.add_argument("--gather-every", type=int, default=None,
@@ -89,7 +90,18 @@ def parse():
                         "process group, launched by torch.distributed.run): exercises the RCCL code path on one GPU")
     p.add_argument("--dump-rollout", type=str, default=None,
                    help="test hook: rank 0 saves the decoded rows and the gathered records of the timed window (.npz)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.rollout == "on" and args.task not in ROLLOUT_TASKS:
+        p.error(f"--rollout on: the compact rollout records rebuild history rows of the flat / rsl layouts only "
+                f"(--task {args.task} has {'no history' if args.task in ('rough', 'c5') else 'CaT dones'})")
+    if args.dump_rollout and args.steps > args.rollout_steps * (1 if args.rollout_decode else 2):
+        # the dump saves the first ring half's records and tail with the latest decoded rows: one rollout's data only
+        # while the window has not wrapped the ring (decode: rows of the first rollout only while K <= T)
+        p.error("--dump-rollout needs --steps <= rollout length (x2 without --rollout-decode)")
+    return args
+
+
+ROLLOUT_TASKS = ("flat", "rsl")
 
 
 def load_pmc(path):
@@ -158,7 +170,7 @@ def cpu_baseline(seconds: float):
 
     avail = usable_cpus()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or avail["usable"]
-    threads = max(1, min(threads, avail["usable"], 16))
+    threads = max(1, min(threads, avail["usable"]))
     n = 4096
     cfg = H12FlatEnvCfg()
     cfg.scene.num_envs = n
@@ -326,7 +338,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    rollout = args.rollout == "on" or (args.rollout == "auto" and world > 1)
+    rollout = args.rollout == "on" or (args.rollout == "auto" and world > 1 and args.task in ROLLOUT_TASKS)
     rg = None
     if rollout:  # C4: compact rollout records all-gathered on a side stream and decoded on every rank
         from h12env import distributed as D
@@ -534,7 +546,8 @@ def main():
                 "parallelism": f"env-shard x{world}" + (f" + RCCL all-gather of the rollout every {rg.G} steps"
                                                          if rg is not None and world > 1 else ""),
             },
-            "c4_rollout_allgather": c4,
+            "c4_rollout_allgather": c4 if c4 is not None or args.task in ROLLOUT_TASKS else {
+                "skipped": f"--task {args.task}: the compact records rebuild flat / rsl history rows only"},
             "burn_in": B,
             "resets_in_window": resets_in_window,
             "replay_bit_exact": replay_exact,

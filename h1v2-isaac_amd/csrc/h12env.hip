@@ -193,9 +193,6 @@ struct Workspace {
   float* F;    // [H12_NF_FLOAT][n]
   int32_t* I;  // [H12_NF_INT][n]
   int n;
-#ifdef H12_EXP_DUMMY_HIP
-  float* xd;   // experiment builds only: a hipMalloc'd buffer nothing reads
-#endif
 };
 
 enum { ST_RESET = 1, ST_CMD = 2, ST_OBS = 3, ST_PUSH = 4 };
@@ -1042,14 +1039,11 @@ H12_DEV HelpLds& help_lds() {
   __shared__ HelpLds H;
   return H;
 }
-#ifndef H12_OBS_POL
-#define H12_OBS_POL 0  // cache policy bits of the observation-row stores (buffer store aux: 1 sc0, 2 nt, 16 sc1)
-#endif
 // one float4 of an observation row (16-byte aligned rows) at float4 index j of dst
 H12_DEV void st_row4(float* dst, int j, float4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
                                          __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
-                                         H12_OBS_POL);
+                                         0);
 }
 // ---- Fused observation assembly (step path; the history layouts -- Flat, Rsl, CaT: StepArgs.fuse).  The rows
 // obs_assemble_kernel would write are stored by step_kernel's helper waves instead, mostly while the physics wave
@@ -1103,9 +1097,6 @@ H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
   // early store has completed)
   const int kmax = (f4 + nt - 1) / nt;
   const int k0 = (it - 1) * kmax / (n_steps - 1), k1 = it * kmax / (n_steps - 1);
-#ifdef H12_EXP_FUSE_NO_EARLY  // experiment builds only: the shifted-row stores dropped
-  return;
-#endif
   for (int k = k0; k < k1; ++k) {
     const int j = t + k * nt;
     if (j >= f4) break;
@@ -1345,11 +1336,7 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
 // range of envs -- each XCD's state loads / stores are contiguous runs of every field instead of 128-B chunks
 // 1 KB apart (the round-robin order put the tail of the waves on some XCDs 2 us behind the others)
 H12_DEV int xcd_block(int b, int nb);
-#ifdef H12_EXP_PLAIN_MAP  // experiment builds only: env chunk = block index (chunks interleaved over the XCDs)
-H12_DEV int step_block() { return blockIdx.x; }
-#else
 H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
-#endif
 
 // The helper wave's torso-box ground contact (lane 0 of each pair): the lowest corner's implicit contact and, while it
 // touches, the face's other corners (torso_face) -> H.torso for the physics wave's base combine after R2.
@@ -1365,11 +1352,7 @@ H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const
     float dummy[2];
     const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
                                                            org, P.mus, P.mud, ict);
-#ifdef H12_EXP_NOGATE
-    torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
-#else
     if (c || !Feat<K>::terrain) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
-#endif
     t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
     t[14] = c ? 1.f : 0.f;
   }
@@ -1624,11 +1607,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       float dummy[2];
       c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
                                                    P.mus, P.mud, ict);
-#ifdef H12_EXP_NOGATE
-      torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
-#else
       if (c || !Feat<K>::terrain) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, ft, fr.torso);
-#endif
     }
     if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
     for (int i = 0; i < 6; ++i) pAcc[i] -= ft[i];
@@ -1720,53 +1699,17 @@ H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc(void* base) { return __builtin_amdgcn_mak
 H12_DEV float ldf(const Workspace& W, int f, int e, int lf = 0) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.F), (e + lf * W.n) * 4, f * W.n * 4, 0));
 }
-#ifdef H12_DROP_STATE_STORES  // experiment builds only: price the state write-back (zero-record descriptor)
-H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0, 0x00020000); }
-#else
-H12_DEV __amdgpu_buffer_rsrc_t ws_rsrc_st(void* base) { return ws_rsrc(base); }
-#endif
-H12_DEV __amdgpu_buffer_rsrc_t st_F(const Workspace& W) { return ws_rsrc_st(W.F); }
-H12_DEV __amdgpu_buffer_rsrc_t st_I(const Workspace& W) { return ws_rsrc_st(W.I); }
-#ifdef H12_EXP_DUMMY_HIP
-#define H12_EXP_DUMMY_FM
-#endif
-#if defined(H12_EXP_DUMMY_FM) || defined(H12_EXP_DUMMY_COMPACT)
-// experiment builds only: the state write-back into a buffer nothing reads, field-major (the workspace layout)
-// or compact per block ([block][field][32 envs]: a wave's stores span 7 pages instead of ~200)
-__device__ float g_exp_dummy[1 << 22];
-H12_DEV void exp_st(const Workspace& W, int f, int e, uint32_t x, int lf, int region) {
-#ifdef H12_EXP_DUMMY_HIP
-  auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)W.xd, 0, -1, 0x00020000);
-#else
-  auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)g_exp_dummy, 0, -1, 0x00020000);
-#endif
-#ifdef H12_EXP_DUMMY_FM
-  __builtin_amdgcn_raw_buffer_store_b32(x, rs, (e + lf * 4096) * 4 + region * (8 << 20), f * 4096 * 4, 0);
-#else
-  __builtin_amdgcn_raw_buffer_store_b32(x, rs, (((e >> 5) * 256 + lf) * 128 + (e & 31) * 4) + region * (8 << 20),
-                                        f * 128, 0);
-#endif
-}
-H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) { exp_st(W, f, e, __builtin_bit_cast(uint32_t, x), lf, 0); }
-#else
-#ifndef H12_ST_POL
-#define H12_ST_POL 0
-#endif
+H12_DEV __amdgpu_buffer_rsrc_t st_F(const Workspace& W) { return ws_rsrc(W.F); }
+H12_DEV __amdgpu_buffer_rsrc_t st_I(const Workspace& W) { return ws_rsrc(W.I); }
 H12_DEV void stf(const Workspace& W, int f, int e, float x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), st_F(W), (e + lf * W.n) * 4, f * W.n * 4,
-                                        H12_ST_POL);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), st_F(W), (e + lf * W.n) * 4, f * W.n * 4, 0);
 }
-#endif
 H12_DEV int ldi(const Workspace& W, int f, int e) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(ws_rsrc(W.I), e * 4, f * W.n * 4, 0);
 }
-#if defined(H12_EXP_DUMMY_FM) || defined(H12_EXP_DUMMY_COMPACT)
-H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) { exp_st(W, f, e, (uint32_t)x, lf, 1); }
-#else
 H12_DEV void sti(const Workspace& W, int f, int e, int x, int lf = 0) {
-  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, H12_ST_POL);
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, 0);
 }
-#endif
 
 struct EnvSt {
   Base b;
@@ -2199,9 +2142,6 @@ H12_DEV void cmd_metrics(const KParams& P, EnvSt& s) {
 // first (48 rows), then base position (3) and yaw cos / sin (2) for the height scan.
 template <int K>
 H12_DEV void obs_frame(const KParams& P, const EnvSt& s, int leg, int e, int n, float* frame) {
-#ifdef H12_EXP_NO_FRAME  // experiment builds only: the frame is not written (timing of the store tail)
-  return;
-#endif
   const float sg = leg ? -1.f : 1.f;
   const int o = (Feat<K>::ext && P.task == H12_TASK_ROUGH) ? 3 : 0;
   if (leg == 0) {
@@ -2324,10 +2264,7 @@ H12_DEV void log_fold(const AsmArgs& A, float acc) {
     log_fold_one(A, pv, a);
   }
 }
-#ifndef H12_ASM_ROWS
-#define H12_ASM_ROWS 4
-#endif
-constexpr int ASM_ROWS = H12_ASM_ROWS;  // rows per block (the frame's [45][n] rows are read in 4*ROWS-byte segments)
+constexpr int ASM_ROWS = 4;  // rows per block (the frame's [45][n] rows are read in 4*ROWS-byte segments)
 static_assert((ASM_ROWS * H12_OBS_FRAME) % 4 == 0, "float4 rows for every history length");
 static_assert(ASM_ROWS * 8 <= ASM_BLOCK, "one Philox block per thread");
 
@@ -2759,9 +2696,6 @@ H12_DEV void fuse_late(const KParams& P, const StepArgs& A, const FuseCtx& fc, i
     }
   }
   if (fc.on) {
-#ifdef H12_EXP_FUSE_NO_LATE  // experiment builds only: the newest-slot / refill stores dropped
-    return;
-#endif
     for (int w = t; w < FUSE_ROWS * H12_OBS_FRAME; w += nt) {
       const int r = w / H12_OBS_FRAME, c = w - r * H12_OBS_FRAME;
       fc.dst[r * row + newest_col(c, nh)] = fr[w];
@@ -2861,9 +2795,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
         __syncthreads();                // F: the physics wave's noisy frames and refill flags
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
-#ifndef H12_EXP_NO_LOG_ATOMICS  // experiment builds only: the per-block episode-log partials dropped
       if (lv) A.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;
-#endif
     } else {
       self_wave<K>(P, W.n, nsteps, fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
@@ -2890,9 +2822,6 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     load_phys<K>(P, W, e, leg, s);
     // the MDP part of the state is loaded here too: its memory round trip overlaps the physics loop
     load_mdp<K>(P, W, e, leg, s);
-#ifdef H12_EXP_WAIT_LOADS  // experiment builds only: expose the state-load round trip in phase slot 0
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
@@ -2967,11 +2896,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     }
     if (Feat<K>::ext && P.cat) cat_constraints<true>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
     PH(3);
-#ifdef H12_EXP_NO_RESET  // experiment builds only: price the in-kernel reset path
-    const bool reset = false;
-#else
     const bool reset = term || tout;
-#endif
     if (leg == 0) {
       A.rew[e] = r;
       A.term[e] = (uint8_t)term;
@@ -3031,9 +2956,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       obs_frame<K>(P, s, leg, e, W.n, A.frame);
     }
     PH(6);
-#ifndef H12_EXP_NO_STORE  // experiment builds only (knock-out timing)
     store_env<K>(P, W, e, leg, s);
-#endif
     PH(7);
     PH_WAVE_END();
   }
@@ -3377,8 +3300,8 @@ __global__ void __launch_bounds__(DEC_BLOCK) rollout_decode_kernel(DecArgs D) {
     const int h = c < 9 ? (col % (3 * NH)) / 3 : ((col - 9 * NH) % (12 * NH)) / 12;
     s_col[col] = (ce & 0xFFFFu) | ((uint32_t)h << 16);
   }
-  // a capped grid strides over the env groups (DEC_MAX_BLOCKS: the decode runs beside the env kernels on a side
-  // stream and must leave them CUs)
+  // a capped grid strides over the env groups (DEC_MAX_BLOCKS: a caller may launch the decode on a stream of its own
+  // beside the env kernels, which then keep CUs; h12env.rollout's RolloutGather launches it on the env's stream)
   for (int grp = blockIdx.x; grp < D.n_shards * bps; grp += gridDim.x) {
   const int shard = grp / bps, e0 = (grp - shard * bps) * DEC_ENVS;
   const int ne = min(DEC_ENVS, D.n - e0);
@@ -3926,9 +3849,6 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   h->W.F = (float*)state_dev;
   h->W.I = (int32_t*)((float*)state_dev + (size_t)H12_NF_FLOAT * n_envs);
   h->W.n = n_envs;
-#ifdef H12_EXP_DUMMY_HIP
-  if (hipMalloc(&h->W.xd, 16 << 20) != hipSuccess) return set_err(H12_E_ALLOC, "exp dummy");
-#endif
   e = hipMalloc(&h->frame, sizeof(float) * FRAME_ROWS * (size_t)n_envs);
   if (e != hipSuccess) {
     if (h->own) (void)hipFree(state_dev);

@@ -498,6 +498,7 @@ class H12VelocityEnv:
         return int(seed)
 
     def reset(self, seed: int | None = None, env_ids=None, options=None):
+        self._no_bound_rollout("reset()")
         if seed is not None:
             self.seed(seed)
         mask = None
@@ -570,7 +571,8 @@ class H12VelocityEnv:
         config C4): the step's reward, terminated / truncated flags and new observation frame (as it enters the
         history) are written by the kernels straight into ring slot ``rec.t``, which then advances (mod rec.slots); the
         returned reward / flag tensors are views of that record.  Flat observation layout only (the frames rebuild
-        the history rows)."""
+        the history rows).  Only step() may run while it is bound: reset() / observe() raise (their rows would not be in
+        the records) -- unbind, reset, and bind a fresh recorder."""
         if self.obs_dim == NOBS_ROUGH or self._cat:
             raise ValueError("bind_rollout needs the flat observation layout (history) and a non-CaT task")
         if rec.n != self.num_envs or rec.history * 45 != self.obs_dim:
@@ -587,6 +589,13 @@ class H12VelocityEnv:
                 setattr(o, name, getattr(src, name))
             self._rollout_outs.append((o, C.byref(o)))
         self._rollout = rec
+
+    def _no_bound_rollout(self, what):
+        # only step() writes rollout records: a reset / observe in the middle of a recorded rollout would change the
+        # history rows without a frame or done flag in the records, and h12env_rollout_decode would rebuild rows
+        # that differ from the ones the env returned
+        if getattr(self, "_rollout", None) is not None:
+            raise RuntimeError(f"{what} while a rollout recorder is bound: call unbind_rollout() first")
 
     def unbind_rollout(self):
         if self._rollout is not None:
@@ -630,6 +639,7 @@ class H12VelocityEnv:
 
     def observe(self, fill_mask: torch.Tensor | None = None):
         """ObservationManager.compute(): append a frame of the current state to the history."""
+        self._no_bound_rollout("observe()")
         prev = self._obs[self._k]
         self._k ^= 1
         out = self._obs[self._k]

@@ -192,8 +192,11 @@ class EmpiricalNormalization(nn.Module):
         """Running update from one batch; under torch.distributed (world > 1) the batch is the union of
         every rank's shard, so all ranks keep identical statistics.  The shards' statistics are merged with
         Chan's parallel formula (global mean from sum n_r mean_r, then M2 = sum n_r (var_r + (mean_r - mean)^2)):
-        no E[x^2] - mean^2 cancellation, so the merged variance is never negative.  The union size is
-        all-reduced once per local batch size and cached (no host sync per update)."""
+        no E[x^2] - mean^2 cancellation, so the merged variance is never negative.  Every call issues exactly two
+        all-reduces on every rank: the union size rides in the first one (with the shards' weighted means), so
+        ranks never disagree on which collectives run, whatever their local batch sizes.  The merge itself uses the
+        device-side union size; the host-side count reads it once per local batch size (cached, so no host sync per
+        update)."""
         if self.until is not None and self.count >= self.until:
             return
         n = x.shape[0]
@@ -201,15 +204,16 @@ class EmpiricalNormalization(nn.Module):
         mean_x = torch.mean(x, dim=0, keepdim=True)
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
                 and torch.distributed.get_world_size() > 1:
-            if n not in self._global_n:
-                cnt = torch.tensor([float(n)], device=x.device)
-                D.all_reduce(cnt)
-                self._global_n[n] = int(cnt.item())
-            n_tot = self._global_n[n]
-            g_mean = mean_x * (n / n_tot)
-            D.all_reduce(g_mean)
-            m2 = (var_x + (mean_x - g_mean) ** 2) * (n / n_tot)
+            s1 = torch.cat([mean_x * n, torch.full((1, 1), float(n), device=x.device, dtype=mean_x.dtype)], 1)
+            D.all_reduce(s1)
+            n_dev = s1[:, -1:]
+            g_mean = s1[:, :-1] / n_dev
+            m2 = (var_x + (mean_x - g_mean) ** 2) * n
             D.all_reduce(m2)
+            m2 = m2 / n_dev
+            if n not in self._global_n:
+                self._global_n[n] = int(round(float(n_dev.item())))
+            n_tot = self._global_n[n]
             n, mean_x, var_x = n_tot, g_mean, m2
         self.count += n
         rate = n / self.count

@@ -122,7 +122,11 @@ class RolloutGather:
     """All-gather of the shards' rollout records, one collective per chunk of G steps (default G = T: one per
     rollout), issued asynchronously on RCCL's own stream right after the chunk's last step, so it runs while the env
     steps the next chunk into the other half of the recorder's ring; optionally every chunk's global
-    (T, N_global, 45H) observation rows are rebuilt right after it arrives (``h12env_rollout_decode``).
+    (T, N_global, 45H) observation rows are rebuilt right after it arrives (``h12env_rollout_decode``).  The rebuild
+    is SERIALISED with the env: it runs on the compute stream after ``work.wait()``, so with decode on the compute
+    stream waits for every chunk's gather at once and the gather does not overlap the next steps (a side stream
+    ordered by events cost ~95 us of host time per hand-off on this stack); bench figures
+    taken with --rollout-decode are serialised figures.  Decode off (the default) keeps the overlap.
 
     Ordering uses the collectives' own stream semantics (torch.distributed Work): before the env rewrites a ring
     chunk, ``before_step`` makes the compute stream wait for that chunk's previous gather (``work.wait()``, a device-side

@@ -80,7 +80,12 @@ def test_decoded_rows_equal_env_rows(gpu, task, n):
         want = torch.stack(rows)
         assert torch.equal(got, want), (it, (got != want).nonzero()[:5])
     assert dones > 0
+    with pytest.raises(RuntimeError):  # only step() writes records: a reset mid-rollout would desync the rebuild
+        env.reset()
+    with pytest.raises(RuntimeError):
+        env.observe()
     env.unbind_rollout()
+    env.reset()
     env.close()
 
 
@@ -194,3 +199,86 @@ def test_rccl_rollout_allgather_one_rank(tmp_path):
     g = unpack(d["gathered"], 1, 64, int(d["T"]), int(d["G"]), list(d["off"]), int(d["step_bytes"]))
     done = g["terminated"] | g["truncated"]
     np.testing.assert_array_equal(decode_ref(g["frames"], done, d["tail"], 10), d["obs"])
+
+
+@pytest.mark.timeout(900)
+def test_c4_size_eight_rank_rehearsal(tmp_path):
+    """BASELINE config C4 at its size, rehearsed on one GPU: 8 ranks of bench.py's N > 1 path (child processes, all
+    on cuda:0, gloo: RCCL refuses several ranks on one device) x 4096 envs = 32 768 global envs (4096 per GPU,
+    V/velocity_env_cfg.py:288), one full rollout of T = 24 steps (C12/agents/rsl_rl_ppo_cfg.py:12) recorded, all-gathered
+    as one chunk and decoded into the global (24, 32768, 450) rows on every rank.  The gathered records and the
+    decoded rows must equal one process stepping all 32 768 envs with the same actions, bit for bit.  (gloo stages
+    the gather through the host, so no bandwidth figure is claimed; the ranks rendezvous in init_process_group before
+    any of them touches the GPU.)"""
+    world, n, K, B, W = 8, 4096, 24, 40, 3
+    port = _free_port()
+    dump = tmp_path / "rollout.npz"
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                   LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
+        log = open(tmp_path / f"rank{rank}.log", "w")
+        cmd = [sys.executable, "-u", str(ROOT / "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
+               "--envs", str(n), "--steps", str(K), "--warmup", str(W), "--burn-in", str(B), "--rollout", "on",
+               "--no-cpu-baseline", "--rollout-decode", "--dump-rollout", str(dump)]
+        procs.append((subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, cwd=str(ROOT)), log))
+    try:
+        for p, _ in procs:
+            p.wait(timeout=780)
+    finally:
+        for p, log in procs:
+            if p.poll() is None:
+                p.kill()
+            log.close()
+    for rank, (p, _) in enumerate(procs):
+        assert p.returncode == 0, (tmp_path / f"rank{rank}.log").read_text()[-3000:]
+    line = [ln for ln in (tmp_path / "rank0.log").read_text().splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    print("C4 rehearsal line:", line[:400])
+    c4 = out["c4_rollout_allgather"]
+    assert out["n_gpus"] == world and out["config"]["global_envs"] == world * n
+    assert c4["chunks"] == 1 and c4["gather_every"] == K and c4["rows_rebuilt"]
+    assert c4["gathered_bytes_per_iter"] == pytest.approx(world * n * c4["record_bytes_per_env_step"] * K)
+
+    d = np.load(dump)
+    assert d["obs"].shape == (K, world * n, 450)
+    from h12env import H12FlatEnvCfg
+    from h12env.env import H12VelocityEnv
+
+    cfg = H12FlatEnvCfg()
+    cfg.scene.num_envs = world * n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    pool = int(d["pool"])
+    acts, eplen = [], []
+    for r in range(world):  # each rank's generator: actions first, then the episode lengths (bench.py)
+        g = torch.Generator(device="cuda:0").manual_seed(1234 + r)
+        acts.append(torch.randn(pool, n, 12, device="cuda:0", generator=g))
+        eplen.append(torch.randint(0, env.max_episode_length, (n,), device="cuda:0", generator=g, dtype=torch.int32))
+    acts = torch.cat(acts, 1)
+    env.episode_length_buf = torch.cat(eplen)
+    for i in range(B + W):
+        env.step(acts[i % pool])
+    tail = env.get_observations()["policy"].clone()
+    rows = torch.empty(K, world * n, 450, device="cuda:0")
+    rew, term, trunc, used = [], [], [], []
+    for i in range(K):
+        a = acts[(B + W + i) % pool]
+        obs, r_, te, tr, _ = env.step(a)
+        rows[i].copy_(obs["policy"])
+        rew.append(r_.clone())
+        term.append(te.clone())
+        trunc.append(tr.clone())
+        used.append(a)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d["tail"], tail.cpu().numpy())
+    got = torch.from_numpy(d["obs"]).to("cuda:0")
+    assert torch.equal(got, rows), (got != rows).nonzero()[:5]
+    g = unpack(d["gathered"], world, n, int(d["T"]), int(d["G"]), list(d["off"]), int(d["step_bytes"]))
+    np.testing.assert_array_equal(g["rewards"], torch.stack(rew).cpu().numpy())
+    np.testing.assert_array_equal(g["terminated"], torch.stack(term).cpu().numpy().astype(np.uint8))
+    np.testing.assert_array_equal(g["truncated"], torch.stack(trunc).cpu().numpy().astype(np.uint8))
+    np.testing.assert_array_equal(g["actions"], torch.stack(used).cpu().numpy())
+    assert (g["terminated"] | g["truncated"]).sum() > 100  # resets inside the rollout (random episode lengths + falls)
+    env.close()

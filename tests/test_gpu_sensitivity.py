@@ -1,0 +1,115 @@
+"""GPU: parity gates that resolve 1e-5 (round 4).
+
+The per-env-step tolerances of tests/helpers/forced.py (1e-3 relative) police switching flips; they cannot see a
+SYSTEMATIC error of 1e-5..1e-4 (a wrong inertia entry, PD gain or contact constant).  On the random-action Flat
+runs a finer gate is not available either: there the oracle moves by ~1e-5 (p50) under a 1e-7 relative perturbation
+of the pre-step state (the conditioning probe, ForcedParity.quantiles("cond")), so no fp32 implementation can sit
+below that.  These tests put the kernel in well-conditioned states instead (tests/helpers/scenarios.py) and gate
+the error QUANTILES of the teacher-forced comparison there (forced.SCEN_GATE, set from the measured fp32 floor);
+tests/test_forced_harness.py shows on the CPU that planted 1e-4-relative constant errors move those quantiles past
+the gate at the same noise level.
+
+The last test is the north_star criterion (<= 1e-4 relative q error over 1000 policy steps, sim2sim semantics) on a
+FREE floating base: zero gravity (no floor contact), so the free joint's quaternion integration and the base row
+of the articulated-body solve (M/h12_12dof.xml:68; D/simulator/sim_mujoco.py:39-44,102-121) run for 20 000
+substeps next to the fp64 oracle."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from forced import SCEN_GATE, ForcedParity
+from h12env import H12FlatEnvCfg, mujoco_cfg
+from h12env._abi import F as FIELDS
+from h12env.env import H12VelocityEnv
+from scenarios import SCENARIOS
+
+pytestmark = pytest.mark.gpu
+
+SCALE = dict(flight=1.0, lying=0.3)
+
+
+def scenario_cfg():
+    cfg = H12FlatEnvCfg()
+    # the lying robots' torso contact is an illegal contact: kept in contact here to measure the contact phase
+    cfg.terminations.base_contact_torso = False
+    cfg.terminations.base_contact_knees = False
+    return cfg
+
+
+def run_scenario(name, n=1024, steps=20, seed=31):
+    cfg = scenario_cfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    rng = np.random.default_rng(seed)
+    Fm = env._fstate.cpu().numpy().copy()
+    SCENARIOS[name](env._model, Fm, rng)
+    env._fstate.copy_(torch.from_numpy(Fm))
+    fp = ForcedParity(env, seed=seed + 1)
+    for _ in range(steps):
+        fp.step((rng.normal(size=(n, 12)) * SCALE[name]).astype(np.float32))
+    return env, fp
+
+
+@pytest.mark.parametrize("name", list(SCENARIOS))
+def test_forced_error_quantiles_well_conditioned(gpu, name):
+    env, fp = run_scenario(name)
+    fp.check(max_bad_frac=0.01)
+    print(name, "quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe", fp.quantiles("cond"))
+    fp.check_quantiles(SCEN_GATE[name])
+    env.close()
+
+
+def test_mujoco_mode_free_base_zero_gravity_1000_steps(gpu, monkeypatch):
+    """north_star criterion with the free joint: sim2sim semantics (1 kHz PD, x20 decimation, MJCF clamps, implicit
+    joint damping), floating base in zero gravity (no contact), 1000 policy steps of random actions: max relative
+    joint-position error <= 1e-4 against the fp64 oracle; the base orientation is reported and held to 1e-3."""
+    import h12env.env as envmod
+    from h12env.model import build_model
+
+    def zero_g_model():
+        m = build_model()
+        m.gravity = 0.0
+        return m
+
+    monkeypatch.setattr(envmod, "build_model", zero_g_model)
+    n = 8
+    cfg = mujoco_cfg()
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    assert env._model.gravity == 0.0
+    rng = np.random.default_rng(4)
+    Fm = env._fstate.cpu().numpy().copy()
+    Fm[FIELDS["POS"][0] + 2] = 3.0
+    Fm[FIELDS["WANG"][0]:FIELDS["WANG"][0] + 3] = rng.normal(size=(3, n)) * 0.3  # a tumbling base
+    env._fstate.copy_(torch.from_numpy(Fm))
+    q0 = np.asarray(env._model.q_default)
+    states = [np.concatenate([Fm[o:o + c, i] for o, c in (FIELDS[k] for k in ("POS", "QUAT", "VLIN", "WANG", "Q",
+                                                                                  "QD"))]).astype(np.float64)
+              for i in range(n)]
+    worst_q = worst_quat = 0.0
+    steps = 1000
+    for t in range(steps):
+        q_ref = q0[None] + 0.25 * rng.normal(size=(n, 12))
+        env.step_physics(torch.from_numpy(q_ref.astype(np.float32)).cuda(), 20)
+        for i in range(n):
+            states[i], _ = O.mujoco_rollout(env._model, env._ccfg, states[i],
+                                            q_ref[i].astype(np.float32).astype(np.float64), 20)
+        if t % 50 == 49 or t == steps - 1:
+            G = env._fstate.cpu().numpy()
+            S = np.array(states)
+            gq, oq = G[FIELDS["Q"][0]:FIELDS["Q"][0] + 12].T, S[:, 13:25]
+            worst_q = max(worst_q, (np.abs(gq - oq) / np.maximum(1, np.abs(oq).max(axis=1, keepdims=True))).max())
+            gw = G[FIELDS["QUAT"][0]:FIELDS["QUAT"][0] + 4].T
+            dot = np.abs((gw * S[:, 3:7]).sum(axis=1))
+            worst_quat = max(worst_quat, float(np.max(2 * np.arccos(np.minimum(1.0, dot)))))
+            assert np.abs(G[FIELDS["POS"][0] + 2] - 3.0).max() < 50.0  # drifting, not falling
+    print(f"free base, zero g, 1000 policy steps: max rel q error {worst_q:.3g}, max base orientation error "
+          f"{worst_quat:.3g} rad")
+    assert worst_q <= 1e-4, worst_q
+    assert worst_quat <= 1e-3, worst_quat
+    env.close()

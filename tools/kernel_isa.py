@@ -81,6 +81,20 @@ def report(text: str, name: str) -> dict:
     return r
 
 
+def isa_sha256(text: str) -> str:
+    """sha256 of the device assembly with comments and the per-source compile-unit id (__hip_cuid_*) removed: equal
+    for two sources that compile to the same machine code (e.g. after a comment-only or dead-macro edit)."""
+    import hashlib
+    import re
+
+    lines = []
+    for ln in text.splitlines():
+        if ln.lstrip().startswith(";") or ln.startswith("\t.file") or ".ident" in ln:
+            continue
+        lines.append(re.sub(r"__hip_cuid_[0-9a-f]+", "__hip_cuid", ln.split(";")[0].rstrip()))
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest()
+
+
 def physics_wave_json(text: str, meta: dict, out: Path) -> None:
     """profiles/latest_isa.json for bench.py's issue roofline: the Flat step_kernel's register allocation and the
     VALU count of its physics wave's physics-step loop, keyed by the kernel source's sha256 like latest_pmc.json.
@@ -102,7 +116,7 @@ def physics_wave_json(text: str, meta: dict, out: Path) -> None:
                                  "column decodes the descriptor's granulated field with a granule of 4 instead of 8 "
                                  "(half the allocated count)"},
            "physics_step_loop": {"label": top[0], "instructions": top[1], "valu": top[2], "v_accvgpr": top[3]},
-           "valu_total_static": r["valu"]}
+           "valu_total_static": r["valu"], "isa_sha256": isa_sha256(text)}
     out.write_text(json.dumps(res, indent=1) + "\n")
     print("wrote", out)
 
@@ -118,6 +132,7 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         text = build_asm(Path(td)).read_text()
     meta = metadata(text)
+    print("isa_sha256", isa_sha256(text))
     if js is not None:
         physics_wave_json(text, meta, js)
     for name, g in sorted(meta.items()):
