@@ -64,27 +64,35 @@ template <int K> struct Feat {
 // over waves (lane 0), read back with h12env_phase_profile.  Not part of the product library.
 #ifdef H12_PHASE_PROFILE
 __device__ unsigned long long g_phase[16];
-__device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, [4]: after reset + command, [5]: XCC id  // per physics wave of the last launch: realtime start, end, end after waitcnt
+// per physics wave of the last launch, realtime: [0] start, [1] end, [2] end after waitcnt, [3] after the physics
+// loop, [4] after reset + command, [5] XCC id, [6] after the frame + barrier F (before the state stores),
+// [7] / [8] the shader-clock counter (s_memtime) at the start / at [2] -> the XCD's clock rate over the wave,
+// [9] / [10] the cycles this wave waited in barriers R1 / R2 over the launch
+__device__ unsigned long long g_wave[1024][11];
 #define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter(); \
-  const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime()
+  const unsigned long long _ph_c0 = _ph_t;                                \
+  const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime();    \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) g_wave[blockIdx.x][9] = g_wave[blockIdx.x][10] = 0
 #define PH_WAVE_END()                                                          \
   do {                                                                         \
     const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();           \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
     const unsigned long long _r2 = __builtin_amdgcn_s_memrealtime();           \
+    const unsigned long long _c2 = __builtin_readcyclecounter();               \
     unsigned _xcc;                                                             \
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));        \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                        \
       g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
       g_wave[blockIdx.x][5] = _xcc & 15u;                                      \
+      g_wave[blockIdx.x][7] = _ph_c0; g_wave[blockIdx.x][8] = _c2;             \
     }                                                                          \
   } while (0)
 #define PH(i)                                                                       \
   do {                                                                              \
     unsigned long long _t = __builtin_readcyclecounter();                           \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _ph_t);                \
-    if ((i == 1 || i == 5) && (threadIdx.x & 63) == 0 && blockIdx.x < 1024)          \
-      g_wave[blockIdx.x][i == 1 ? 3 : 4] = __builtin_amdgcn_s_memrealtime();        \
+    if ((i == 1 || i == 5 || i == 6) && (threadIdx.x & 63) == 0 && blockIdx.x < 1024) \
+      g_wave[blockIdx.x][i == 1 ? 3 : i == 5 ? 4 : 6] = __builtin_amdgcn_s_memrealtime(); \
     _ph_t = _t;                                                                     \
   } while (0)
 // inside inner_step (its own clock mark): slots 10.. split the inner step around the helper hand-off
@@ -93,6 +101,8 @@ __device__ unsigned long long g_wave[1024][6];  // [3]: after the physics loop, 
   do {                                                                              \
     unsigned long long _t = __builtin_readcyclecounter();                           \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[i], _t - _phx_t);               \
+    if ((i == 8 || i == 9) && (threadIdx.x & 63) == 0 && blockIdx.x < 1024)         \
+      atomicAdd(&g_wave[blockIdx.x][i + 1], _t - _phx_t);                           \
     _phx_t = _t;                                                                    \
   } while (0)
 #else
@@ -4221,7 +4231,7 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 }
 int h12env_wave_times(unsigned long long* out, int nwaves) {
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave), sizeof(unsigned long long) * 6 * (size_t)nwaves));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave), sizeof(unsigned long long) * 11 * (size_t)nwaves));
   return 0;
 }
 #endif

@@ -82,17 +82,21 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
     if hasattr(lib, "h12env_wave_times"):  # per-wave realtime stamps (100 MHz) of single launches
         import numpy as np
 
-        wt = (C.c_ulonglong * (6 * waves))()
+        wt = (C.c_ulonglong * (11 * waves))()
         keys = ("span", "start_spread", "end_spread", "dur_mean", "dur_max", "drain_max")
-        rows, raw, rsets = [], [], []
+        rows, raw, rsets, clk, bw = [], [], [], [], []
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
             lib.h12env_wave_times(wt, waves)
-            full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 6).astype(np.int64)
-            a = full[:, :5].copy()
+            full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
+            bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
+            clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
+            a = np.concatenate([full[:, :5], full[:, 6:7]], axis=1)
             a -= a[:, 0].min()
-            a = np.concatenate([a, full[:, 5:6]], axis=1)  # column 5: the wave's XCC id (s_getreg HW_REG_XCC_ID)
+            # columns: 0 start, 1 end, 2 end after waitcnt, 3 after physics, 4 after reset, 5 XCC id
+            # (s_getreg HW_REG_XCC_ID), 6 after barrier F
+            a = np.concatenate([a[:, :5], full[:, 5:6], a[:, 5:6]], axis=1)
             raw.append(a.copy())
             rs = (env.reset_terminated | env.reset_time_outs).view(-1, 32).sum(1).cpu().numpy()
             rsets.append(rs)
@@ -103,6 +107,21 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             np.save(os.environ["H12_WAVE_DUMP"], np.asarray(raw))
             np.save(os.environ["H12_WAVE_DUMP"].replace(".npy", "_resets.npy"), np.asarray(rsets))
         res["wave_realtime_us_median"] = dict(zip(keys, (np.median(np.asarray(rows), axis=0) / 100.0).round(2).tolist()))
+        R = np.asarray(raw)  # (launches, waves, 7)
+        per = {}
+        for x in range(8):
+            m = R[:, :, 5] == x
+            if not m.any():
+                continue
+            w = R[m]
+            med = lambda v: round(float(np.median(v)) / 100.0, 2)  # noqa: E731
+            per[f"xcc{x}"] = {"physics": med(w[:, 3] - w[:, 0]), "sensor..reset": med(w[:, 4] - w[:, 3]),
+                              "frame+F wait": med(w[:, 6] - w[:, 4]), "store issue": med(w[:, 1] - w[:, 6]),
+                              "store completion": med(w[:, 2] - w[:, 1]), "end": med(w[:, 2]),
+                              "clock_MHz": round(float(np.median(np.asarray(clk)[m])), 0),
+                              "barrier R1 wait": round(float(np.median(np.asarray(bw)[m][:, 0])), 2),
+                              "barrier R2 wait": round(float(np.median(np.asarray(bw)[m][:, 1])), 2)}
+        res["per_xcc_us_median"] = per
     env.close()
     return res
 

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Experiment builds from a patched COPY of the kernel source (round 4: the product source carries no experiment
+macros).  A patch is a list of (old, new) string replacements applied to csrc/h12env.hip in a scratch tree under
+tools/_variants/<tag>/ (with include/ beside it, so the relative includes resolve); the library is
+tools/_variants/lib_<tag>.so, loaded with H12ENV_LIB=... by bench.py / tools/phase_profile.py.
+
+    python tools/variant.py <tag> [--profile]      # builds the variant named <tag> from PATCHES below
+"""
+from __future__ import annotations
+
+import argparse
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
+
+PATCHES = {
+    # the helper waves' shifted-row stores during the physics loop dropped (timing only: the rows are wrong)
+    "no_early": [("  for (int k = k0; k < k1; ++k) {\n    const int j = t + k * nt;",
+                  "  for (int k = k0; k < k0; ++k) {\n    const int j = t + k * nt;")],
+    # the state write-back dropped (timing only: the state never advances)
+    "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
+}
+
+
+def build(tag: str, profile: bool) -> Path:
+    from h12env.build import ARCH, hipcc
+
+    src = (ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_text()
+    for old, new in PATCHES[tag]:
+        if src.count(old) != 1:
+            raise SystemExit(f"patch {tag!r}: {old[:60]!r} matches {src.count(old)} times")
+        src = src.replace(old, new)
+    top = ROOT / "tools" / "_variants" / tag
+    if top.exists():
+        shutil.rmtree(top)
+    csrc = top / "a" / "csrc"
+    shutil.copytree(ROOT / "h1v2-isaac_amd" / "csrc", csrc)
+    shutil.copytree(ROOT / "include", top / "include")
+    (csrc / "h12env.hip").write_text(src)
+    out = ROOT / "tools" / "_variants" / f"lib_{tag}.so"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
+           "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros", "-fPIC", "-shared", "-Wno-unused-function",
+           *(["-DH12_PHASE_PROFILE"] if profile else []), "-o", str(out), str(csrc / "h12env.hip")]
+    subprocess.run(cmd, check=True)
+    shutil.rmtree(top)
+    print("built", out)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag", choices=sorted(PATCHES))
+    ap.add_argument("--profile", action="store_true")
+    a = ap.parse_args()
+    build(a.tag, a.profile)
