@@ -85,6 +85,86 @@ class SplitKLinear(nn.Linear):
         return nn.functional.linear(x, self.weight, self.bias)
 
 
+class _TwinLinearFn(torch.autograd.Function):
+    """Two independent linear layers as ONE batched GEMM: y[k] = x[k] W[k]^T + b[k] for k in (actor, critic), x
+    (2, B, in) (any batch stride: a (B, 2 in) activation viewed as (2, B, in) is read in place), W (2, out, in).  The
+    weight gradient is split-K over the minibatch like _SplitKLinearFn (2 x split batched GEMMs, summed)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, split, dt):
+        with torch.autocast(device_type="cuda", enabled=False):
+            xc, wc = x.to(dt), w.to(dt)
+            ctx.save_for_backward(xc, wc)
+            ctx.split, ctx.x_dtype = split, x.dtype
+            return torch.baddbmm(b.to(dt).unsqueeze(1), xc, wc.transpose(1, 2))
+
+    @staticmethod
+    def backward(ctx, gy):
+        xc, wc = ctx.saved_tensors
+        s, n = ctx.split, xc.shape[1]
+        with torch.autocast(device_type="cuda", enabled=False):
+            gy = gy.to(wc.dtype)
+            gx = torch.bmm(gy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+            if s > 1 and n % s == 0:
+                xs = xc.reshape(2 * s, n // s, xc.shape[2]) if xc.is_contiguous() else \
+                    xc.contiguous().view(2 * s, n // s, xc.shape[2])
+                gw = torch.bmm(gy.reshape(2 * s, n // s, -1).transpose(1, 2), xs).view(2, s, wc.shape[1], wc.shape[2])
+                gw = gw.sum(1) if gw.dtype == torch.float32 else gw.float().sum(1)
+            else:
+                gw = torch.bmm(gy.transpose(1, 2), xc).float()
+            return gx, gw, gy.float().sum(1), None, None
+
+
+def twin_compatible(actor: nn.Sequential, critic: nn.Sequential) -> bool:
+    """True when the two MLPs have the same hidden layer shapes and activations (the Flat / Rough / Rsl agents:
+    [512, 256, 128] ELU for both, C12/agents/rsl_rl_ppo_cfg.py:17-21), so their hidden layers batch pairwise."""
+    a, c = list(actor), list(critic)
+    if len(a) != len(c) or len(a) < 3:
+        return False
+    for la, lc in zip(a[:-1], c[:-1]):
+        if isinstance(la, nn.Linear) != isinstance(lc, nn.Linear) or type(la) is not type(lc):
+            return False
+        if isinstance(la, nn.Linear) and (la.in_features, la.out_features) != (lc.in_features, lc.out_features):
+            return False
+    return isinstance(a[-1], nn.Linear) and isinstance(c[-1], nn.Linear) and a[-1].in_features == c[-1].in_features
+
+
+def twin_forward(actor: nn.Sequential, critic: nn.Sequential, x: torch.Tensor, split: int = 1):
+    """(actor(x), critic(x)) for one input, the two networks evaluated together (learning phase): the first layer as
+    one GEMM with the two weight matrices stacked along the output (N = 2 x 512), the hidden layers as 2-batch GEMMs,
+    the output layers as one 2-batch GEMM with the critic's single row zero-padded to the actor's width; every
+    activation is one elementwise kernel over both networks.  Same math as the two separate forwards (fp32
+    summation order aside); gradients reach each network's own parameters through the stacks."""
+    a, c = list(actor), list(critic)
+    dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) else torch.float32
+    l0a, l0c = a[0], c[0]
+    w0 = torch.cat([l0a.weight, l0c.weight], 0)
+    b0 = torch.cat([l0a.bias, l0c.bias], 0)
+    ok_split = split > 1 and x.shape[0] % split == 0
+    if ok_split:
+        h = _SplitKLinearFn.apply(x, w0, b0, split, dt)
+    else:
+        with torch.autocast(device_type="cuda", enabled=False):
+            h = nn.functional.linear(x.to(dt), w0.to(dt), b0.to(dt))
+    h = a[1](h)  # the activation over both halves at once
+    width = l0a.out_features
+    h = h.view(h.shape[0], 2, width).transpose(0, 1)  # (2, B, width), strided: no copy
+    for i in range(2, len(a) - 1, 2):
+        la, lc = a[i], c[i]
+        w = torch.stack([la.weight, lc.weight])
+        b = torch.stack([la.bias, lc.bias])
+        h = a[i + 1](_TwinLinearFn.apply(h, w, b, split if ok_split else 1, dt))
+    la, lc = a[-1], c[-1]
+    pad = la.out_features - lc.out_features
+    if pad >= 0:
+        wc = torch.cat([lc.weight, lc.weight.new_zeros(pad, lc.in_features)], 0)
+        bc = torch.cat([lc.bias, lc.bias.new_zeros(pad)], 0)
+        y = _TwinLinearFn.apply(h, torch.stack([la.weight, wc]), torch.stack([la.bias, bc]),
+                                split if ok_split else 1, dt)
+        return y[0], y[1, :, :lc.out_features]
+    return la(h[0]), lc(h[1])
+
+
 def mlp(n_in: int, hidden: list[int], n_out: int, act: str) -> nn.Sequential:
     layers: list[nn.Module] = []
     d = n_in
@@ -327,6 +407,10 @@ class PPO:
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be fp32 or bf16, got {precision!r}")
         self.precision = precision
+        # actor + critic batched in the learning phase (twin_forward) when their layer shapes match; H12_TWIN=0 turns
+        # it off (A/B)
+        self._twin = (os.environ.get("H12_TWIN", "1") != "0" and hasattr(self.policy, "actor")
+                      and twin_compatible(self.policy.actor, self.policy.critic))
 
     def init_storage(self, num_envs, num_steps, obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_steps, obs_shape[0],
@@ -448,8 +532,17 @@ class PPO:
             advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False,
                             enabled=self.precision == "bf16" and str(self.device).startswith("cuda")):
-            self.policy.update_distribution(obs)  # rsl_rl calls act(); the sample itself is unused
-            value = self.policy.evaluate(critic_obs).float()
+            if self._twin and critic_obs is obs:
+                # actor and critic on the same input: batched together (twin_forward), same math
+                n = obs.shape[0]
+                split = SplitKLinear.SPLIT_K if (obs.is_cuda and n >= SplitKLinear.MIN_BATCH
+                                                 and n % SplitKLinear.SPLIT_K == 0) else 1
+                mean, value = twin_forward(self.policy.actor, self.policy.critic, obs, split)
+                self.policy.distribution = Normal(mean, self.policy._std(mean))
+                value = value.float()
+            else:
+                self.policy.update_distribution(obs)  # rsl_rl calls act(); the sample itself is unused
+                value = self.policy.evaluate(critic_obs).float()
         if self.precision == "bf16":  # distribution statistics in fp32
             self.policy.distribution = Normal(self.policy.distribution.mean.float(),
                                               self.policy.distribution.stddev.float())
