@@ -407,9 +407,12 @@ class PPO:
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be fp32 or bf16, got {precision!r}")
         self.precision = precision
-        # actor + critic batched in the learning phase (twin_forward) when their layer shapes match; H12_TWIN=0 turns
-        # it off (A/B)
-        self._twin = (os.environ.get("H12_TWIN", "1") != "0" and hasattr(self.policy, "actor")
+        # actor + critic batched in the learning phase (twin_forward) when their layer shapes match: opt-in
+        # (H12_TWIN=1).  Measured and not the default (round 4, C3 at 4096 envs, A/B on one box,
+        # profiles/r4/r4i_learner_twin_ab.txt): learning 45.0 / 45.4 ms per iteration against 40.9 / 41.5 ms with the
+        # two networks separate -- the 2-batch GEMMs and the larger split-K partial sums cost more than the launches
+        # they save
+        self._twin = (os.environ.get("H12_TWIN", "0") == "1" and hasattr(self.policy, "actor")
                       and twin_compatible(self.policy.actor, self.policy.critic))
 
     def init_storage(self, num_envs, num_steps, obs_shape, critic_obs_shape, action_shape):
