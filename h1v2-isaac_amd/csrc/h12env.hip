@@ -69,6 +69,35 @@ __device__ unsigned long long g_phase[16];
 // [7] / [8] the shader-clock counter (s_memtime) at the start / at [2] -> the XCD's clock rate over the wave,
 // [9] / [10] the cycles this wave waited in barriers R1 / R2 over the launch
 __device__ unsigned long long g_wave[1024][11];
+#ifdef H12_PHASE_LIGHT
+// light mode (-DH12_PHASE_PROFILE -DH12_PHASE_LIGHT): the realtime stamps only, kept in registers and stored once at
+// the wave's end (no per-phase atomics): the least perturbed view of the product kernel's per-XCD timing
+#define PH_INIT() const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime(); \
+  unsigned long long _ph_s1 = 0, _ph_s5 = 0, _ph_s6 = 0
+#define PH_WAVE_END()                                                          \
+  do {                                                                         \
+    const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();           \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
+    const unsigned long long _r2 = __builtin_amdgcn_s_memrealtime();           \
+    unsigned _xcc;                                                             \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));        \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                        \
+      g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
+      g_wave[blockIdx.x][3] = _ph_s1; g_wave[blockIdx.x][4] = _ph_s5; g_wave[blockIdx.x][6] = _ph_s6; \
+      g_wave[blockIdx.x][5] = _xcc & 15u;                                      \
+      g_wave[blockIdx.x][7] = 0; g_wave[blockIdx.x][8] = 0;                     \
+      g_wave[blockIdx.x][9] = 0; g_wave[blockIdx.x][10] = 0;                    \
+    }                                                                          \
+  } while (0)
+#define PH(i)                                                                       \
+  do {                                                                              \
+    if (i == 1) _ph_s1 = __builtin_amdgcn_s_memrealtime();                         \
+    if (i == 5) _ph_s5 = __builtin_amdgcn_s_memrealtime();                         \
+    if (i == 6) _ph_s6 = __builtin_amdgcn_s_memrealtime();                         \
+  } while (0)
+#define PHX_INIT() (void)0
+#define PHX(i) (void)0
+#else
 #define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter(); \
   const unsigned long long _ph_c0 = _ph_t;                                \
   const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime();    \
@@ -105,6 +134,7 @@ __device__ unsigned long long g_wave[1024][11];
       atomicAdd(&g_wave[blockIdx.x][i + 1], _t - _phx_t);                           \
     _phx_t = _t;                                                                    \
   } while (0)
+#endif
 #else
 #define PH_INIT() (void)0
 #define PH_WAVE_END() (void)0
@@ -2477,8 +2507,7 @@ __global__ void __launch_bounds__(64) log_flush_kernel(FoldArgs F) {
   if (threadIdx.x == 0 && acc != 0.f) F.acc[k][log_slot(v)] += acc;
 }
 template <int NH>
-__global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(const KParams* __restrict__ Pd, AsmArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(ASM_BLOCK) obs_assemble_kernel(KParams P, AsmArgs A) {
   const float lacc = log_load(A);
   obs_assemble_body<NH>(P, A);
   log_fold(A, lacc);
@@ -2498,8 +2527,7 @@ H12_DEV float rough_noise(const KParams& P, const AsmArgs& A, int e, int t) {
   return P.corrupt ? (-nmax + 2.f * nmax * u01(rv)) : 0.f;
 }
 
-__global__ void __launch_bounds__(ASM_BLOCK) rough_obs_kernel(const KParams* __restrict__ Pd, AsmArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(ASM_BLOCK) rough_obs_kernel(KParams P, AsmArgs A) {
   log_fold(A, log_load(A));
   const int n = A.n;
   const int gid = blockIdx.x * ASM_BLOCK + threadIdx.x;
@@ -2754,8 +2782,7 @@ H12_DEV void obs_frame_fused(const KParams& P, const EnvSt& s, int leg, int r, b
 }
 
 template <int K>
-__global__ void __launch_bounds__(3 * BLOCK) step_kernel(const KParams* __restrict__ Pd, Workspace W, StepArgs A) {
-  const KParams& P = *Pd;  // device-resident parameters (Handle::dP): scalar loads through K$ / L2
+__global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
     const int nsteps = P.decimation * P.inner;
     FuseCtx fc = {};
@@ -2979,8 +3006,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(const KParams* __restri
 // physics applies on the workspace state as it stands, per env [leg][knee, foot][moment xyz, force xyz] in
 // REAL body coordinates (the oracle's fext layout).
 template <int K>
-__global__ void __launch_bounds__(BLOCK) selfc_kernel(const KParams* __restrict__ Pd, Workspace W, float* out) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(BLOCK) selfc_kernel(KParams P, Workspace W, float* out) {
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
   const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);
@@ -3033,8 +3059,7 @@ struct TermArgs {
   uint8_t* trunc;     // (n,)
 };
 template <int K>
-__global__ void __launch_bounds__(BLOCK) terms_kernel(const KParams* __restrict__ Pd, Workspace W, TermArgs T) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, TermArgs T) {
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
   const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);
@@ -3072,8 +3097,7 @@ __global__ void __launch_bounds__(BLOCK) terms_kernel(const KParams* __restrict_
 // the wave totals.  The column maxima (CaT.add: constraint.max(dim=0)) fold step_kernel's per-block maxima
 // (cpart, formed by its helper wave from LDS: no separate pass over the [col][n] scratch).
 constexpr int CAT_RBLOCK = 1024;
-__global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(const KParams* __restrict__ Pd, int n) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n) {
   __shared__ int s_wsum[CAT_RBLOCK / 64];
   __shared__ int s_base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3141,8 +3165,7 @@ struct CatArgs {
   int log_nb;
 };
 constexpr int CAT_PBLOCK = 64;
-__global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(const KParams* __restrict__ Pd, Workspace W, CatArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspace W, CatArgs A) {
   const int n = W.n;
   const int i = blockIdx.x * CAT_PBLOCK + threadIdx.x;
   if (i >= n) return;
@@ -3201,8 +3224,7 @@ __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(const KParams* __r
 }
 
 template <int K>
-__global__ void __launch_bounds__(BLOCK) reset_kernel(const KParams* __restrict__ Pd, Workspace W, StepArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(BLOCK) reset_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
@@ -3221,8 +3243,7 @@ __global__ void __launch_bounds__(BLOCK) reset_kernel(const KParams* __restrict_
 // ObservationManager.compute() outside step(): new frame from the current state, history shifted
 // (or filled where fill_mask[e]); RNG counter domain (observe call, 0xFFFFFFFE)
 template <int K>
-__global__ void __launch_bounds__(BLOCK) observe_kernel(const KParams* __restrict__ Pd, Workspace W, StepArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(BLOCK) observe_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
@@ -3236,8 +3257,7 @@ __global__ void __launch_bounds__(BLOCK) observe_kernel(const KParams* __restric
 
 // parity hook (h12env_step_physics): n_substeps physics steps, PD to held q_ref every physics step
 template <int K>
-__global__ void __launch_bounds__(BLOCK) physics_kernel(const KParams* __restrict__ Pd, Workspace W, StepArgs A) {
-  const KParams& P = *Pd;
+__global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, StepArgs A) {
   const int lane_pair = threadIdx.x >> 1;
   const int leg = threadIdx.x & 1;
   const float sg = leg ? -1.f : 1.f;
@@ -3380,18 +3400,6 @@ __global__ void __launch_bounds__(DEC_BLOCK) rollout_decode_kernel(DecArgs D) {
 // ------------------------------------------------------------------ host side
 struct Handle {
   KParams P;
-  // device-resident copy of P for the physics kernels (step_kernel, physics_kernel): their loops re-read the
-  // parameters with scalar loads, and the runtime's default kernel-argument segment is not cached like device
-  // memory -- each re-read was a round trip (HIP_FORCE_DEV_KERNARG=1 measured 3.5-4 us per launch faster in the
-  // physics phase on every XCD, profiles/r4/r4j.txt).  Uploaded on the launch stream when P changes (P_up: the
-  // host copy of what dP holds).
-  KParams* dP = nullptr;
-  mutable KParams P_up;
-  mutable bool P_ok = false;
-  // pinned staging slots of the uploads (a slot is rewritten only after the event recorded behind its copy)
-  KParams* P_stage = nullptr;
-  hipEvent_t P_ev[4] = {};
-  mutable int P_slot = 0;
   Workspace W;
   bool own;
   int device;
@@ -3694,30 +3702,11 @@ int feature_level(const KParams& P) {
     }                                                                                                       \
   } while (0)
 
-// h->dP with the current parameters, uploaded on `stream` when P changed since the last upload (stream order makes
-// it visible to the kernels launched after it; the host copy P_up outlives the copy)
-const KParams* dev_params(const Handle* h, hipStream_t stream) {
-  if (!h->P_ok || std::memcmp(&h->P_up, &h->P, sizeof(KParams)) != 0) {
-    const int k = h->P_slot;
-    h->P_slot = (k + 1) % 4;
-    if (hipEventSynchronize(h->P_ev[k]) != hipSuccess) return nullptr;  // slot k's previous copy has run
-    h->P_stage[k] = h->P;
-    if (hipMemcpyAsync(h->dP, &h->P_stage[k], sizeof(KParams), hipMemcpyHostToDevice, stream) != hipSuccess ||
-        hipEventRecord(h->P_ev[k], stream) != hipSuccess)
-      return nullptr;
-    h->P_up = h->P;
-    h->P_ok = true;
-  }
-  return h->dP;
-}
-
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
                     hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, float* log_acc = nullptr,
                     float* frame_out = nullptr, float* log_part = nullptr) {
-  const KParams* dp = dev_params(h, stream);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
   AsmArgs A = {};
   A.frame_out = frame_out;
   A.log_part = log_part;
@@ -3738,7 +3727,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   if (h->P.task == H12_TASK_ROUGH) {
     if (frame_out) return set_err(H12_E_ARG, "frame_out needs the flat observation layout (history)");
     const int nb = (int)(((size_t)h->W.n * H12_NOBS_ROUGH + ASM_BLOCK - 1) / ASM_BLOCK);
-    hipExtLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, dp, A);
+    hipExtLaunchKernelGGL(rough_obs_kernel, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, h->P, A);
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -3746,7 +3735,7 @@ int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const ui
   A.vec = (((uintptr_t)obs | (uintptr_t)src) & 15u) == 0;
   const int nb = (h->W.n + ASM_ROWS - 1) / ASM_ROWS;
 #define H12_ASM_CASE(NH) \
-  case NH: hipExtLaunchKernelGGL(obs_assemble_kernel<NH>, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, dp, A); break;
+  case NH: hipExtLaunchKernelGGL(obs_assemble_kernel<NH>, dim3(nb), dim3(ASM_BLOCK), 0, stream, e0, e1, 0, h->P, A); break;
   switch (h->P.hist) {
     H12_ASM_CASE(1) H12_ASM_CASE(2) H12_ASM_CASE(3) H12_ASM_CASE(4) H12_ASM_CASE(5)
     H12_ASM_CASE(6) H12_ASM_CASE(7) H12_ASM_CASE(8) H12_ASM_CASE(9) H12_ASM_CASE(10)
@@ -3911,9 +3900,6 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   const size_t log_bytes = sizeof(float) * LOG_RING * LOG_NPART * (size_t)((n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK);
   if (e == hipSuccess) e = hipMalloc(&h->log_part, log_bytes);
   if (e == hipSuccess) e = hipMemset(h->log_part, 0, log_bytes);
-  if (e == hipSuccess) e = hipMalloc(&h->dP, sizeof(KParams));
-  if (e == hipSuccess) e = hipHostMalloc((void**)&h->P_stage, 4 * sizeof(KParams), hipHostMallocDefault);
-  for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&h->P_ev[k], hipEventDisableTiming);
   if (e != hipSuccess) {
     if (h->own) (void)hipFree(state_dev);
     (void)hipFree(h->frame);
@@ -3985,10 +3971,6 @@ void h12env_destroy(h12env* hh) {
   if (h->frame) (void)hipFree(h->frame);
   if (h->dz_cnt) (void)hipFree(h->dz_cnt);
   if (h->log_part) (void)hipFree(h->log_part);
-  if (h->dP) (void)hipFree(h->dP);
-  if (h->P_stage) (void)hipHostFree(h->P_stage);
-  for (hipEvent_t e : h->P_ev)
-    if (e) (void)hipEventDestroy(e);
   if (h->cat_mem) (void)hipFree(h->cat_mem);
   if (h->asm_tab) (void)hipFree(h->asm_tab);
   if (h->fuse_code) (void)hipFree(h->fuse_code);
@@ -4009,9 +3991,7 @@ int h12env_reset(h12env* hh, const uint8_t* mask, float* obs, void* stream) {
   A.hi = 0xFFFFFFFFu;
   A.frame = h->frame;
   h->reset_calls++;
-  const KParams* dp = dev_params(h, (hipStream_t)stream);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
-  LAUNCH_K(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, dp, h->W, A);
+  LAUNCH_K(reset_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return launch_assemble(h, nullptr, obs, nullptr, nullptr, mask, 1, A.lo, A.hi, (hipStream_t)stream);
 }
@@ -4081,18 +4061,16 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   hipEvent_t k0, k1;
   timing_events(h, 0, &k0, &k1);
   // every block carries a helper wave and, with self-collision, a self-contact wave (helper_wave, self_wave)
-  const KParams* dp = dev_params(h, st);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
   LAUNCH_KT(step_kernel, k0, k1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 3 : 2) * BLOCK),
-            A.fuse ? sizeof(FuseLds) : 0, st, dp, h->W, A);
+            A.fuse ? sizeof(FuseLds) : 0, st, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
   if (h->P.cat) {
-    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, st, dp, h->W.n);
+    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, st, h->P, h->W.n);
     HIP_TRY(hipGetLastError());
     static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
     CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
-    hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0, st, dp,
+    hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0, st, h->P,
                        h->W, C);
     HIP_TRY(hipGetLastError());
   }
@@ -4125,9 +4103,7 @@ int h12env_observe(h12env* hh, const float* obs_prev, float* obs, const uint8_t*
   A.hi = 0xFFFFFFFEu;
   h->observe_calls++;
   A.frame = h->frame;
-  const KParams* dp = dev_params(h, (hipStream_t)stream);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
-  LAUNCH_K(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, dp, h->W, A);
+  LAUNCH_K(observe_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return launch_assemble(h, obs_prev, obs, fill_mask, nullptr, nullptr, 0, A.lo, A.hi, (hipStream_t)stream);
 }
@@ -4139,9 +4115,7 @@ int h12env_step_physics(h12env* hh, const float* q_ref, int n_substeps, void* st
   StepArgs A = {};
   A.q_ref = q_ref;
   A.n_substeps = n_substeps;
-  const KParams* dp = dev_params(h, (hipStream_t)stream);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
-  LAUNCH_K(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, dp, h->W, A);
+  LAUNCH_K(physics_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -4153,15 +4127,10 @@ int h12env_eval_terms(h12env* hh, const float* tau, const float* jacc, const flo
   if (!tau || !jacc || !fmax || !terms || !terminated || !truncated)
     return set_err(H12_E_ARG, "tau, jacc, fmax, terms, terminated, truncated are required");
   if (h->P.cat && !cstr) return set_err(H12_E_ARG, "cstr is required on a CaT env");
-  // the constraint rows go to the caller's buffer, not the step's scratch: a parameter set of its own for this
-  // launch (uploaded like any change of P; the next launch of another kernel uploads the handle's own set again)
-  float* const cscr = h->P.cscr;
-  if (h->P.cat) h->P.cscr = cstr;
-  const KParams* dp = dev_params(h, (hipStream_t)stream);
-  h->P.cscr = cscr;
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
+  KParams P = h->P;
+  if (P.cat) P.cscr = cstr;  // the constraint rows go to the caller's buffer, not the step's scratch
   TermArgs T = {tau, jacc, fmax, terms, terminated, truncated};
-  LAUNCH_K(terms_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, dp, h->W, T);
+  LAUNCH_K(terms_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, P, h->W, T);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -4171,9 +4140,7 @@ int h12env_eval_self_contacts(h12env* hh, float* out, void* stream) {
   if (!h) return set_err(H12_E_ARG, "null handle");
   if (!out) return set_err(H12_E_ARG, "out is required");
   if (!h->P.self_coll) return set_err(H12_E_STATE, "self_collision is off in this env's config");
-  const KParams* dp = dev_params(h, (hipStream_t)stream);
-  if (!dp) return set_err(H12_E_HIP, "parameter upload failed");
-  LAUNCH_K(selfc_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, dp, h->W, out);
+  LAUNCH_K(selfc_kernel, dim3(n_blocks(h)), dim3(BLOCK), 0, (hipStream_t)stream, h->P, h->W, out);
   HIP_TRY(hipGetLastError());
   return 0;
 }
