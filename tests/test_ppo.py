@@ -177,3 +177,30 @@ def test_twin_incompatible_shapes_fall_back():
 
     pol = ActorCritic(45, 50, 12, actor_hidden_dims=(64, 32), critic_hidden_dims=(64, 16))
     assert not twin_compatible(pol.actor, pol.critic)
+
+
+@pytest.mark.parametrize("split", [1, 4])
+def test_fused_mlp_matches_modules(split):
+    """_MLPFn (bias gradients folded into the split-K weight-gradient GEMMs through a ones column) == the per-layer
+    modules, in outputs and in every parameter gradient."""
+    from h12env.ppo import ActorCritic, fused_mlp, fused_mlp_ok
+
+    torch.manual_seed(1)
+    pol = ActorCritic(45, 45, 12, actor_hidden_dims=(64, 32, 16), critic_hidden_dims=(64, 32, 16))
+    for net, k in ((pol.actor, 12), (pol.critic, 1)):
+        assert fused_mlp_ok(net)
+        x = torch.randn(64, 45)
+        g = torch.randn(64, k)
+        for p in net.parameters():
+            p.grad = None
+        y0 = net(x)
+        (y0 * g).sum().backward()
+        g0 = [p.grad.clone() for p in net.parameters()]
+        for p in net.parameters():
+            p.grad = None
+        y1 = fused_mlp(net, x, split)
+        (y1 * g).sum().backward()
+        g1 = [p.grad.clone() for p in net.parameters()]
+        torch.testing.assert_close(y1, y0, rtol=1e-5, atol=1e-6)
+        for a, b in zip(g1, g0):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
