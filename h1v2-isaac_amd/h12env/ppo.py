@@ -493,8 +493,8 @@ class PPO:
         # profiles/r4/r4i_learner_twin_ab.txt): learning 45.0 / 45.4 ms per iteration against 40.9 / 41.5 ms with the
         # two networks separate -- the 2-batch GEMMs and the larger split-K partial sums cost more than the launches
         # they save
-        # the fused MLP node (_MLPFn) for the fp32 learning phase; H12_FUSED_MLP=0 selects the per-layer modules
-        self._fused_mlp = (os.environ.get("H12_FUSED_MLP", "1") != "0" and hasattr(self.policy, "actor")
+        # the fused MLP node (_MLPFn) for the fp32 learning phase (H12_FUSED_MLP=1; default: the per-layer modules)
+        self._fused_mlp = (os.environ.get("H12_FUSED_MLP", "0") == "1" and hasattr(self.policy, "actor")
                            and fused_mlp_ok(self.policy.actor) and fused_mlp_ok(self.policy.critic))
         self._twin = (os.environ.get("H12_TWIN", "0") == "1" and hasattr(self.policy, "actor")
                       and twin_compatible(self.policy.actor, self.policy.critic))
