@@ -85,167 +85,6 @@ class SplitKLinear(nn.Linear):
         return nn.functional.linear(x, self.weight, self.bias)
 
 
-class _TwinLinearFn(torch.autograd.Function):
-    """Two independent linear layers as ONE batched GEMM: y[k] = x[k] W[k]^T + b[k] for k in (actor, critic), x
-    (2, B, in) (any batch stride: a (B, 2 in) activation viewed as (2, B, in) is read in place), W (2, out, in).  The
-    weight gradient is split-K over the minibatch like _SplitKLinearFn (2 x split batched GEMMs, summed)."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, split, dt):
-        with torch.autocast(device_type="cuda", enabled=False):
-            xc, wc = x.to(dt), w.to(dt)
-            ctx.save_for_backward(xc, wc)
-            ctx.split, ctx.x_dtype = split, x.dtype
-            return torch.baddbmm(b.to(dt).unsqueeze(1), xc, wc.transpose(1, 2))
-
-    @staticmethod
-    def backward(ctx, gy):
-        xc, wc = ctx.saved_tensors
-        s, n = ctx.split, xc.shape[1]
-        with torch.autocast(device_type="cuda", enabled=False):
-            gy = gy.to(wc.dtype)
-            gx = torch.bmm(gy, wc).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
-            if s > 1 and n % s == 0:
-                xs = xc.reshape(2 * s, n // s, xc.shape[2]) if xc.is_contiguous() else \
-                    xc.contiguous().view(2 * s, n // s, xc.shape[2])
-                gw = torch.bmm(gy.reshape(2 * s, n // s, -1).transpose(1, 2), xs).view(2, s, wc.shape[1], wc.shape[2])
-                gw = gw.sum(1) if gw.dtype == torch.float32 else gw.float().sum(1)
-            else:
-                gw = torch.bmm(gy.transpose(1, 2), xc).float()
-            return gx, gw, gy.float().sum(1), None, None
-
-
-AUG = 4  # hidden activations carry AUG extra columns (a ones column + padding that keeps rows 16-byte aligned)
-
-
-class _MLPFn(torch.autograd.Function):
-    """A whole Linear-ELU-...-Linear MLP as one autograd node (fp32 learning phase): each hidden activation is written
-    into a (B, width + AUG) buffer whose column `width` is 1, so the split-K weight-gradient GEMM of the next layer,
-    run on that buffer, returns the layer's bias gradient as its extra column -- no separate reduction over the
-    24 576-row minibatch per layer (13 % of the learner's GPU time were reductions).  ELU's
-    derivative comes from its output (alpha = 1: 1 where y > 0, else y + 1).  The first layer's bias gradient is a
-    plain reduction (its input is the observation batch)."""
-
-    @staticmethod
-    def forward(ctx, x, split, *params):
-        n = x.shape[0]
-        ws, bs = params[0::2], params[1::2]
-        acts = []
-        h = x
-        for k, (w, b) in enumerate(zip(ws, bs)):
-            z = torch.addmm(b, h, w.t())
-            if k == len(ws) - 1:
-                out = z
-                break
-            width = z.shape[1]
-            a = torch.empty(n, width + AUG, device=x.device, dtype=z.dtype)
-            a[:, width:].zero_()
-            a[:, width].fill_(1.0)
-            torch.ops.aten.elu.out(z, 1.0, 1.0, 1.0, out=a[:, :width])
-            acts.append(a)
-            h = a[:, :width]
-        ctx.save_for_backward(x, *acts, *ws)
-        ctx.split, ctx.n_layers = split, len(ws)
-        return out
-
-    @staticmethod
-    def backward(ctx, gy):
-        saved = ctx.saved_tensors
-        L = ctx.n_layers
-        x, acts, ws = saved[0], saved[1:L], saved[L:]
-        s, n = ctx.split, x.shape[0]
-        grads_w, grads_b = [None] * L, [None] * L
-        g = gy.contiguous()
-        for k in range(L - 1, -1, -1):
-            out_k = g.shape[1]
-            gs = g.view(s, n // s, out_k).transpose(1, 2)
-            if k > 0:
-                a = acts[k - 1]
-                width = a.shape[1] - AUG
-                gw = torch.bmm(gs, a.view(s, n // s, width + AUG)).sum(0)
-                grads_w[k], grads_b[k] = gw[:, :width], gw[:, width]
-                gh = g @ ws[k]
-                y = a[:, :width]
-                g = torch.where(y > 0, gh, gh * (y + 1.0))
-            else:
-                grads_w[0] = torch.bmm(gs, x.view(s, n // s, x.shape[1])).sum(0)
-                grads_b[0] = g.sum(0)
-        out = [None, None]
-        for gw, gb in zip(grads_w, grads_b):
-            out += [gw, gb]
-        return tuple(out)
-
-
-def fused_mlp_ok(net: nn.Sequential) -> bool:
-    """True for the agents' MLPs (Linear layers with ELU(alpha=1) between them) -- what _MLPFn computes."""
-    mods = list(net)
-    if len(mods) < 3 or len(mods) % 2 == 0:
-        return False
-    for i, m in enumerate(mods):
-        if i % 2 == 0 and not isinstance(m, nn.Linear):
-            return False
-        if i % 2 == 1 and not (isinstance(m, nn.ELU) and m.alpha == 1.0):
-            return False
-    return True
-
-
-def fused_mlp(net: nn.Sequential, x: torch.Tensor, split: int) -> torch.Tensor:
-    params = []
-    for m in list(net)[0::2]:
-        params += [m.weight, m.bias]
-    return _MLPFn.apply(x, split, *params)
-
-
-def twin_compatible(actor: nn.Sequential, critic: nn.Sequential) -> bool:
-    """True when the two MLPs have the same hidden layer shapes and activations (the Flat / Rough / Rsl agents:
-    [512, 256, 128] ELU for both, C12/agents/rsl_rl_ppo_cfg.py:17-21), so their hidden layers batch pairwise."""
-    a, c = list(actor), list(critic)
-    if len(a) != len(c) or len(a) < 3:
-        return False
-    for la, lc in zip(a[:-1], c[:-1]):
-        if isinstance(la, nn.Linear) != isinstance(lc, nn.Linear) or type(la) is not type(lc):
-            return False
-        if isinstance(la, nn.Linear) and (la.in_features, la.out_features) != (lc.in_features, lc.out_features):
-            return False
-    return isinstance(a[-1], nn.Linear) and isinstance(c[-1], nn.Linear) and a[-1].in_features == c[-1].in_features
-
-
-def twin_forward(actor: nn.Sequential, critic: nn.Sequential, x: torch.Tensor, split: int = 1):
-    """(actor(x), critic(x)) for one input, the two networks evaluated together (learning phase): the first layer as
-    one GEMM with the two weight matrices stacked along the output (N = 2 x 512), the hidden layers as 2-batch GEMMs,
-    the output layers as one 2-batch GEMM with the critic's single row zero-padded to the actor's width; every
-    activation is one elementwise kernel over both networks.  Same math as the two separate forwards (fp32
-    summation order aside); gradients reach each network's own parameters through the stacks."""
-    a, c = list(actor), list(critic)
-    dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) else torch.float32
-    l0a, l0c = a[0], c[0]
-    w0 = torch.cat([l0a.weight, l0c.weight], 0)
-    b0 = torch.cat([l0a.bias, l0c.bias], 0)
-    ok_split = split > 1 and x.shape[0] % split == 0
-    if ok_split:
-        h = _SplitKLinearFn.apply(x, w0, b0, split, dt)
-    else:
-        with torch.autocast(device_type="cuda", enabled=False):
-            h = nn.functional.linear(x.to(dt), w0.to(dt), b0.to(dt))
-    h = a[1](h)  # the activation over both halves at once
-    width = l0a.out_features
-    h = h.view(h.shape[0], 2, width).transpose(0, 1)  # (2, B, width), strided: no copy
-    for i in range(2, len(a) - 1, 2):
-        la, lc = a[i], c[i]
-        w = torch.stack([la.weight, lc.weight])
-        b = torch.stack([la.bias, lc.bias])
-        h = a[i + 1](_TwinLinearFn.apply(h, w, b, split if ok_split else 1, dt))
-    la, lc = a[-1], c[-1]
-    pad = la.out_features - lc.out_features
-    if pad >= 0:
-        wc = torch.cat([lc.weight, lc.weight.new_zeros(pad, lc.in_features)], 0)
-        bc = torch.cat([lc.bias, lc.bias.new_zeros(pad)], 0)
-        y = _TwinLinearFn.apply(h, torch.stack([la.weight, wc]), torch.stack([la.bias, bc]),
-                                split if ok_split else 1, dt)
-        return y[0], y[1, :, :lc.out_features]
-    return la(h[0]), lc(h[1])
-
-
 def mlp(n_in: int, hidden: list[int], n_out: int, act: str) -> nn.Sequential:
     layers: list[nn.Module] = []
     d = n_in
@@ -488,16 +327,6 @@ class PPO:
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be fp32 or bf16, got {precision!r}")
         self.precision = precision
-        # actor + critic batched in the learning phase (twin_forward) when their layer shapes match: opt-in
-        # (H12_TWIN=1).  Measured and not the default (round 4, C3 at 4096 envs, A/B on one box,
-        # profiles/r4/r4i_learner_twin_ab.txt): learning 45.0 / 45.4 ms per iteration against 40.9 / 41.5 ms with the
-        # two networks separate -- the 2-batch GEMMs and the larger split-K partial sums cost more than the launches
-        # they save
-        # the fused MLP node (_MLPFn) for the fp32 learning phase (H12_FUSED_MLP=1; default: the per-layer modules)
-        self._fused_mlp = (os.environ.get("H12_FUSED_MLP", "0") == "1" and hasattr(self.policy, "actor")
-                           and fused_mlp_ok(self.policy.actor) and fused_mlp_ok(self.policy.critic))
-        self._twin = (os.environ.get("H12_TWIN", "0") == "1" and hasattr(self.policy, "actor")
-                      and twin_compatible(self.policy.actor, self.policy.critic))
 
     def init_storage(self, num_envs, num_steps, obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_steps, obs_shape[0],
@@ -619,23 +448,8 @@ class PPO:
             advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False,
                             enabled=self.precision == "bf16" and str(self.device).startswith("cuda")):
-            if self._twin and critic_obs is obs:
-                # actor and critic on the same input: batched together (twin_forward), same math
-                n = obs.shape[0]
-                split = SplitKLinear.SPLIT_K if (obs.is_cuda and n >= SplitKLinear.MIN_BATCH
-                                                 and n % SplitKLinear.SPLIT_K == 0) else 1
-                mean, value = twin_forward(self.policy.actor, self.policy.critic, obs, split)
-                self.policy.distribution = Normal(mean, self.policy._std(mean))
-                value = value.float()
-            elif self._fused_mlp and obs.is_cuda and obs.shape[0] >= SplitKLinear.MIN_BATCH \
-                    and obs.shape[0] % SplitKLinear.SPLIT_K == 0 and self.precision == "fp32":
-                # each network as one autograd node with the bias gradients folded into the weight-gradient GEMMs
-                mean = fused_mlp(self.policy.actor, obs, SplitKLinear.SPLIT_K)
-                self.policy.distribution = Normal(mean, self.policy._std(mean))
-                value = fused_mlp(self.policy.critic, critic_obs, SplitKLinear.SPLIT_K).float()
-            else:
-                self.policy.update_distribution(obs)  # rsl_rl calls act(); the sample itself is unused
-                value = self.policy.evaluate(critic_obs).float()
+            self.policy.update_distribution(obs)  # rsl_rl calls act(); the sample itself is unused
+            value = self.policy.evaluate(critic_obs).float()
         if self.precision == "bf16":  # distribution statistics in fp32
             self.policy.distribution = Normal(self.policy.distribution.mean.float(),
                                               self.policy.distribution.stddev.float())

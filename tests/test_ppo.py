@@ -142,65 +142,3 @@ def test_two_rank_noise_differs_and_normaliser_is_shared():
     assert res[0][1] != res[1][1]          # exploration noise differs between ranks
     assert res[0][2] == res[1][2]          # normaliser statistics identical
 
-
-@pytest.mark.parametrize("split", [1, 4])
-def test_twin_forward_matches_separate_networks(split):
-    """twin_forward (actor and critic batched in the learning phase) == the two separate forwards, in values and in
-    every parameter gradient (fp32; the summation order of the split-K weight gradient differs)."""
-    from h12env.ppo import ActorCritic, twin_compatible, twin_forward
-
-    torch.manual_seed(0)
-    pol = ActorCritic(45, 45, 12, actor_hidden_dims=(64, 32, 16), critic_hidden_dims=(64, 32, 16))
-    assert twin_compatible(pol.actor, pol.critic)
-    x = torch.randn(64, 45)
-    gm, gv = torch.randn(64, 12), torch.randn(64, 1)
-
-    def grads(mean, value):
-        for p in pol.parameters():
-            p.grad = None
-        ((mean * gm).sum() + (value * gv).sum()).backward()
-        return [p.grad.clone() for p in pol.parameters() if p.grad is not None]
-
-    m0, v0 = pol.actor(x), pol.critic(x)
-    g0 = grads(m0, v0)
-    m1, v1 = twin_forward(pol.actor, pol.critic, x, split)
-    g1 = grads(m1, v1)
-    torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-6)
-    assert len(g1) == len(g0)
-    for a, b in zip(g1, g0):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
-
-
-def test_twin_incompatible_shapes_fall_back():
-    from h12env.ppo import ActorCritic, twin_compatible
-
-    pol = ActorCritic(45, 50, 12, actor_hidden_dims=(64, 32), critic_hidden_dims=(64, 16))
-    assert not twin_compatible(pol.actor, pol.critic)
-
-
-@pytest.mark.parametrize("split", [1, 4])
-def test_fused_mlp_matches_modules(split):
-    """_MLPFn (bias gradients folded into the split-K weight-gradient GEMMs through a ones column) == the per-layer
-    modules, in outputs and in every parameter gradient."""
-    from h12env.ppo import ActorCritic, fused_mlp, fused_mlp_ok
-
-    torch.manual_seed(1)
-    pol = ActorCritic(45, 45, 12, actor_hidden_dims=(64, 32, 16), critic_hidden_dims=(64, 32, 16))
-    for net, k in ((pol.actor, 12), (pol.critic, 1)):
-        assert fused_mlp_ok(net)
-        x = torch.randn(64, 45)
-        g = torch.randn(64, k)
-        for p in net.parameters():
-            p.grad = None
-        y0 = net(x)
-        (y0 * g).sum().backward()
-        g0 = [p.grad.clone() for p in net.parameters()]
-        for p in net.parameters():
-            p.grad = None
-        y1 = fused_mlp(net, x, split)
-        (y1 * g).sum().backward()
-        g1 = [p.grad.clone() for p in net.parameters()]
-        torch.testing.assert_close(y1, y0, rtol=1e-5, atol=1e-6)
-        for a, b in zip(g1, g0):
-            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
