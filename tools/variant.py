@@ -21,14 +21,6 @@ PATCHES = {
     # the helper waves' shifted-row stores during the physics loop dropped (timing only: the rows are wrong)
     "no_early": [("  for (int k = k0; k < k1; ++k) {\n    const int j = t + k * nt;",
                   "  for (int k = k0; k < k0; ++k) {\n    const int j = t + k * nt;")],
-    # the observation-row stores (shifted rows, newest slot via st_row4) with the nt (streaming) policy
-    "nt_rows": [("                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,\n                                         0);",
-                 "                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,\n                                         2);")],
-    # ... and the state write-back too
-    "nt_all": [("                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,\n                                         0);",
-                "                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,\n                                         2);"),
-               ("st_F(W), (e + lf * W.n) * 4, f * W.n * 4, 0);", "st_F(W), (e + lf * W.n) * 4, f * W.n * 4, 2);"),
-               ("(uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, 0);", "(uint32_t)x, st_I(W), (e + lf * W.n) * 4, f * W.n * 4, 2);")],
     # the state write-back dropped (timing only: the state never advances)
     "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
 }
