@@ -486,6 +486,17 @@ def main():
                 or args.inner_steps is not None or args.explicit_penalty):  # tools/profile.sh: the default workload
             pmc, pmc_src = {}, "not collected for this workload (tools/profile.sh profiles the default flat line)"
         traffic = pmc.get("step_kernel", {}).get("hbm_bytes_per_launch")
+        # algorithmic read / write split of the fused Flat step (h12env_kernel_cost(0): state fields read and written,
+        # actions read, reward / flags / applied torque / foot force written, the row's H-1 old frames read and its H
+        # frames written) beside the PMC's
+        split = None
+        if traffic is not None and env.obs_fused:
+            row = float(env.obs_dim)  # floats per observation row (H frames of 45)
+            fields4 = (bytes_env - 110.0 - (2.0 * row - 45.0) * 4.0) / 2.0
+            rd = fields4 + 48.0 + (row - 45.0) * 4.0
+            k = pmc.get("step_kernel", {})
+            split = {"algorithmic_read": rd * n, "algorithmic_write": (bytes_env - rd) * n,
+                     "pmc_read": k.get("hbm_read_bytes_per_launch"), "pmc_write": k.get("hbm_write_bytes_per_launch")}
         # kernel 1 of the timing / cost pairs: the observation assembly kernel, or -- when step_kernel assembles the
         # rows itself (env.obs_fused) -- the deferred episode-log fold, launched once per <= 32 steps
         fused = env.obs_fused
@@ -561,6 +572,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_split": split,
                 "kernel": "step_kernel",
                 "kernel_ms_avg": kern_ms_avg,
                 "kernel_timing": "HIP event pair bound to each dispatch (hipExtLaunchKernelGGL), replayed window",
