@@ -21,6 +21,9 @@ PATCHES = {
     # the helper waves' shifted-row stores during the physics loop dropped (timing only: the rows are wrong)
     "no_early": [("  for (int k = k0; k < k1; ++k) {\n    const int j = t + k * nt;",
                   "  for (int k = k0; k < k0; ++k) {\n    const int j = t + k * nt;")],
+    # the Rough observation's height scan without its heightfield gathers (timing only: the scan reads 0)
+    "scan_nogather": [("      hz = ground(P, px + cy * xl - sy * yl, py + sy * xl + cy * yl, gx, gy);",
+                       "      hz = 0.f * (px + cy * xl - sy * yl) * (py + sy * xl + cy * yl); gx = gy = 0.f;")],
     # the state write-back dropped (timing only: the state never advances)
     "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
 }
