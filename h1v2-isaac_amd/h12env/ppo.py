@@ -290,6 +290,22 @@ class RolloutStorage:
 
 
 # ---------------------------------------------------------------------------------------------- PPO
+def enable_tunable_gemm():
+    """PyTorch's TunableOp for the learner's GEMMs: the first call of each GEMM shape times the available
+    hipBLASLt / rocBLAS solutions and keeps the fastest for the process (the minibatch shapes are fixed, so a few
+    seconds once per run).  Round 4, C3 at 4096 envs, 2 runs each: learning 38.6 / 38.5 ms per iteration against 41.3
+    / 40.8 ms with the default heuristics (profiles/r4/r4t_blas_tunableop_ab.txt).  Process-wide; H12_TUNABLEOP=0
+    turns it off.  The tuning table goes to the temp directory, not the working directory."""
+    import tempfile
+
+    t = torch.cuda.tunable
+    if not t.is_enabled():
+        if not os.environ.get("PYTORCH_TUNABLEOP_FILENAME"):
+            t.set_filename(os.path.join(tempfile.gettempdir(), f"h12env_tunableop_{os.getpid()}_%d.csv"))
+        t.enable(True)
+        t.tuning_enable(True)
+
+
 class PPO:
     """Clipped-surrogate PPO with clipped value loss, entropy bonus and KL-adaptive learning rate
     (rsl_rl 2.3 algorithms/ppo.py semantics)."""
@@ -302,6 +318,8 @@ class PPO:
         self.policy = policy.to(device)
         self.actor_critic = self.policy  # rsl_rl < 2.3 name
         self.device = device
+        if str(device).startswith("cuda") and os.environ.get("H12_TUNABLEOP", "1") != "0":
+            enable_tunable_gemm()
         # fused Adam (one kernel for all parameters) on the GPU with the learning rate as a device tensor, so
         # the KL-adaptive schedule runs on the device (no host sync per minibatch); plain Adam on CPU
         fused = str(device).startswith("cuda")
