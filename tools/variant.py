@@ -24,6 +24,18 @@ PATCHES = {
     # the Rough observation's height scan without its heightfield gathers (timing only: the scan reads 0)
     "scan_nogather": [("      hz = ground(P, px + cy * xl - sy * yl, py + sy * xl + cy * yl, gx, gy);",
                        "      hz = 0.f * (px + cy * xl - sy * yl) * (py + sy * xl + cy * yl); gx = gy = 0.f;")],
+    # probe: 300 VALU of dependent dummy work in the self-contact wave before R1 (its slack there)
+    "self_slack150": [("      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];",
+                        "      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n" + '      {  // probe: N dependent FMAs of dummy work in the self-contact wave before R1 (its slack there)\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < NDUMMY; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile("" :: "v"(d0), "v"(d1));\n      }\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];'.replace("NDUMMY", "150"))],
+    # probe: 600 VALU of dependent dummy work in the self-contact wave before R1 (its slack there)
+    "self_slack300": [("      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];",
+                        "      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n" + '      {  // probe: N dependent FMAs of dummy work in the self-contact wave before R1 (its slack there)\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < NDUMMY; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile("" :: "v"(d0), "v"(d1));\n      }\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];'.replace("NDUMMY", "300"))],
+    # probe: 1200 VALU of dependent dummy work in the self-contact wave before R1 (its slack there)
+    "self_slack600": [("      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];",
+                        "      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);\n" + '      {  // probe: N dependent FMAs of dummy work in the self-contact wave before R1 (its slack there)\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < NDUMMY; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile("" :: "v"(d0), "v"(d1));\n      }\n    }\n    __syncthreads();  // R1\n    if (active) {\n      float w[12];'.replace("NDUMMY", "600"))],
+    # probe: 600 VALU of dependent dummy work in the helper wave before R1 (its slack there)
+    "helper_slack300": [("      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n    }\n    __syncthreads();  // R1",
+                         "      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n      {\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < 300; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile(\"\" :: \"v\"(d0), \"v\"(d1));\n      }\n    }\n    __syncthreads();  // R1")],
     # the state write-back dropped (timing only: the state never advances)
     "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
 }
