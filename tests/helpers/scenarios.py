@@ -70,4 +70,34 @@ def lying(model, Fm, rng):
     return Fm
 
 
+def lying_terrain(model, Fm, rng, terrain):
+    """`lying` on the Rough heightfield: each robot at its env origin (H12_F_ORIGIN, +-0.5 m), the body placed so that
+    the deepest of the torso box's 8 corners is 0-4 mm below the heightfield under it (h12env.terrain.ground_height,
+    the kernels' triangle interpolation) -- the heightfield contact path (ground_local, torso_face on terrain)."""
+    from h12env.terrain import ground_height
+
+    n = Fm.shape[1]
+    ch = np.array(model.torso_center, dtype=np.float64)
+    hh = np.array(model.torso_half, dtype=np.float64)
+    signs = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], dtype=np.float64)
+    o, _ = FIELDS["ORIGIN"]
+    for i in range(n):
+        pitch = rng.uniform(np.deg2rad(80), np.deg2rad(100)) * (1 if i % 2 else -1)
+        quat = _quat(rng.uniform(-0.2, 0.2), pitch, rng.uniform(-np.pi, np.pi))
+        s = np.zeros(37)
+        s[3:7] = quat
+        s[13:25] = np.asarray(model.q_default) + rng.normal(size=12) * 0.05
+        R, p = O.body_poses(model, s)
+        c = (R[0] @ (ch[None] + signs * hh[None]).T).T + p[0]  # corners relative to the base position
+        x, y = Fm[o, i] + rng.uniform(-0.5, 0.5), Fm[o + 1, i] + rng.uniform(-0.5, 0.5)
+        g = ground_height(terrain, x + c[:, 0], y + c[:, 1])
+        _set(Fm, "POS", i, [x, y, float(np.max(g - c[:, 2])) - rng.uniform(0.0, 0.004)])
+        _set(Fm, "QUAT", i, quat)
+        _set(Fm, "VLIN", i, rng.normal(size=3) * 0.1)
+        _set(Fm, "WANG", i, rng.normal(size=3) * 0.1)
+        _set(Fm, "Q", i, s[13:25])
+        _set(Fm, "QD", i, 0.0)
+    return Fm
+
+
 SCENARIOS = dict(flight=flight, lying=lying)

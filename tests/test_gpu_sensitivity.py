@@ -22,7 +22,7 @@ from forced import SCEN_GATE, ForcedParity
 from h12env import H12FlatEnvCfg, mujoco_cfg
 from h12env._abi import F as FIELDS
 from h12env.env import H12VelocityEnv
-from scenarios import SCENARIOS
+from scenarios import SCENARIOS, lying_terrain
 
 pytestmark = pytest.mark.gpu
 
@@ -59,6 +59,37 @@ def test_forced_error_quantiles_well_conditioned(gpu, name):
     fp.check(max_bad_frac=0.01)
     print(name, "quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe", fp.quantiles("cond"))
     fp.check_quantiles(SCEN_GATE[name])
+    env.close()
+
+
+def test_forced_error_quantiles_lying_on_terrain(gpu):
+    """The lying scenario on the Rough task's heightfield (C5 randomisation: per-env friction and added torso mass):
+    the heightfield contact path (ground_local, the torso face on terrain, the height scan) under the same quantile
+    gate as `lying`, forced.SCEN_GATE["lying_terrain"]."""
+    from h12env.cfg import c5_cfg
+
+    n = 1024
+    cfg = c5_cfg(n)
+    cfg.terminations.base_contact_torso = False
+    cfg.terminations.base_contact_knees = False
+    cfg.sim.device = "cuda:0"
+    g = cfg.scene.terrain.terrain_generator
+    g.num_rows, g.num_cols, g.border_width = 6, 8, 5.0  # a smaller grid keeps the oracle's terrain setup quick
+    env = H12VelocityEnv(cfg)
+    t = env.terrain
+    O.set_terrain(t.heights, t.hscale, t.x0, t.y0, t.origins)
+    env.reset()
+    rng = np.random.default_rng(41)
+    Fm = env._fstate.cpu().numpy().copy()
+    lying_terrain(env._model, Fm, rng, t)
+    env._fstate.copy_(torch.from_numpy(Fm))
+    fp = ForcedParity(env, seed=42)
+    for _ in range(20):
+        fp.step((rng.normal(size=(n, 12)) * SCALE["lying"]).astype(np.float32))
+    fp.check(max_bad_frac=0.01)
+    print("lying_terrain quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe",
+          fp.quantiles("cond"))
+    fp.check_quantiles(SCEN_GATE["lying_terrain"])
     env.close()
 
 
