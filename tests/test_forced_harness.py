@@ -37,6 +37,14 @@ class OracleStandIn:
         elif name == "mass":  # one link's mass (left ankle pitch) too large
             model.link_mass[4] *= 1.0 + rel
         self.core = O.OracleEnv(model, ccfg, n)
+        if cfg.scene.terrain.terrain_type == "generator":  # startup state (origins, materials) and the heightfield
+            from h12env.startup import apply_to_arrays, startup_state
+
+            st = startup_state(cfg, n)
+            apply_to_arrays(st, self.core.F, self.core.I)
+            t = st.terrain
+            O.set_terrain(t.heights, t.hscale, t.x0, t.y0, t.origins)
+            self.terrain = t
         self.core.reset()
         self._fstate = torch.from_numpy(self.core.F)
         self._istate = torch.from_numpy(self.core.I)
@@ -130,3 +138,38 @@ def test_scenario_gate_passes_clean_stand_in(name):
 def test_scenario_gate_catches_small_constant_errors(name, bug):
     fp = run_scenario(name, bug)
     assert fp.quantile_violations(SCEN_GATE[name]), fp.report()
+
+
+# The heightfield lying scenario (C5 randomisation) under forced.SCEN_GATE["lying_terrain"]: stand-in noise calibrated
+# to the kernel's floor there (clean p50 of the phys error >= 5.2e-6), planted 1e-4 constant errors caught.
+TERRAIN_NOISE = 4e-8  # clean p50 5.0e-6 against the kernel's 5.2e-6
+
+
+def run_terrain(bug, n=96, steps=16):
+    from h12env.cfg import c5_cfg
+    from scenarios import lying_terrain
+
+    cfg = c5_cfg(n)
+    cfg.terminations.base_contact_torso = False
+    cfg.terminations.base_contact_knees = False
+    g = cfg.scene.terrain.terrain_generator
+    g.num_rows, g.num_cols, g.border_width = 6, 8, 5.0
+    env = OracleStandIn(n, bug, cfg=cfg, noise=TERRAIN_NOISE)
+    lying_terrain(env._model, env.core.F, np.random.default_rng(5), env.terrain)
+    fp = ForcedParity(env, seed=1)
+    rng = np.random.default_rng(2)
+    for _ in range(steps):
+        fp.step((rng.normal(size=(n, 12)) * SCEN_SCALE["lying"]).astype(np.float32))
+    return fp
+
+
+def test_terrain_gate_passes_clean_stand_in():
+    fp = run_terrain(None)
+    fp.check(max_bad_frac=0.02)
+    fp.check_quantiles(SCEN_GATE["lying_terrain"])
+
+
+@pytest.mark.parametrize("bug", ["inertia", "kd", "contact_k"])
+def test_terrain_gate_catches_small_constant_errors(bug):
+    fp = run_terrain(bug)
+    assert fp.quantile_violations(SCEN_GATE["lying_terrain"]), fp.report()
