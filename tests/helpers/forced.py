@@ -94,6 +94,10 @@ COND_EPS = 1e-7
 COND_LIM = 1e-6
 SCEN_GATE = dict(flight=dict(phys=(3e-6, 1.2e-4), rew=(4e-7, 1.5e-5), terms=(2e-6, 5e-5), obs=(3e-6, 1.2e-4)),
                  lying=dict(phys=(8e-6, 6e-4), rew=(8e-7, 4e-5), terms=(6e-6, 2e-4), obs=(8e-6, 6e-4)),
+                 # the Rsl task (per-env materials / mass, 16-term rewards, 6-frame history with smaller scales):
+                 # measured floors p50 phys 6.9e-7 (flight) / 2.8e-6 (lying)
+                 flight_rsl=dict(phys=(2e-6, 6e-5), rew=(2.5e-7, 1e-6), terms=(2e-6, 3e-5), obs=(4e-7, 1e-5)),
+                 lying_rsl=dict(phys=(8e-6, 9e-4), rew=(1.3e-6, 8e-5), terms=(8e-6, 4e-4), obs=(2e-6, 1e-4)),
                  # the heightfield lying scenario (C5 randomisation): measured floor p50 5.2e-6 phys, 5.0e-7 reward
                  lying_terrain=dict(phys=(1.3e-5, 8e-4), rew=(1.3e-6, 8e-5), terms=(1e-5, 3e-4), obs=(1.3e-5, 8e-4)))
 RUN_GATE = dict(phys=(4.5e-5, 4e-4), rew=(2.5e-6, 5e-5), terms=(1.5e-5, 1.5e-4), obs=(4.5e-5, 4e-4))

@@ -29,16 +29,18 @@ pytestmark = pytest.mark.gpu
 SCALE = dict(flight=1.0, lying=0.3)
 
 
-def scenario_cfg():
-    cfg = H12FlatEnvCfg()
+def scenario_cfg(task="flat"):
+    from h12env.cfg import H12RslEnvCfg
+
+    cfg = H12RslEnvCfg() if task == "rsl" else H12FlatEnvCfg()
     # the lying robots' torso contact is an illegal contact: kept in contact here to measure the contact phase
     cfg.terminations.base_contact_torso = False
     cfg.terminations.base_contact_knees = False
     return cfg
 
 
-def run_scenario(name, n=1024, steps=20, seed=31):
-    cfg = scenario_cfg()
+def run_scenario(name, n=1024, steps=20, seed=31, task="flat"):
+    cfg = scenario_cfg(task)
     cfg.scene.num_envs = n
     cfg.sim.device = "cuda:0"
     env = H12VelocityEnv(cfg)
@@ -53,12 +55,16 @@ def run_scenario(name, n=1024, steps=20, seed=31):
     return env, fp
 
 
+@pytest.mark.parametrize("task", ["flat", "rsl"])
 @pytest.mark.parametrize("name", list(SCENARIOS))
-def test_forced_error_quantiles_well_conditioned(gpu, name):
-    env, fp = run_scenario(name)
+def test_forced_error_quantiles_well_conditioned(gpu, name, task):
+    """Flat, and the Rsl task (per-env materials and added mass, the 16-term reward table, deadzone commands,
+    6-frame history) under its own measured gate (forced.SCEN_GATE[name + "_rsl"])."""
+    env, fp = run_scenario(name, task=task)
     fp.check(max_bad_frac=0.01)
-    print(name, "quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe", fp.quantiles("cond"))
-    fp.check_quantiles(SCEN_GATE[name])
+    print(name, task, "quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe",
+          fp.quantiles("cond"))
+    fp.check_quantiles(SCEN_GATE[name if task == "flat" else name + "_rsl"])
     env.close()
 
 
