@@ -85,7 +85,6 @@ __device__ unsigned long long g_wave[1024][11];
       g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
       g_wave[blockIdx.x][3] = _ph_s1; g_wave[blockIdx.x][4] = _ph_s5; g_wave[blockIdx.x][6] = _ph_s6; \
       g_wave[blockIdx.x][5] = _xcc & 15u;                                      \
-      g_wave[blockIdx.x][7] = 0; g_wave[blockIdx.x][8] = 0;                     \
       g_wave[blockIdx.x][9] = 0; g_wave[blockIdx.x][10] = 0;                    \
     }                                                                          \
   } while (0)
@@ -97,7 +96,16 @@ __device__ unsigned long long g_wave[1024][11];
   } while (0)
 #define PHX_INIT() (void)0
 #define PHX(i) (void)0
+// the helper / self-contact waves' end (after their stores completed): columns 7 / 8
+#define PH_HELPER_END()                                                        \
+  do {                                                                         \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
+    const unsigned long long _he = __builtin_amdgcn_s_memrealtime();           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                          \
+      g_wave[blockIdx.x][threadIdx.x < 2 * BLOCK ? 7 : 8] = _he;               \
+  } while (0)
 #else
+#define PH_HELPER_END() (void)0
 #define PH_INIT() unsigned long long _ph_t = __builtin_readcyclecounter(); \
   const unsigned long long _ph_c0 = _ph_t;                                \
   const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime();    \
@@ -136,6 +144,7 @@ __device__ unsigned long long g_wave[1024][11];
   } while (0)
 #endif
 #else
+#define PH_HELPER_END() (void)0
 #define PH_INIT() (void)0
 #define PH_WAVE_END() (void)0
 #define PH(i) (void)0
@@ -2851,6 +2860,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
     }
+    PH_HELPER_END();
     return;
   }
   const int lane_pair = threadIdx.x >> 1;

@@ -84,7 +84,7 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
 
         wt = (C.c_ulonglong * (11 * waves))()
         keys = ("span", "start_spread", "end_spread", "dur_mean", "dur_max", "drain_max")
-        rows, raw, rsets, clk, bw = [], [], [], [], []
+        rows, raw, rsets, clk, bw, ends = [], [], [], [], [], []
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
@@ -92,6 +92,8 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
+            if os.environ.get("H12_PHASE_LIGHT"):  # light build: columns 7 / 8 are the helper / self waves' end
+                ends.append(np.stack([full[:, 2], full[:, 7], full[:, 8]], 1) - full[:, 0:1])
             a = np.concatenate([full[:, :5], full[:, 6:7]], axis=1)
             a -= a[:, 0].min()
             # columns: 0 start, 1 end, 2 end after waitcnt, 3 after physics, 4 after reset, 5 XCC id
@@ -122,6 +124,15 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
                               "barrier R1 wait": round(float(np.median(np.asarray(bw)[m][:, 0])), 2),
                               "barrier R2 wait": round(float(np.median(np.asarray(bw)[m][:, 1])), 2)}
         res["per_xcc_us_median"] = per
+        if ends:
+            E = np.concatenate(ends) / 100.0  # us from the physics wave's start: physics / helper / self wave ends
+            res["wave_role_end_us"] = {"physics_median": round(float(np.median(E[:, 0])), 2),
+                                       "helper_median": round(float(np.median(E[:, 1])), 2),
+                                       "self_median": round(float(np.median(E[:, 2])), 2),
+                                       "block_end_max_role": ["physics", "helper", "self"][
+                                           int(np.bincount(np.argmax(E, 1), minlength=3).argmax())],
+                                       "helper_after_physics_median": round(float(np.median(E[:, 1] - E[:, 0])), 2),
+                                       "self_after_physics_median": round(float(np.median(E[:, 2] - E[:, 0])), 2)}
     env.close()
     return res
 
