@@ -2765,7 +2765,8 @@ H12_DEV void fuse_late(const KParams& P, const StepArgs& A, const FuseCtx& fc, i
       for (int i = 0; i < NRI; ++i) d[(size_t)(2 * i) * row] = v[i];
     }
     // a resetting env's row restarts its history: the frame in every slot
-    uint32_t fm = (uint32_t)__ballot(F.fill[threadIdx.x & (FUSE_ROWS - 1)] != 0);  // wave-uniform
+    constexpr uint32_t ROWS_MASK = FUSE_ROWS >= 32 ? ~0u : (1u << FUSE_ROWS) - 1u;  // a lane per row, no repeats
+    uint32_t fm = (uint32_t)__ballot(F.fill[threadIdx.x & (FUSE_ROWS - 1)] != 0) & ROWS_MASK;  // wave-uniform
     while (fm) {
       const int r = __builtin_ctz(fm);
       fm &= fm - 1u;

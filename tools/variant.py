@@ -38,6 +38,18 @@ PATCHES = {
                          "      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n      {\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < 300; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile(\"\" :: \"v\"(d0), \"v\"(d1));\n      }\n    }\n    __syncthreads();  // R1")],
     # the state write-back dropped (timing only: the state never advances)
     "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
+    # 16 envs per block (256 blocks at 4096 envs: one per CU), the upper half of every 64-lane wave idle; a correct
+    # build (the parity tests run on it with H12ENV_LIB)
+    "epb16": [("constexpr int ENVS_PER_BLOCK = 32;", "constexpr int ENVS_PER_BLOCK = 16;"),
+              ("  const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;",
+               "  const bool active = (l >> 1) < ENVS_PER_BLOCK && step_block() * ENVS_PER_BLOCK + (l >> 1) < n;", 2),
+              ("  const int e = e0 + lane_pair;",
+               "  const int e = lane_pair < ENVS_PER_BLOCK ? e0 + lane_pair : 0x3fffffff;", 3),
+              ("  const int e = blockIdx.x * ENVS_PER_BLOCK + lane_pair;",
+               "  const int e = lane_pair < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + lane_pair : 0x3fffffff;"),
+              ("  const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);",
+               "  const int e = (threadIdx.x >> 1) < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1) "
+               ": 0x3fffffff;", 2)],
 }
 
 
@@ -45,9 +57,10 @@ def build(tag: str, profile: bool) -> Path:
     from h12env.build import ARCH, hipcc
 
     src = (ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_text()
-    for old, new in PATCHES[tag]:
-        if src.count(old) != 1:
-            raise SystemExit(f"patch {tag!r}: {old[:60]!r} matches {src.count(old)} times")
+    for old, new, *cnt in PATCHES[tag]:  # (old, new[, expected number of matches, default 1])
+        want = cnt[0] if cnt else 1
+        if src.count(old) != want:
+            raise SystemExit(f"patch {tag!r}: {old[:60]!r} matches {src.count(old)} times, not {want}")
         src = src.replace(old, new)
     top = ROOT / "tools" / "_variants" / tag
     if top.exists():
