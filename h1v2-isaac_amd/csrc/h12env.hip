@@ -1711,6 +1711,16 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     }
   }
   // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates
+  if constexpr (HW) {
+    // the step's start pose, velocities and joint angles read back from the helper waves' LDS copy (put_state, the
+    // same floats): their registers die after pass 1 instead of being parked in AGPRs through the ABA passes
+    // (-63 VALU per inner step, +0.9 % env-steps/s, profiles/r4/r4zf_state_reload_ab.txt)
+    float x[20];
+    get4(help_lds().st, threadIdx.x, x, 5);
+    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }
+    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
+    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];
+  }
   if (!P.fix_base) {
     float nd[6];
     for (int i = 0; i < 6; ++i) nd[i] = a0[i] + ag[i];

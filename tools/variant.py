@@ -38,6 +38,43 @@ PATCHES = {
                          "      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n      {\n        float d0 = p[0], d1 = p[1];\n        for (int i = 0; i < 300; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile(\"\" :: \"v\"(d0), \"v\"(d1));\n      }\n    }\n    __syncthreads();  // R1")],
     # the state write-back dropped (timing only: the state never advances)
     "no_store": [("    store_env<K>(P, W, e, leg, s);\n    PH(7);", "    PH(7);")],
+    # static probe: the MDP state loaded after the physics loop (register pressure in the loop; Flat only -- the
+    # terrain origin is loaded before the loop as well)
+    "mdp_late": [("    load_mdp<K>(P, W, e, leg, s);\n    PH(0);",
+                  "    for (int i = 0; i < 3; ++i) s.origin[i] = Feat<K>::terrain ? ldf(W, H12_F_ORIGIN + i, e) : 0.f;\n    PH(0);"),
+                 ("    PH(1);\n    // ContactSensor._update_buffers_impl", "    PH(1);\n    load_mdp<K>(P, W, e, leg, s);\n    // ContactSensor._update_buffers_impl")],
+    # the physics wave's integration reads the step's start state (pos, quat, v, w, q) back from the helpers' LDS copy
+    # instead of keeping it in registers through the ABA passes
+    "st_reload": [("  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n",
+                   "  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n"
+                   "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
+                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
+                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
+                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
+    # st_reload, and the joint velocities read back before pass 3 too
+    "st_reload_qd": [("  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n",
+                      "  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n"
+                      "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
+                      "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
+                      "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
+                      "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n"),
+                     ("  // ---- pass 3 (root -> leaf) in the lane frame\n",
+                      "  // ---- pass 3 (root -> leaf) in the lane frame\n"
+                      "  if constexpr (HW) {\n    float x[32];\n    get4(help_lds().st, threadIdx.x, x, 7);\n"
+                      "    for (int k = 0; k < NL; ++k) lg.qd[k] = x[19 + k];\n  }\n")],
+    # st_reload with the LDS reads placed before the base's pair sum / before pass 3 (latency hidden behind the solve)
+    "st_reload_pair": [("  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n",
+                        "  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n"
+                        "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
+                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
+                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
+                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
+    "st_reload_p3": [("  // ---- pass 3 (root -> leaf) in the lane frame\n",
+                      "  // ---- pass 3 (root -> leaf) in the lane frame\n"
+                      "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
+                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
+                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
+                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
     # 16 envs per block (256 blocks at 4096 envs: one per CU), the upper half of every 64-lane wave idle; a correct
     # build (the parity tests run on it with H12ENV_LIB)
     "epb16": [("constexpr int ENVS_PER_BLOCK = 32;", "constexpr int ENVS_PER_BLOCK = 16;"),
@@ -53,7 +90,7 @@ PATCHES = {
 }
 
 
-def build(tag: str, profile: bool) -> Path:
+def build(tag: str, profile: bool, isa: bool = False) -> Path:
     from h12env.build import ARCH, hipcc
 
     src = (ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_text()
@@ -72,8 +109,21 @@ def build(tag: str, profile: bool) -> Path:
     out = ROOT / "tools" / "_variants" / f"lib_{tag}.so"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
            "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros", "-fPIC", "-shared", "-Wno-unused-function",
-           *(["-DH12_PHASE_PROFILE"] if profile else []), "-o", str(out), str(csrc / "h12env.hip")]
-    subprocess.run(cmd, check=True)
+           *(["-DH12_PHASE_PROFILE"] if profile else []), *(["-save-temps"] if isa else []), "-o", str(out),
+           str(csrc / "h12env.hip")]
+    subprocess.run(cmd, check=True, cwd=top)
+    if isa:  # the Flat step kernel's static report (tools/kernel_isa.py), as for the product
+        sys.path.insert(0, str(ROOT / "tools"))
+        import kernel_isa
+
+        text = sorted(top.glob(f"*{ARCH}*.s"))[0].read_text()
+        name = "_ZN12_GLOBAL__N_111step_kernelILi0EEEvNS_7KParamsENS_9WorkspaceENS_8StepArgsE"
+        md = kernel_isa.metadata(text)[name]
+        r = kernel_isa.report(text, name)
+        print("vgpr", md.get("vgpr_count"), "agpr", md.get("agpr_count"), "valu", r["valu"], "accvgpr", r["accvgpr"])
+        for lp in r["loops"]:
+            if lp[1] > 2000:
+                print("  loop", lp)
     shutil.rmtree(top)
     print("built", out)
     return out
@@ -83,5 +133,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("tag", choices=sorted(PATCHES))
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--isa", action="store_true", help="print the Flat step kernel's static ISA report")
     a = ap.parse_args()
-    build(a.tag, a.profile)
+    build(a.tag, a.profile, a.isa)
