@@ -75,6 +75,13 @@ PATCHES = {
                    "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
                    "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
                    "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
+    # the link velocities parked in the joint-terms LDS slot (free after the physics wave has read it at R1) and read
+    # back before the base pair sum for pass 3
+    "v_lds": [("    knee_pz = jt[26];\n  } else {",
+               "    knee_pz = jt[26];\n    put4(help_lds().jt, threadIdx.x, &v[0][0], 9);\n  } else {"),
+              ("  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n",
+               "  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n"
+               "  if constexpr (HW) get4(help_lds().jt, threadIdx.x, &v[0][0], 9);\n")],
     # 16 envs per block (256 blocks at 4096 envs: one per CU), the upper half of every 64-lane wave idle; a correct
     # build (the parity tests run on it with H12ENV_LIB)
     "epb16": [("constexpr int ENVS_PER_BLOCK = 32;", "constexpr int ENVS_PER_BLOCK = 16;"),
