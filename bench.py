@@ -106,8 +106,9 @@ ROLLOUT_TASKS = ("flat", "rsl")
 
 def load_pmc(path):
     """Per-launch PMC figures of step_kernel / obs_assemble_kernel from a tools/profile.sh summary, used
-    only if they were measured on the current kernel source (sha256 of csrc/h12env.hip): HBM bytes
-    (FETCH_SIZE doubled + WRITE_SIZE per MI355X_MICROARCH.md) and the SQ wave / VALU-instruction counts."""
+    only if they were measured on the current kernel: the same source (sha256 of csrc/h12env.hip), or the same
+    device ISA (the summary's isa_sha256 equal to profiles/latest_isa.json's, itself made from the current source):
+    HBM bytes (FETCH_SIZE doubled + WRITE_SIZE per MI355X_MICROARCH.md) and the SQ wave / VALU-instruction counts."""
     import hashlib
     p = Path(path) if path else ROOT / "profiles" / "latest_pmc.json"
     if not p.exists():
@@ -115,8 +116,11 @@ def load_pmc(path):
     d = json.loads(p.read_text())
     src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
     if d.get("source_sha256") != src:
-        return {}, f"{p.name}: stale (kernel source changed)"
-    return d.get("kernels", {}), (f"{p.relative_to(ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH doubled "
+        isa, _ = load_isa()
+        if not (d.get("isa_sha256") and isa.get("isa_sha256") == d["isa_sha256"]):
+            return {}, f"{p.name}: stale (kernel source changed)"
+    where = p.relative_to(ROOT) if p.resolve().is_relative_to(ROOT) else p
+    return d.get("kernels", {}), (f"{where} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, FETCH doubled "
                                   f"per MI355X_MICROARCH.md; SQ_INSTS_VALU / SQ_WAVES)")
 
 

@@ -72,8 +72,9 @@ __device__ unsigned long long g_wave[1024][11];
 #ifdef H12_PHASE_LIGHT
 // light mode (-DH12_PHASE_PROFILE -DH12_PHASE_LIGHT): the realtime stamps only, kept in registers and stored once at
 // the wave's end (no per-phase atomics): the least perturbed view of the product kernel's per-XCD timing
+// (columns 9 / 10: after the rewards, after barrier L)
 #define PH_INIT() const unsigned long long _ph_rt0 = __builtin_amdgcn_s_memrealtime(); \
-  unsigned long long _ph_s1 = 0, _ph_s5 = 0, _ph_s6 = 0
+  unsigned long long _ph_s1 = 0, _ph_s3 = 0, _ph_s4 = 0, _ph_s5 = 0, _ph_s6 = 0
 #define PH_WAVE_END()                                                          \
   do {                                                                         \
     const unsigned long long _r1 = __builtin_amdgcn_s_memrealtime();           \
@@ -85,12 +86,14 @@ __device__ unsigned long long g_wave[1024][11];
       g_wave[blockIdx.x][0] = _ph_rt0; g_wave[blockIdx.x][1] = _r1; g_wave[blockIdx.x][2] = _r2; \
       g_wave[blockIdx.x][3] = _ph_s1; g_wave[blockIdx.x][4] = _ph_s5; g_wave[blockIdx.x][6] = _ph_s6; \
       g_wave[blockIdx.x][5] = _xcc & 15u;                                      \
-      g_wave[blockIdx.x][9] = 0; g_wave[blockIdx.x][10] = 0;                    \
+      g_wave[blockIdx.x][9] = _ph_s3; g_wave[blockIdx.x][10] = _ph_s4;          \
     }                                                                          \
   } while (0)
 #define PH(i)                                                                       \
   do {                                                                              \
     if (i == 1) _ph_s1 = __builtin_amdgcn_s_memrealtime();                         \
+    if (i == 3) _ph_s3 = __builtin_amdgcn_s_memrealtime();                         \
+    if (i == 4) _ph_s4 = __builtin_amdgcn_s_memrealtime();                         \
     if (i == 5) _ph_s5 = __builtin_amdgcn_s_memrealtime();                         \
     if (i == 6) _ph_s6 = __builtin_amdgcn_s_memrealtime();                         \
   } while (0)

@@ -36,3 +36,25 @@ def test_dump_rollout_window_bound(monkeypatch):
     parse(monkeypatch, "--rollout", "on", "--steps", "24", "--rollout-decode", "--dump-rollout", "x.npz")
     with pytest.raises(SystemExit):
         parse(monkeypatch, "--rollout", "on", "--steps", "25", "--rollout-decode", "--dump-rollout", "x.npz")
+
+
+def test_pmc_summary_matched_by_source_or_device_isa(monkeypatch, tmp_path):
+    """bench.load_pmc uses a PMC summary only for the current kernel: the same source hash, or the same device ISA
+    hash as profiles/latest_isa.json (which must itself be made from the current source)."""
+    import hashlib
+    import json
+
+    src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"source_sha256": src, "kernels": {"step_kernel": {"x": 1}}}))
+    assert bench.load_pmc(p)[0] == {"step_kernel": {"x": 1}}
+    monkeypatch.setattr(bench, "load_isa", lambda: ({"isa_sha256": "aa"}, "isa"))
+    p.write_text(json.dumps({"source_sha256": "old", "isa_sha256": "aa", "kernels": {"step_kernel": {}}}))
+    assert bench.load_pmc(p)[0] == {"step_kernel": {}}
+    for isa in ("bb", None):
+        p.write_text(json.dumps({"source_sha256": "old", "isa_sha256": isa, "kernels": {"step_kernel": {}}}))
+        k, why = bench.load_pmc(p)
+        assert k == {} and "stale" in why
+    monkeypatch.setattr(bench, "load_isa", lambda: ({}, "latest_isa.json: stale (kernel source changed)"))
+    p.write_text(json.dumps({"source_sha256": "old", "isa_sha256": "aa", "kernels": {"step_kernel": {}}}))
+    assert bench.load_pmc(p)[0] == {}

@@ -84,7 +84,7 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
 
         wt = (C.c_ulonglong * (11 * waves))()
         keys = ("span", "start_spread", "end_spread", "dur_mean", "dur_max", "drain_max")
-        rows, raw, rsets, clk, bw, ends = [], [], [], [], [], []
+        rows, raw, rsets, clk, bw, ends, light = [], [], [], [], [], [], []
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
@@ -92,8 +92,11 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
-            if os.environ.get("H12_PHASE_LIGHT"):  # light build: columns 7 / 8 are the helper / self waves' end
+            if os.environ.get("H12_PHASE_LIGHT"):  # light build: columns 7 / 8 are the helper / self waves' end,
+                # 9 / 10 the stamps after the rewards and after barrier L
                 ends.append(np.stack([full[:, 2], full[:, 7], full[:, 8]], 1) - full[:, 0:1])
+                light.append(np.stack([full[:, 3] - full[:, 0], full[:, 9] - full[:, 3], full[:, 10] - full[:, 9],
+                                       full[:, 4] - full[:, 10], full[:, 6] - full[:, 4], full[:, 1] - full[:, 6]], 1))
             a = np.concatenate([full[:, :5], full[:, 6:7]], axis=1)
             a -= a[:, 0].min()
             # columns: 0 start, 1 end, 2 end after waitcnt, 3 after physics, 4 after reset, 5 XCC id
@@ -124,6 +127,15 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
                               "barrier R1 wait": round(float(np.median(np.asarray(bw)[m][:, 0])), 2),
                               "barrier R2 wait": round(float(np.median(np.asarray(bw)[m][:, 1])), 2)}
         res["per_xcc_us_median"] = per
+        if light:  # the physics wave's phases, medians over waves with / without a resetting env
+            Lp = np.concatenate(light) / 100.0
+            rw = np.concatenate(rsets) > 0
+            names = ("physics loop", "sensor + rewards", "outputs + log + barrier L", "reset + command + events",
+                     "frame + barrier F", "store issue")
+            res["light_phases_us_median"] = {
+                grp: {k: round(float(np.median(Lp[sel][:, i])), 2) for i, k in enumerate(names)}
+                for grp, sel in (("waves_with_reset", rw), ("waves_without_reset", ~rw)) if sel.any()}
+            res["light_phases_us_median"]["fraction_of_waves_with_reset"] = round(float(rw.mean()), 3)
         if ends:
             E = np.concatenate(ends) / 100.0  # us from the physics wave's start: physics / helper / self wave ends
             res["wave_role_end_us"] = {"physics_median": round(float(np.median(E[:, 0])), 2),

@@ -52,6 +52,13 @@ def main():
            "command": "bash tools/profile.sh (rocprofv3 --pmc <counters> --kernel-trace -f csv -- python3 bench.py "
                       "--steps 100 --warmup 20 --no-cpu-baseline --profile-only)",
            "kernels": {}}
+    # the device ISA the counters belong to (tools/kernel_isa.py --json, when made from this same source): a later
+    # source edit that leaves the ISA unchanged (comments, profile-only macros) keeps the counters valid
+    isa = ROOT / "profiles" / "latest_isa.json"
+    if isa.exists():
+        d = json.loads(isa.read_text())
+        if d.get("source_sha256") == res["source_sha256"]:
+            res["isa_sha256"] = d.get("isa_sha256")
     fetch, meta = counters(src / "fetch")
     write, _ = counters(src / "write")
     sq, _ = counters(src / "sq")
