@@ -137,15 +137,66 @@ H12_DEV void sym_rotate(float* S, float c, float s) {
   S[sidx(i, k)] = c * sik - s * sjk;
   S[sidx(j, k)] = s * sik + c * sjk;
 }
+// two floats in one 64-bit register pair: v_pk_{fma,mul,add}_f32 do both lanes of the pair in one VALU op
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// a pair from two scalars.  The empty asm hands lane 0 over as a value: otherwise the optimiser turns "element k
+// of S into lane 0" into a 2-wide load at &S[k] (then replaces lane 1), and that overlapping access keeps the
+// whole array on the stack (scratch)
+H12_DEV f32x2 pk2(float a, float b) {
+  asm("" : "+v"(a));
+  f32x2 v;
+  v.x = a;
+  v.y = b;
+  return v;
+}
+// sym_rotate of the A and C blocks together (the same rotation, elementwise the same operations): one packed op
+// per pair of scalar ones
+template <int A>
+H12_DEV void sym_rotate_ac(float* SA, float* SC, float c, float s) {
+  constexpr int i = (A + 1) % 3, j = (A + 2) % 3, k = A;
+  const float cc = c * c, ss = s * s, cs = c * s;
+  const f32x2 sii = pk2(SA[sidx(i, i)], SC[sidx(i, i)]), sjj = pk2(SA[sidx(j, j)], SC[sidx(j, j)]);
+  const f32x2 sij = pk2(SA[sidx(i, j)], SC[sidx(i, j)]);
+  const f32x2 sik = pk2(SA[sidx(i, k)], SC[sidx(i, k)]), sjk = pk2(SA[sidx(j, k)], SC[sidx(j, k)]);
+  const f32x2 nii = cc * sii - 2.f * cs * sij + ss * sjj;
+  const f32x2 njj = ss * sii + 2.f * cs * sij + cc * sjj;
+  const f32x2 nij = cs * (sii - sjj) + (cc - ss) * sij;
+  const f32x2 nik = c * sik - s * sjk;
+  const f32x2 njk = s * sik + c * sjk;
+  SA[sidx(i, i)] = nii.x; SC[sidx(i, i)] = nii.y;
+  SA[sidx(j, j)] = njj.x; SC[sidx(j, j)] = njj.y;
+  SA[sidx(i, j)] = nij.x; SC[sidx(i, j)] = nij.y;
+  SA[sidx(i, k)] = nik.x; SC[sidx(i, k)] = nik.y;
+  SA[sidx(j, k)] = njk.x; SC[sidx(j, k)] = njk.y;
+}
 // rotate every block into parent axes: X_rot^T I X_rot with E^T = R_A(q)
 template <int A>
 H12_DEV void ai_rotate(AInertia& I, float c, float s) {
   float T[3][3];
-  sym_rotate<A>(I.A, c, s);
-  sym_rotate<A>(I.C, c, s);
-  // B block: R B R^T
-  for (int j = 0; j < 3; ++j) { float col[3] = {I.B[0][j], I.B[1][j], I.B[2][j]}, o[3]; rot<A>(c, s, col, o); T[0][j] = o[0]; T[1][j] = o[1]; T[2][j] = o[2]; }
-  for (int i = 0; i < 3; ++i) { float row[3] = {T[i][0], T[i][1], T[i][2]}, o[3]; rot<A>(c, s, row, o); I.B[i][0] = o[0]; I.B[i][1] = o[1]; I.B[i][2] = o[2]; }
+  sym_rotate_ac<A>(I.A, I.C, c, s);
+  // B block: R B R^T (columns 0 / 1, then rows 0 / 1, as packed pairs)
+  {
+    const f32x2 x = pk2(I.B[0][0], I.B[0][1]), y = pk2(I.B[1][0], I.B[1][1]), z = pk2(I.B[2][0], I.B[2][1]);
+    f32x2 o0, o1, o2;
+    if constexpr (A == 0) { o0 = x; o1 = c * y - s * z; o2 = s * y + c * z; }
+    else if constexpr (A == 1) { o0 = c * x + s * z; o1 = y; o2 = -s * x + c * z; }
+    else { o0 = c * x - s * y; o1 = s * x + c * y; o2 = z; }
+    T[0][0] = o0.x; T[0][1] = o0.y; T[1][0] = o1.x; T[1][1] = o1.y; T[2][0] = o2.x; T[2][1] = o2.y;
+    float col[3] = {I.B[0][2], I.B[1][2], I.B[2][2]}, o[3];
+    rot<A>(c, s, col, o);
+    T[0][2] = o[0]; T[1][2] = o[1]; T[2][2] = o[2];
+  }
+  {
+    const f32x2 x = pk2(T[0][0], T[1][0]), y = pk2(T[0][1], T[1][1]), z = pk2(T[0][2], T[1][2]);
+    f32x2 o0, o1, o2;
+    if constexpr (A == 0) { o0 = x; o1 = c * y - s * z; o2 = s * y + c * z; }
+    else if constexpr (A == 1) { o0 = c * x + s * z; o1 = y; o2 = -s * x + c * z; }
+    else { o0 = c * x - s * y; o1 = s * x + c * y; o2 = z; }
+    I.B[0][0] = o0.x; I.B[1][0] = o0.y; I.B[0][1] = o1.x; I.B[1][1] = o1.y; I.B[0][2] = o2.x; I.B[1][2] = o2.y;
+    float row[3] = {T[2][0], T[2][1], T[2][2]}, o[3];
+    rot<A>(c, s, row, o);
+    I.B[2][0] = o[0]; I.B[2][1] = o[1]; I.B[2][2] = o[2];
+  }
 }
 // shift the reference point from the child origin to the parent origin (child origin at r in
 // parent coords, parent axes): A += S + S^T - T rx, B += T, with T = rx C, S = rx B^T.
