@@ -82,6 +82,11 @@ PATCHES = {
               ("  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n",
                "  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n"
                "  if constexpr (HW) get4(help_lds().jt, threadIdx.x, &v[0][0], 9);\n")],
+    # probes: 300 VALU of dependent dummy work in the R1 -> R2 window of the self-contact / helper wave
+    "self_r2slack300": [("      put4(H.selfw, l, w, 3);\n    }",
+                         "      put4(H.selfw, l, w, 3);\n      {\n        float d0 = w[0], d1 = w[1];\n        for (int i = 0; i < 150; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile(\"\" :: \"v\"(d0), \"v\"(d1));\n      }\n    }")],
+    "helper_r2slack300": [("      put4(H.bias, l, o, 11);\n",
+                           "      put4(H.bias, l, o, 11);\n" + "      {\n        float d0 = w[0], d1 = w[1];\n        for (int i = 0; i < 150; ++i) { d0 = __builtin_fmaf(d0, 0.999f, d1); d1 = __builtin_fmaf(d1, 1.001f, d0); }\n        asm volatile(\"\" :: \"v\"(d0), \"v\"(d1));\n      }\n".replace("w[0]", "o[0]").replace("w[1]", "o[1]"))],
     # 16 envs per block (256 blocks at 4096 envs: one per CU), the upper half of every 64-lane wave idle; a correct
     # build (the parity tests run on it with H12ENV_LIB)
     "epb16": [("constexpr int ENVS_PER_BLOCK = 32;", "constexpr int ENVS_PER_BLOCK = 16;"),
