@@ -61,6 +61,9 @@ def parse():
                         "of the train.py runner, rollout all-gathered over RCCL when N > 1)")
     p.add_argument("--iterations", type=int, default=5, help="train mode: timed PPO iterations")
     p.add_argument("--precision", choices=("fp32", "bf16"), default="fp32", help="train mode: learning-phase GEMM precision")
+    p.add_argument("--tunableop", action="store_true",
+                   help="train mode: PyTorch TunableOp GEMM selection for the learner (opt-in: the timed selection can "
+                        "differ between runs and ranks, so runs are not bit-reproducible; h12env.ppo.enable_tunable_gemm)")
     p.add_argument("--task", choices=("flat", "rough", "c5", "rsl", "cat"), default="flat",
                    help="flat: the metric's task; rough: Isaac-Velocity-Rough-H12_12dof-v0; c5: BASELINE config C5 "
                         "(rough + per-env friction / torso mass, 8192 envs unless --envs); rsl: "
@@ -104,18 +107,22 @@ def parse():
 ROLLOUT_TASKS = ("flat", "rsl")
 
 
+def kernel_source_sha256() -> str:
+    """The key of the ISA / PMC summaries: every kernel source file, headers included (h12env.build.source_sha256)."""
+    from h12env.build import source_sha256
+    return source_sha256()
+
+
 def load_pmc(path):
     """Per-launch PMC figures of step_kernel / obs_assemble_kernel from a tools/profile.sh summary, used
-    only if they were measured on the current kernel: the same source (sha256 of csrc/h12env.hip), or the same
+    only if they were measured on the current kernel: the same sources (kernel_source_sha256: csrc/*.hip, csrc/*.h, include/*.h), or the same
     device ISA (the summary's isa_sha256 equal to profiles/latest_isa.json's, itself made from the current source):
     HBM bytes (FETCH_SIZE doubled + WRITE_SIZE per MI355X_MICROARCH.md) and the SQ wave / VALU-instruction counts."""
-    import hashlib
     p = Path(path) if path else ROOT / "profiles" / "latest_pmc.json"
     if not p.exists():
         return {}, None
     d = json.loads(p.read_text())
-    src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
-    if d.get("source_sha256") != src:
+    if d.get("source_sha256") != kernel_source_sha256():
         isa, _ = load_isa()
         if not (d.get("isa_sha256") and isa.get("isa_sha256") == d["isa_sha256"]):
             return {}, f"{p.name}: stale (kernel source changed)"
@@ -127,12 +134,11 @@ def load_pmc(path):
 def load_isa():
     """tools/kernel_isa.py --json summary (physics-wave loop VALU count, registers) if it was made from the current
     kernel source."""
-    import hashlib
     p = ROOT / "profiles" / "latest_isa.json"
     if not p.exists():
         return {}, None
     d = json.loads(p.read_text())
-    if d.get("source_sha256") != hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest():
+    if d.get("source_sha256") != kernel_source_sha256():
         return {}, f"{p.name}: stale (kernel source changed)"
     return d, f"{p.relative_to(ROOT)} (static ISA, tools/kernel_isa.py --json)"
 
@@ -231,6 +237,8 @@ def train_mode(args, world, rank, dev, torch, dist):
     agent = H12_12dof_FlatPPORunnerCfg(device=str(dev))
     tcfg = agent.to_dict()
     tcfg["algorithm"]["precision"] = args.precision
+    if args.tunableop:
+        os.environ["H12_TUNABLEOP"] = "1"
     runner = OnPolicyRunner(env, tcfg, log_dir=None, device=str(dev))
     import io
     import contextlib
@@ -271,7 +279,7 @@ def train_mode(args, world, rank, dev, torch, dist):
                        "parallelism": f"env-shard x{world}" + (" + RCCL rollout all-gather + grad all-reduce"
                                                                if world > 1 else "")},
             "collection_env_steps_per_s": steps / coll, "collection_s_per_iter": coll / args.iterations,
-            "learning_s_per_iter": learn / args.iterations}), flush=True)
+            "learning_s_per_iter": learn / args.iterations, "tunableop": bool(args.tunableop)}), flush=True)
     env.close()
 
 

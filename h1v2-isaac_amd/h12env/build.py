@@ -29,6 +29,20 @@ def sources():
     return [CSRC / "h12env.hip", CSRC / "h12_math.h", CSRC / "h12_model_gen.h", REPO / "include" / "h12env.h"]
 
 
+def source_sha256() -> str:
+    """sha256 over every file the kernels are compiled from (csrc/*.hip, csrc/*.h, include/*.h; path + contents, in
+    sorted order): the key profiles/latest_isa.json and the PMC summaries are checked against, so a header-only change
+    (e.g. h12_math.h) also marks them stale."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.h")) + list((REPO / "include").glob("*.h")))
+    for f in files:
+        h.update(f.relative_to(REPO).as_posix().encode() + b"\0")
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
     if not OUT.exists():
         return True

@@ -180,7 +180,6 @@ class EmpiricalNormalization(nn.Module):
         self.register_buffer("_var", torch.ones(shape).unsqueeze(0))
         self.register_buffer("_std", torch.ones(shape).unsqueeze(0))
         self.register_buffer("count", torch.tensor(0, dtype=torch.long))
-        self._global_n: dict[int, int] = {}  # local batch size -> union size over the ranks (one sync per size)
 
     def forward(self, x):
         if self.training:
@@ -194,9 +193,8 @@ class EmpiricalNormalization(nn.Module):
         Chan's parallel formula (global mean from sum n_r mean_r, then M2 = sum n_r (var_r + (mean_r - mean)^2)):
         no E[x^2] - mean^2 cancellation, so the merged variance is never negative.  Every call issues exactly two
         all-reduces on every rank: the union size rides in the first one (with the shards' weighted means), so
-        ranks never disagree on which collectives run, whatever their local batch sizes.  The merge itself uses the
-        device-side union size; the host-side count reads it once per local batch size (cached, so no host sync per
-        update)."""
+        ranks never disagree on which collectives run, whatever their local batch sizes.  The merge and the sample count
+        use the device-side union size (no host sync per update)."""
         if self.until is not None and self.count >= self.until:
             return
         n = x.shape[0]
@@ -211,12 +209,14 @@ class EmpiricalNormalization(nn.Module):
             m2 = (var_x + (mean_x - g_mean) ** 2) * n
             D.all_reduce(m2)
             m2 = m2 / n_dev
-            if n not in self._global_n:
-                self._global_n[n] = int(round(float(n_dev.item())))
-            n_tot = self._global_n[n]
-            n, mean_x, var_x = n_tot, g_mean, m2
-        self.count += n
-        rate = n / self.count
+            # the union size stays on the device (no host sync, and no cache that a rank whose own batch size is
+            # unchanged could keep while another rank's changes)
+            self.count += n_dev.reshape(()).round().long()
+            rate = n_dev / self.count
+            mean_x, var_x = g_mean, m2
+        else:
+            self.count += n
+            rate = n / self.count
         delta = mean_x - self._mean
         self._mean += rate * delta
         self._var += rate * (var_x - self._var + delta * (mean_x - self._mean))
@@ -294,13 +294,24 @@ def enable_tunable_gemm():
     """PyTorch's TunableOp for the learner's GEMMs: the first call of each GEMM shape times the available
     hipBLASLt / rocBLAS solutions and keeps the fastest for the process (the minibatch shapes are fixed, so a few
     seconds once per run).  Round 4, C3 at 4096 envs, 2 runs each: learning 38.6 / 38.5 ms per iteration against 41.3
-    / 40.8 ms with the default heuristics (profiles/r4/r4t_blas_tunableop_ab.txt).  Process-wide; H12_TUNABLEOP=0
-    turns it off.  The tuning table goes to the temp directory, not the working directory."""
+    / 40.8 ms with the default heuristics (profiles/r4/r4t_blas_tunableop_ab.txt).
+
+    OPT-IN (H12_TUNABLEOP=1, or bench.py --mode train --tunableop): the selection is the fastest solution of a timing
+    run, so it can differ between runs and between ranks -- two runs with the same seed are then not bit-reproducible
+    (each rank's GEMMs may round differently), and the switch is process-wide (every GEMM in the process is tuned).
+    With PYTORCH_TUNABLEOP_FILENAME set to an existing tuning table the recorded selections are reused with tuning
+    off (reproducible); otherwise the table is written to the temp directory."""
     import tempfile
 
     t = torch.cuda.tunable
     if not t.is_enabled():
-        if not os.environ.get("PYTORCH_TUNABLEOP_FILENAME"):
+        fixed = os.environ.get("PYTORCH_TUNABLEOP_FILENAME")
+        if fixed and os.path.exists(fixed):
+            t.enable(True)
+            t.tuning_enable(False)  # a checked tuning table: its selections, no timing runs
+            t.read_file(fixed)
+            return
+        if not fixed:
             t.set_filename(os.path.join(tempfile.gettempdir(), f"h12env_tunableop_{os.getpid()}_%d.csv"))
         t.enable(True)
         t.tuning_enable(True)
@@ -318,7 +329,7 @@ class PPO:
         self.policy = policy.to(device)
         self.actor_critic = self.policy  # rsl_rl < 2.3 name
         self.device = device
-        if str(device).startswith("cuda") and os.environ.get("H12_TUNABLEOP", "1") != "0":
+        if str(device).startswith("cuda") and os.environ.get("H12_TUNABLEOP", "0") == "1":
             enable_tunable_gemm()
         # fused Adam (one kernel for all parameters) on the GPU with the learning rate as a device tensor, so
         # the KL-adaptive schedule runs on the device (no host sync per minibatch); plain Adam on CPU

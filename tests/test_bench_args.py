@@ -41,10 +41,9 @@ def test_dump_rollout_window_bound(monkeypatch):
 def test_pmc_summary_matched_by_source_or_device_isa(monkeypatch, tmp_path):
     """bench.load_pmc uses a PMC summary only for the current kernel: the same source hash, or the same device ISA
     hash as profiles/latest_isa.json (which must itself be made from the current source)."""
-    import hashlib
     import json
 
-    src = hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest()
+    src = bench.kernel_source_sha256()
     p = tmp_path / "pmc.json"
     p.write_text(json.dumps({"source_sha256": src, "kernels": {"step_kernel": {"x": 1}}}))
     assert bench.load_pmc(p)[0] == {"step_kernel": {"x": 1}}
@@ -58,3 +57,22 @@ def test_pmc_summary_matched_by_source_or_device_isa(monkeypatch, tmp_path):
     monkeypatch.setattr(bench, "load_isa", lambda: ({}, "latest_isa.json: stale (kernel source changed)"))
     p.write_text(json.dumps({"source_sha256": "old", "isa_sha256": "aa", "kernels": {"step_kernel": {}}}))
     assert bench.load_pmc(p)[0] == {}
+
+
+def test_kernel_source_hash_covers_the_headers(monkeypatch, tmp_path):
+    """The summaries' key changes with a header-only edit (csrc/*.h, include/*.h), not only with csrc/h12env.hip."""
+    import shutil
+
+    from h12env import build as B
+
+    base = bench.kernel_source_sha256()
+    shutil.copytree(ROOT / "h1v2-isaac_amd" / "csrc", tmp_path / "h1v2-isaac_amd" / "csrc")
+    shutil.copytree(ROOT / "include", tmp_path / "include")
+    monkeypatch.setattr(B, "CSRC", tmp_path / "h1v2-isaac_amd" / "csrc")
+    monkeypatch.setattr(B, "REPO", tmp_path)
+    assert B.source_sha256() == base
+    for f in (tmp_path / "h1v2-isaac_amd" / "csrc" / "h12_math.h", tmp_path / "include" / "h12env.h"):
+        old = f.read_bytes()
+        f.write_bytes(old + b"\n// edit\n")
+        assert B.source_sha256() != base, f.name
+        f.write_bytes(old)

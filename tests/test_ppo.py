@@ -142,3 +142,55 @@ def test_two_rank_noise_differs_and_normaliser_is_shared():
     assert res[0][1] != res[1][1]          # exploration noise differs between ranks
     assert res[0][2] == res[1][2]          # normaliser statistics identical
 
+
+
+def _norm_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from h12env.ppo import EmpiricalNormalization
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(7)
+    # per update: each rank's local batch size; rank 0 keeps 5 while rank 1 changes (the case a count cached per
+    # local batch size got wrong)
+    sizes = [(5, 3), (5, 9), (5, 1), (2, 9)]
+    norm = EmpiricalNormalization(4)
+    for s in sizes:
+        xs = [torch.randn(n, 4, generator=g, dtype=torch.float64).float() for n in s]
+        norm.update(xs[rank])
+    q.put((rank, (norm._mean.numpy().tobytes(), norm._var.numpy().tobytes(), int(norm.count))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_normaliser_union_with_changing_batch_sizes():
+    """The normaliser's sample count and update rate follow the union size of every update, also when one rank's local
+    batch size stays the same while another's changes: both ranks end identical and equal to one
+    process updating with the concatenated batches."""
+    import multiprocessing as mp
+    import random
+
+    import numpy as np
+
+    from h12env.ppo import EmpiricalNormalization
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    ps = [ctx.Process(target=_norm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    g = torch.Generator().manual_seed(7)
+    ref = EmpiricalNormalization(4)
+    for s in [(5, 3), (5, 9), (5, 1), (2, 9)]:
+        xs = [torch.randn(n, 4, generator=g, dtype=torch.float64).float() for n in s]
+        ref.update(torch.cat(xs))
+    assert res[0][2] == int(ref.count) == 39
+    np.testing.assert_allclose(np.frombuffer(res[0][0], np.float32), ref._mean.numpy().ravel(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np.frombuffer(res[0][1], np.float32), ref._var.numpy().ravel(), rtol=1e-4, atol=1e-6)

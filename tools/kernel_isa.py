@@ -101,13 +101,14 @@ def physics_wave_json(text: str, meta: dict, out: Path) -> None:
     The physics wave is the one whose registers overflow into AGPRs, so its loop is the one with the most
     v_accvgpr moves (largest VALU count among ties); the helper / self-contact loops use none and, with the fused
     observation stores, the helper loop has more VALU than the physics loop."""
-    import hashlib
     import json
+
+    from h12env.build import source_sha256
 
     name = next(k for k in meta if "step_kernelILi0E" in k)
     g, r = meta[name], report(text, name)
     top = max(r["loops"], key=lambda x: (x[3], x[2]))
-    res = {"source_sha256": hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest(),
+    res = {"source_sha256": source_sha256(),
            "kernel": name,
            "registers": {"vgpr_count_total": g.get("vgpr_count"), "agpr_count": g.get("agpr_count"),
                          "arch_vgpr": (g.get("vgpr_count") or 0) - (g.get("agpr_count") or 0),

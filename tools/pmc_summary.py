@@ -8,7 +8,6 @@ from __future__ import annotations
 
 import csv
 import glob
-import hashlib
 import json
 import shutil
 import sys
@@ -16,6 +15,8 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
+from h12env.build import source_sha256  # noqa: E402
 KERNELS = ("step_kernel", "obs_assemble_kernel")
 
 
@@ -48,7 +49,7 @@ def mean(v):
 
 def main():
     src, tag = Path(sys.argv[1]), sys.argv[2]
-    res = {"tag": tag, "source_sha256": hashlib.sha256((ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_bytes()).hexdigest(),
+    res = {"tag": tag, "source_sha256": source_sha256(),
            "command": "bash tools/profile.sh (rocprofv3 --pmc <counters> --kernel-trace -f csv -- python3 bench.py "
                       "--steps 100 --warmup 20 --no-cpu-baseline --profile-only)",
            "kernels": {}}

@@ -17,6 +17,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "h1v2-isaac_amd"))
 
+# The recorded round-4 experiments were written against the round-4 kernel (commit R4_BASE): they are applied to that
+# commit's sources (git show), so they stay reproducible while the product kernel moves on.  Experiments against the
+# current sources go into PATCHES_HEAD.
+R4_BASE = "787ede1"
+
 PATCHES = {
     # the helper waves' shifted-row stores during the physics loop dropped (timing only: the rows are wrong)
     "no_early": [("  for (int k = k0; k < k1; ++k) {\n    const int j = t + k * nt;",
@@ -43,38 +48,6 @@ PATCHES = {
     "mdp_late": [("    load_mdp<K>(P, W, e, leg, s);\n    PH(0);",
                   "    for (int i = 0; i < 3; ++i) s.origin[i] = Feat<K>::terrain ? ldf(W, H12_F_ORIGIN + i, e) : 0.f;\n    PH(0);"),
                  ("    PH(1);\n    // ContactSensor._update_buffers_impl", "    PH(1);\n    load_mdp<K>(P, W, e, leg, s);\n    // ContactSensor._update_buffers_impl")],
-    # the physics wave's integration reads the step's start state (pos, quat, v, w, q) back from the helpers' LDS copy
-    # instead of keeping it in registers through the ABA passes
-    "st_reload": [("  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n",
-                   "  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n"
-                   "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
-                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
-                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
-                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
-    # st_reload, and the joint velocities read back before pass 3 too
-    "st_reload_qd": [("  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n",
-                      "  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates\n"
-                      "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
-                      "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
-                      "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
-                      "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n"),
-                     ("  // ---- pass 3 (root -> leaf) in the lane frame\n",
-                      "  // ---- pass 3 (root -> leaf) in the lane frame\n"
-                      "  if constexpr (HW) {\n    float x[32];\n    get4(help_lds().st, threadIdx.x, x, 7);\n"
-                      "    for (int k = 0; k < NL; ++k) lg.qd[k] = x[19 + k];\n  }\n")],
-    # st_reload with the LDS reads placed before the base's pair sum / before pass 3 (latency hidden behind the solve)
-    "st_reload_pair": [("  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n",
-                        "  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities\n"
-                        "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
-                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
-                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
-                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
-    "st_reload_p3": [("  // ---- pass 3 (root -> leaf) in the lane frame\n",
-                      "  // ---- pass 3 (root -> leaf) in the lane frame\n"
-                      "  if constexpr (HW) {\n    float x[20];\n    get4(help_lds().st, threadIdx.x, x, 5);\n"
-                   "    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }\n"
-                   "    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];\n"
-                   "    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];\n  }\n")],
     # the link velocities parked in the joint-terms LDS slot (free after the physics wave has read it at R1) and read
     # back before the base pair sum for pass 3
     "v_lds": [("    knee_pz = jt[26];\n  } else {",
@@ -100,23 +73,45 @@ PATCHES = {
                "  const int e = (threadIdx.x >> 1) < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1) "
                ": 0x3fffffff;", 2)],
 }
+PATCHES_HEAD: dict = {}
+ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
+SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
+           "include/h12env.h")
+
+
+def source_at(rev: str | None, rel: str) -> str:
+    """A kernel source file of the working tree (rev None) or of git revision rev."""
+    if rev is None:
+        return (ROOT / rel).read_text()
+    return subprocess.run(["git", "show", f"{rev}:{rel}"], cwd=ROOT, check=True, capture_output=True, text=True).stdout
+
+
+def patched(tag: str) -> tuple[str, str]:
+    """(original, patched) h12env.hip of variant tag"""
+    rev, patches = ALL[tag]
+    src = orig = source_at(rev, SOURCES[0])
+    for old, new, *cnt in patches:  # (old, new[, expected number of matches, default 1])
+        want = cnt[0] if cnt else 1
+        if src.count(old) != want:
+            raise SystemExit(f"patch {tag!r}: {old[:60]!r} matches {src.count(old)} times, not {want}")
+        src = src.replace(old, new)
+    return orig, src
 
 
 def build(tag: str, profile: bool, isa: bool = False) -> Path:
     from h12env.build import ARCH, hipcc
 
-    src = (ROOT / "h1v2-isaac_amd" / "csrc" / "h12env.hip").read_text()
-    for old, new, *cnt in PATCHES[tag]:  # (old, new[, expected number of matches, default 1])
-        want = cnt[0] if cnt else 1
-        if src.count(old) != want:
-            raise SystemExit(f"patch {tag!r}: {old[:60]!r} matches {src.count(old)} times, not {want}")
-        src = src.replace(old, new)
+    rev = ALL[tag][0]
+    _, src = patched(tag)
     top = ROOT / "tools" / "_variants" / tag
     if top.exists():
         shutil.rmtree(top)
     csrc = top / "a" / "csrc"
-    shutil.copytree(ROOT / "h1v2-isaac_amd" / "csrc", csrc)
-    shutil.copytree(ROOT / "include", top / "include")
+    csrc.mkdir(parents=True)
+    (top / "include").mkdir()
+    for rel in SOURCES[1:]:
+        dst = top / "include" / Path(rel).name if rel.startswith("include/") else csrc / Path(rel).name
+        dst.write_text(source_at(rev, rel))
     (csrc / "h12env.hip").write_text(src)
     out = ROOT / "tools" / "_variants" / f"lib_{tag}.so"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
@@ -143,7 +138,7 @@ def build(tag: str, profile: bool, isa: bool = False) -> Path:
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("tag", choices=sorted(PATCHES))
+    ap.add_argument("tag", choices=sorted(ALL))
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--isa", action="store_true", help="print the Flat step kernel's static ISA report")
     a = ap.parse_args()
