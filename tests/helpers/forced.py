@@ -101,6 +101,21 @@ SCEN_GATE = dict(flight=dict(phys=(3e-6, 1.2e-4), rew=(4e-7, 1.5e-5), terms=(2e-
                  # the heightfield lying scenario (C5 randomisation): measured floor p50 5.2e-6 phys, 5.0e-7 reward
                  lying_terrain=dict(phys=(1.3e-5, 8e-4), rew=(1.3e-6, 8e-5), terms=(1e-5, 3e-4), obs=(1.3e-5, 8e-4)))
 RUN_GATE = dict(phys=(4.5e-5, 4e-4), rew=(2.5e-6, 5e-5), terms=(1.5e-5, 1.5e-4), obs=(4.5e-5, 4e-4))
+# The sole-contact scenarios (round 5): their absolute-error quantiles sit at the fp32 floor of a sole depth computed
+# from ~1 m positions (p50 ~5.5e-5, the oracle's own conditioning probe ~4e-5) -- gated at 2x the kernel's measured
+# floor -- and the resolving gate is the per-field SIGNED mean error (ForcedParity.bias_violations) against 3x the
+# kernel's own measured fp32 bias + 6 standard errors per field (BIAS_GATE; tools/gen_sole_bias_gate.py from
+# profiles/r5/bias_*.json, the GPU run of test_forced_sole_contact_scenarios under H12_GATE_MEASURE).
+def _sole_gates():
+    import json
+
+    d = json.loads(open(os.path.join(os.path.dirname(__file__), "..", "golden", "sole_bias_gate.json")).read())
+    for k, q in d["quant"].items():
+        SCEN_GATE[k] = {c: tuple(v) for c, v in q.items()}
+    return d["bias"]
+
+
+BIAS_GATE = _sole_gates()
 TERMS = ("EPSUM", "EPSUM2", "METRIC")  # episode sums of the 20 kernel reward terms (12 Flat + 8 Rsl), command metrics
 CRITERIA = ("phys", "flags", "ints", "rew", "terms", "obs")
 
@@ -221,6 +236,10 @@ class ForcedParity:
         # by at most COND_LIM.  There an fp32 kernel must sit near the probe's own error; a constant error does not.
         self.errs_wc = {c: [] for c in QCRIT}
         self.cond = {c: [] for c in QCRIT}
+        # signed relative error of every physics-state field (PHYS rows, |g - o| / max(1, |o|) with its sign) over the
+        # passing env-steps: a constant parameter error shifts their MEAN consistently, fp32 rounding does not --
+        # bias() resolves shifts far below the p50 of the absolute error (the sole-contact scenarios, round 5)
+        self.signed = []
         self.steps = 0
         self.env_steps = 0
 
@@ -254,6 +273,8 @@ class ForcedParity:
             self.bad_counts[c] += int((~ok[c]).sum())
             allok &= ok[c]
         live = ~(g[4] | g[5] | o[4] | o[5])  # the term contributions of resetting envs are not compared
+        pg, po = _rows(g[0], PHYS).astype(np.float64), _rows(o[0], PHYS).astype(np.float64)
+        self.signed.append(((pg - po) / np.maximum(1.0, np.abs(po)))[:, ok["phys"] & live].astype(np.float32))
         p = self._oracle_step(perturbed(self.rng, F0, COND_EPS), I0, obs0, a_np, t)  # the conditioning probe
         _, dcond = compare(F0, *p[:6], *o[:6])
         O.set_dz_count(dz1)
@@ -380,6 +401,34 @@ class ForcedParity:
             q[c]["max"] = float(f"{x.max():.3g}")
             q[c]["n"] = int(x.size)
         return q
+
+    def bias_fields(self):
+        """(names, mean, standard error) of the signed relative error per physics-state field over the passing
+        env-steps"""
+        names = [f"{k}{i}" for k in PHYS for i in range(FIELDS[k][1])]
+        x = np.concatenate(self.signed, axis=1).astype(np.float64) if self.signed else np.zeros((len(names), 1))
+        n = x.shape[1]
+        return names, x.mean(axis=1), x.std(axis=1) / np.sqrt(max(n - 1, 1))
+
+    def bias_violations(self, limits: dict) -> list:
+        """Fields whose |mean signed error| exceeds limits[field] (a field missing from limits: limits["*"])."""
+        names, m, _ = self.bias_fields()
+        lim = [limits[f] if f in limits else limits.get("*", np.inf) for f in names]
+        return [(f, float(f"{v:.3g}"), x) for f, v, x in zip(names, m, lim) if abs(v) > x]
+
+    def bias(self) -> dict:
+        """Per physics-state field: the mean signed relative error over the passing env-steps and its z-score (mean /
+        standard error); {"z_max": .., "field": .., "mean": .., "n": ..} of the field with the largest |z|.  fp32
+        rounding averages out over the env-steps; a constant parameter error does not."""
+        names = [f"{k}{i}" for k in PHYS for i in range(FIELDS[k][1])]
+        x = np.concatenate(self.signed, axis=1).astype(np.float64) if self.signed else np.zeros((len(names), 1))
+        n = x.shape[1]
+        m = x.mean(axis=1)
+        se = x.std(axis=1) / np.sqrt(max(n - 1, 1)) + 1e-30
+        z = m / se
+        k = int(np.argmax(np.abs(z)))
+        return {"z_max": float(f"{z[k]:.3g}"), "field": names[k], "mean": float(f"{m[k]:.3g}"), "n": int(n),
+                "z": {names[i]: float(f"{z[i]:.3g}") for i in np.argsort(-np.abs(z))[:6]}}
 
     def report(self) -> str:
         frac = {c: self.bad_counts[c] / max(1, self.env_steps) for c in CRITERIA}

@@ -13,14 +13,28 @@ well-conditioned, so that the error quantiles of the teacher-forced comparison s
   lying    robots resting on the torso box (h12_12dof.urdf:387), as test_torso_face_contacts_forced: the
            face's corner contacts carry the body with both contact spring and damper active, joints moving
            under small actions
+  stance   (round 5) both feet flat on the floor at the default pose, the 8 sole spheres in persistent, STICKING
+           contact (anchors at the spheres, contact flags set), PD holding the default targets under small actions:
+           the sole-contact path the benchmark spends its time in -- normal spring / damper, the anchored stiction
+           spring k_t / damper c_t (V/velocity_env_cfg.py:153-163 material, h12_12dof.urdf:168-191 sole geometry)
+  single_stance  (round 5) the same on ONE foot: the other leg's hip and knee flexed so its foot is ~6 cm up, the
+           pelvis placed over the stance foot's support polygon; the stance foot carries the whole weight
+  slip     (round 5) stance with the base sliding at 1.5-2.5 m/s and every sole anchor 8 mm behind its sphere: the
+           soles SLIP, dragged at mu_d fn (the dynamic friction coefficient shapes the force directly)
 
-Each function rewrites the physics rows of the field-major float state Fm [H12_NF_FLOAT, n] in place."""
+Each function rewrites the physics rows of the field-major float state Fm [H12_NF_FLOAT, n] in place (and, for the
+sole-contact scenarios, the sole contact flags of the packed int row Im[H12_I_PACK] when Im is given, and the action
+history; those return the (n, 12) hold action the steps are driven around)."""
 from __future__ import annotations
 
 import numpy as np
 
 import oracle as O
 from h12env._abi import F as FIELDS
+from h12env._abi import I as IFIELDS
+
+FOOT_BODY = (6, 12)  # ankle-roll bodies of the left / right leg in the oracle's body order
+CMASK_BIT0 = 13      # H12_I_PACK bit of sole sphere 0 of the left foot (bit 13 + 4 foot + point)
 
 
 def _set(Fm, name, i, v):
@@ -100,4 +114,124 @@ def lying_terrain(model, Fm, rng, terrain):
     return Fm
 
 
+def _soles(model, s):
+    """World centres (2, 4, 3) of the 8 sole spheres for the 37-float physics state s (oracle kinematics)."""
+    R, p = O.body_poses(model, s)
+    pts = np.asarray(model.foot_pts, dtype=np.float64)
+    return np.stack([(R[b] @ pts.T).T + p[b] for b in FOOT_BODY])
+
+
+def _stance_state(model, rng, quat, q):
+    s = np.zeros(37)
+    s[3:7] = quat
+    s[13:25] = q
+    return s
+
+
+def _place_on_soles(model, Fm, Im, i, s, feet, depth, anchor_shift=(0.0, 0.0), action_scale=0.5, preload=0.0):
+    """Base height so that the lowest sole sphere of `feet` is `depth` deep; anchors at the spheres' current xy
+    (world xy on the plane tasks) shifted by anchor_shift; contact flags of those feet's spheres set; the action
+    history (ACT, ACT_PREV: the delayed-PD targets of the next steps) holding the joint angles.  Returns the hold
+    action (JointPositionAction: target = q_default + scale a)."""
+    r = float(model.foot_radius)
+    sol = _soles(model, s)
+    zmin = min(sol[f][:, 2].min() for f in feet)
+    s[2] = r - depth - zmin
+    sol = _soles(model, s)
+    _set(Fm, "POS", i, s[0:3])
+    _set(Fm, "QUAT", i, s[3:7])
+    _set(Fm, "VLIN", i, s[7:10])
+    _set(Fm, "WANG", i, s[10:13])
+    _set(Fm, "Q", i, s[13:25])
+    _set(Fm, "QD", i, s[25:37])
+    oa, _ = FIELDS["ANCHOR"]
+    org = 0.0  # plane tasks: anchors in world xy (only the heightfield kernels work relative to the env origin)
+    # preload: each foot's anchors `preload` m beyond its spheres along the base's lateral axis, away from the other
+    # foot -- the sticking stiction springs then carry k_t x preload each (the legs pushed apart), so the tangential
+    # spring's constant shapes the step
+    lat = np.array(O.body_poses(model, s)[0][0][:2, 1])
+    lat = lat / max(np.linalg.norm(lat), 1e-12)
+    for f in range(2):
+        side = 1.0 if f == 0 else -1.0
+        for q in range(4):
+            Fm[oa + 8 * f + 2 * q:oa + 8 * f + 2 * q + 2, i] = (sol[f][q, :2] - org + np.asarray(anchor_shift)
+                                                                + side * preload * lat)
+    if Im is not None:
+        op, _ = IFIELDS["PACK"]
+        pk = int(Im[op, i]) & ~(0xFF << CMASK_BIT0)
+        for f in feet:
+            pk |= 0xF << (CMASK_BIT0 + 4 * f)
+        Im[op, i] = pk
+    hold = (s[13:25] - np.asarray(model.q_default, dtype=np.float64)) / action_scale
+    _set(Fm, "ACT", i, hold)
+    _set(Fm, "ACT_PREV", i, hold)
+    return hold
+
+
+def stance(model, Fm, rng, Im=None, action_scale=0.5, preload=0.0):
+    """Both feet flat (default pose: hip pitch + knee + ankle pitch sum to 0), the 8 soles ~0.8 mm deep (the static
+    load of 661 N over 8 spheres at 1e5 N/m), small velocities."""
+    n = Fm.shape[1]
+    q0 = np.asarray(model.q_default, dtype=np.float64)
+    hold = np.zeros((n, 12))
+    for i in range(n):
+        s = _stance_state(model, rng, _quat(0.0, 0.0, rng.uniform(-np.pi, np.pi)), q0 + rng.normal(size=12) * 0.005)
+        s[7:10] = rng.normal(size=3) * 0.01
+        s[10:13] = rng.normal(size=3) * 0.01
+        s[25:37] = rng.normal(size=12) * 0.02
+        s[0:2] = rng.uniform(-1, 1, 2)  # near the world origin, as flight / lying: fp32 positions to ~1e-7 m
+        hold[i] = _place_on_soles(model, Fm, Im, i, s, (0, 1), 0.8e-3, action_scale=action_scale, preload=preload)
+    return hold
+
+
+def single_stance(model, Fm, rng, Im=None, action_scale=0.5):
+    """One foot flat on the floor carrying the robot (~1.6 mm deep); the other leg's hip pitch -0.3 rad, knee +0.6 rad
+    and ankle pitch -0.3 rad (its foot ~6 cm up, level); the stance leg's hip roll / ankle roll / ankle pitch set so
+    the stance foot is flat and the composite centre of mass is over it (to ~2 mm; found once with the oracle's
+    kinematics), so the robot balances on that foot through the scenario's policy steps."""
+    n = Fm.shape[1]
+    q0 = np.asarray(model.q_default, dtype=np.float64)
+    stance_leg = {0: (-0.21944, 0.21659, 0.00376), 1: (0.22135, -0.21848, 0.00382)}  # hip roll, ankle roll, pitch
+    hold = np.zeros((n, 12))
+    for i in range(n):
+        f = i % 2  # stance foot
+        q = q0 + rng.normal(size=12) * 0.003
+        sw = 6 * (1 - f)
+        q[sw + 1] += -0.3   # swing hip pitch
+        q[sw + 3] += 0.6    # swing knee
+        q[sw + 4] += -0.3   # swing ankle pitch: the swing foot stays level
+        hr, ar, ap = stance_leg[f]
+        q[6 * f + 2] += hr
+        q[6 * f + 5] += ar
+        q[6 * f + 4] += ap
+        s = _stance_state(model, rng, _quat(0.0, 0.0, rng.uniform(-np.pi, np.pi)), q)
+        s[7:10] = rng.normal(size=3) * 0.01
+        s[10:13] = rng.normal(size=3) * 0.01
+        s[25:37] = rng.normal(size=12) * 0.02
+        s[0:2] = rng.uniform(-1, 1, 2)
+        hold[i] = _place_on_soles(model, Fm, Im, i, s, (f,), 1.6e-3, action_scale=action_scale)
+    return hold
+
+
+def slip(model, Fm, rng, Im=None, action_scale=0.5):
+    """stance, the base sliding horizontally at 1.5-2.5 m/s (random heading) with every sole anchor 8 mm behind its
+    sphere: the anchored stiction spring's trial force (k_t 8 mm + c_t v = 240 N + 200 N) is far above mu_s fn, so
+    every sole slips and is dragged at mu_d fn from the first physics step on."""
+    n = Fm.shape[1]
+    q0 = np.asarray(model.q_default, dtype=np.float64)
+    hold = np.zeros((n, 12))
+    for i in range(n):
+        s = _stance_state(model, rng, _quat(0.0, 0.0, rng.uniform(-np.pi, np.pi)), q0 + rng.normal(size=12) * 0.005)
+        hd = rng.uniform(-np.pi, np.pi)
+        u = np.array([np.cos(hd), np.sin(hd)])
+        s[7:9] = u * rng.uniform(1.5, 2.5)
+        s[25:37] = rng.normal(size=12) * 0.02
+        s[0:2] = rng.uniform(-1, 1, 2)
+        hold[i] = _place_on_soles(model, Fm, Im, i, s, (0, 1), 0.8e-3, anchor_shift=tuple(-8e-3 * u),
+                                  action_scale=action_scale)
+    return hold
+
+
 SCENARIOS = dict(flight=flight, lying=lying)
+# the sole-contact scenarios (take the packed int rows too)
+SOLE_SCENARIOS = dict(stance=stance, single_stance=single_stance, slip=slip)

@@ -13,16 +13,18 @@ The last test is the north_star criterion (<= 1e-4 relative q error over 1000 po
 FREE floating base: zero gravity (no floor contact), so the free joint's quaternion integration and the base row
 of the articulated-body solve (M/h12_12dof.xml:68; D/simulator/sim_mujoco.py:39-44,102-121) run for 20 000
 substeps next to the fp64 oracle."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
 import oracle as O
-from forced import SCEN_GATE, ForcedParity
+from forced import BIAS_GATE, SCEN_GATE, ForcedParity
 from h12env import H12FlatEnvCfg, mujoco_cfg
 from h12env._abi import F as FIELDS
 from h12env.env import H12VelocityEnv
-from scenarios import SCENARIOS, lying_terrain
+from scenarios import SCENARIOS, SOLE_SCENARIOS, lying_terrain
 
 pytestmark = pytest.mark.gpu
 
@@ -65,6 +67,61 @@ def test_forced_error_quantiles_well_conditioned(gpu, name, task):
     print(name, task, "quantiles", fp.quantiles(), "well-conditioned", fp.quantiles("wc"), "probe",
           fp.quantiles("cond"))
     fp.check_quantiles(SCEN_GATE[name if task == "flat" else name + "_rsl"])
+    env.close()
+
+
+SOLE_KW = dict(stance=dict(preload=1e-3), single_stance={}, slip={})
+
+
+def run_sole_scenario(name, n=1024, steps=20, seed=37, task="flat"):
+    """A sole-contact scenario (tests/helpers/scenarios.py SOLE_SCENARIOS): the state, sole contact flags, anchors and
+    action history written into the workspace; the steps driven by the scenario's hold action + N(0, 0.05)."""
+    cfg = scenario_cfg(task)
+    cfg.scene.num_envs = n
+    cfg.sim.device = "cuda:0"
+    env = H12VelocityEnv(cfg)
+    env.reset()
+    rng = np.random.default_rng(seed)
+    Fm = env._fstate.cpu().numpy().copy()
+    Im = env._istate.cpu().numpy().copy()
+    hold = SOLE_SCENARIOS[name](env._model, Fm, rng, Im=Im, action_scale=cfg.actions.joint_pos.scale, **SOLE_KW[name])
+    env._fstate.copy_(torch.from_numpy(Fm))
+    env._istate.copy_(torch.from_numpy(Im))
+    fp = ForcedParity(env, seed=seed + 1)
+    for _ in range(steps):
+        fp.step((hold + rng.normal(size=(n, 12)) * 0.05).astype(np.float32))
+    return env, fp
+
+
+@pytest.mark.parametrize("task", ["flat", "rsl"])
+@pytest.mark.parametrize("name", list(SOLE_SCENARIOS))
+def test_forced_sole_contact_scenarios(gpu, name, task):
+    """The sole-contact path the benchmark spends its time in (round 5): standing on both feet with the legs'
+    stiction springs preloaded, standing on one foot, and both feet slipping (h12_12dof.urdf:168-191 soles,
+    V/velocity_env_cfg.py:153-163 material; Rsl: per-env materials).  The depth of a sole contact is the difference
+    of ~1 m positions, so fp32 rounding of the state moves the one-step map by ~2e-5 here (the conditioning probe)
+    and the absolute-error quantiles cannot resolve 1e-5; the SIGNED mean error per physics-state field does
+    (ForcedParity.bias_fields: fp32 rounding averages out over the env-steps, a constant parameter error does not)
+    -- forced.BIAS_GATE, per field 3x the kernel's own measured fp32 bias + 6 standard errors, with tests/test_forced_harness.py showing on the CPU that planted errors in the stiction spring
+    k_t (1e-4), its damper c_t (1e-3), a sole sphere's x offset (1e-4), the normal spring (1e-4) and, slipping, the
+    dynamic friction coefficient (1e-4) cross it."""
+    env, fp = run_sole_scenario(name, task=task)
+    fp.check(max_bad_frac=0.01)
+    key = name if task == "flat" else name + "_rsl"
+    print(name, task, "quantiles", fp.quantiles(), "probe", fp.quantiles("cond"), "bias", fp.bias())
+    if os.environ.get("H12_GATE_MEASURE"):  # calibration runs: report the floors, gate nothing
+        import json
+
+        names, m, se = fp.bias_fields()
+        out = os.path.join(os.environ["H12_GATE_MEASURE"], f"bias_{key}.json")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        with open(out, "w") as f:
+            json.dump({"names": names, "mean": m.tolist(), "se": se.tolist(), "quantiles": fp.quantiles(),
+                       "probe": fp.quantiles("cond")}, f)
+        return
+    fp.check_quantiles(SCEN_GATE[key])
+    bad = fp.bias_violations(BIAS_GATE[key])
+    assert not bad, (bad, fp.bias(), fp.report())
     env.close()
 
 
