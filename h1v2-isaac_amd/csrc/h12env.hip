@@ -154,6 +154,32 @@ __device__ unsigned long long g_wave[1024][11];
 #define PHX_INIT() (void)0
 #define PHX(i) (void)0
 #endif
+// experiment builds only (-DH12_PHASE_PROFILE -DH12_PHASE_LIGHT): the shader-clock cycles each wave of step_kernel waits
+// in the inner steps' barriers S / R1 / R2, accumulated in registers and stored once per wave ([block][role][barrier];
+// roles 0 physics, 1 helper, 2 contact, 3 self): the wave that waits ~0 at a barrier is the one the block waited for
+#if defined(H12_PHASE_PROFILE) && defined(H12_PHASE_LIGHT)
+__device__ unsigned long long g_bw[1024][4][3];
+#define H12_BW_DECL unsigned long long _bw[3] = {0ull, 0ull, 0ull}
+#define H12_BW_PARAM , unsigned long long (&_bw)[3]
+#define H12_BW_ARG , _bw
+#define SYNC_W(k)                                                                \
+  do {                                                                           \
+    const unsigned long long _t0 = __builtin_readcyclecounter();                \
+    __syncthreads();                                                             \
+    _bw[k] += __builtin_readcyclecounter() - _t0;                               \
+  } while (0)
+#define H12_BW_STORE()                                                           \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
+      for (int _k = 0; _k < 3; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k]; \
+  } while (0)
+#else
+#define H12_BW_DECL (void)0
+#define H12_BW_PARAM
+#define H12_BW_ARG
+#define SYNC_W(k) __syncthreads()
+#define H12_BW_STORE() (void)0
+#endif
 
 thread_local char g_err[512] = "";
 int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
@@ -568,7 +594,12 @@ H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, floa
 // link_ia: on entry IA is the articulated inertia of LINK in its own frame; on exit that of the parent (rigid part
 // included; for LINK == 0 the leg's contribution to the base, at the base origin).  Keeps U, 1/D and
 // Ic = Ia c (c = the velocity-product acceleration) for link_p and pass 3.
-template <int LINK>
+// AV (step_kernel's physics wave, round 5): the velocity-product accelerations are carried by the rigid-body bias forces
+// instead (b_i = I_i a^v_i + v_i x* I_i v_i, a^v the accelerations of the links at zero joint and base acceleration,
+// link_av; computed by the helper / contact waves), so the articulated-body recursion runs with c = 0: no Ic = Ia c
+// here, no c in link_p / link_pass3 (exact algebra: the accelerations a~ = a - a^v obey a~_i = X_i a~_parent + S qdd_i;
+// DESIGN.md section 2)
+template <int LINK, bool AV = false>
 H12_DEV void link_ia(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
                      const ImplC& ick, float knee_pz, const float* dl, AInertia& IA, float (&U)[NL][6],
                      float (&Dinv)[NL], float (&Ic)[NL][6], float h) {
@@ -589,9 +620,11 @@ H12_DEV void link_ia(const KParams& P, const Leg& lg, const float (&cs)[NL][2], 
   IA.C[3] -= Ul[0] * Uld[1]; IA.C[4] -= Ul[0] * Uld[2]; IA.C[5] -= Ul[1] * Uld[2];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * Uld[j];
-  float cb[6];
-  vprod<A>(v[LINK], lg.qd[LINK], cb);
-  ai_mul(IA, cb, Ic[LINK]);
+  if constexpr (!AV) {
+    float cb[6];
+    vprod<A>(v[LINK], lg.qd[LINK], cb);
+    ai_mul(IA, cb, Ic[LINK]);
+  }
   // to the parent: rotate into parent axes, then shift the reference point by r
   ai_rotate<A>(IA, cs[LINK][0], cs[LINK][1]);
   ai_shift(IA, h12m::R[LINK]);
@@ -609,7 +642,7 @@ H12_DEV void link_ia(const KParams& P, const Leg& lg, const float (&cs)[NL][2], 
 }
 // link_p: on entry pAcc is the bias force of LINK (own frame, applied forces subtracted); on exit the parent's
 // (its rigid-body bias force pbias[LINK - 1] included, the knee's external wrench subtracted), u[LINK] set.
-template <int LINK>
+template <int LINK, bool AV = false>
 H12_DEV void link_p(const float (&cs)[NL][2], const float (&U)[NL][6], const float (&Dinv)[NL], const float (&Ic)[NL][6],
                     const float* tau, const float (&pbias)[NL][6], const float* fext_knee, float* pAcc, float (&u)[NL]) {
   constexpr int A = AX[LINK];
@@ -617,7 +650,7 @@ H12_DEV void link_p(const float (&cs)[NL][2], const float (&U)[NL][6], const flo
   u[LINK] = uu;
   const float ud = uu * Dinv[LINK];
   float pa[6];
-  for (int i = 0; i < 6; ++i) pa[i] = pAcc[i] + Ic[LINK][i] + U[LINK][i] * ud;
+  for (int i = 0; i < 6; ++i) pa[i] = AV ? pAcc[i] + U[LINK][i] * ud : pAcc[i] + Ic[LINK][i] + U[LINK][i] * ud;
   const float c = cs[LINK][0], s = cs[LINK][1];
   const float* r = h12m::R[LINK];
   float nr[3], fr[3], rf[3];
@@ -634,7 +667,7 @@ H12_DEV void link_p(const float (&cs)[NL][2], const float (&U)[NL][6], const flo
 }
 
 // ---- ABA pass 3 for leg link LINK (root -> leaf)
-template <int LINK>
+template <int LINK, bool AV = false>
 H12_DEV void link_pass3(const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6], const float (&U)[NL][6],
                         const float (&Dinv)[NL], const float (&u)[NL], float* a, float* qdd) {
   constexpr int A = AX[LINK];
@@ -643,17 +676,69 @@ H12_DEV void link_pass3(const Leg& lg, const float (&cs)[NL][2], const float (&v
   float t[3];
   cross(r, a, t);
   float lin[3] = {a[3] - t[0], a[4] - t[1], a[5] - t[2]};
-  float w[3], l[3], cb[6];
+  float w[3], l[3];
   rotT<A>(c, s, a, w);
   rotT<A>(c, s, lin, l);
-  vprod<A>(v[LINK], lg.qd[LINK], cb);
-  a[0] = w[0] + cb[0]; a[1] = w[1] + cb[1]; a[2] = w[2] + cb[2];
-  a[3] = l[0] + cb[3]; a[4] = l[1] + cb[4]; a[5] = l[2] + cb[5];
+  if constexpr (AV) {
+    a[0] = w[0]; a[1] = w[1]; a[2] = w[2];
+    a[3] = l[0]; a[4] = l[1]; a[5] = l[2];
+  } else {
+    float cb[6];
+    vprod<A>(v[LINK], lg.qd[LINK], cb);
+    a[0] = w[0] + cb[0]; a[1] = w[1] + cb[1]; a[2] = w[2] + cb[2];
+    a[3] = l[0] + cb[3]; a[4] = l[1] + cb[4]; a[5] = l[2] + cb[5];
+  }
   float ua = 0.f;
   for (int i = 0; i < 6; ++i) ua += U[LINK][i] * a[i];
   float x = (u[LINK] - ua) * Dinv[LINK];
   qdd[LINK] = x;
   a[A] += x;
+}
+
+// ---- velocity-product accelerations a^v (round 5, the AV form of the ABA): the links' spatial accelerations when every
+// joint and the base have zero acceleration, a^v_i = X_i a^v_parent + v_i x (e_A qd_i), a^v_base = 0 (link coords, lane
+// frame).  av: on entry the parent's, on exit link LINK's.
+template <int LINK>
+H12_DEV void link_av(const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6], float* av) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  const float c = cs[LINK][0], s = cs[LINK][1];
+  float t[3];
+  cross(r, av, t);
+  float lin[3] = {av[3] - t[0], av[4] - t[1], av[5] - t[2]};
+  float w[3], l[3], cb[6];
+  rotT<A>(c, s, av, w);
+  rotT<A>(c, s, lin, l);
+  vprod<A>(v[LINK], lg.qd[LINK], cb);
+  av[0] = w[0] + cb[0]; av[1] = w[1] + cb[1]; av[2] = w[2] + cb[2];
+  av[3] = l[0] + cb[3]; av[4] = l[1] + cb[4]; av[5] = l[2] + cb[5];
+}
+// b += I_LINK a: the rigid inertia of leg link LINK (Ibar, m c, m; link origin, link coords) times a spatial acceleration
+template <int LINK>
+H12_DEV void rigid_mul_add(const float* a, float* b) {
+  const float* Ibar = h12m::IBAR[LINK];
+  const float* mc = h12m::MC[LINK];
+  const float m = h12m::M[LINK];
+  float x1[3], x2[3];
+  cross(mc, a + 3, x1);
+  cross(mc, a, x2);
+  for (int i = 0; i < 3; ++i) {
+    b[i] += sget(Ibar, i, 0) * a[0] + sget(Ibar, i, 1) * a[1] + sget(Ibar, i, 2) * a[2] + x1[i];
+    b[3 + i] += m * a[3 + i] - x2[i];
+  }
+}
+// b += M a at a body point p (the implicit contact's added point inertia M = beta I + gamma u u^T, body coords): the
+// force M a_p at p (a_p = a_lin + a_ang x p) and its moment p x M a_p
+H12_DEV void point_inertia_mul_add(const float* a, const float* p, const float* u, float beta, float gamma, float* b) {
+  float ap[3];
+  cross(a, p, ap);
+  ap[0] += a[3]; ap[1] += a[4]; ap[2] += a[5];
+  const float gn = gamma * (u[0] * ap[0] + u[1] * ap[1] + u[2] * ap[2]);
+  const float f[3] = {beta * ap[0] + gn * u[0], beta * ap[1] + gn * u[1], beta * ap[2] + gn * u[2]};
+  float n[3];
+  cross(p, f, n);
+  b[0] += n[0]; b[1] += n[1]; b[2] += n[2];
+  b[3] += f[0]; b[4] += f[1]; b[5] += f[2];
 }
 
 // ---- flat ground: the 4 sole spheres of the foot in one pass.  On a plane every sphere has the same ground
@@ -675,6 +760,8 @@ constexpr float sole_pp(int q, int k) {  // p p^T, symmetric packing
   return k < 3 ? f[k] * f[k] : (k == 3 ? f[0] * f[1] : (k == 4 ? f[0] * f[2] : f[1] * f[2]));
 }
 
+// Q0..Q1: the sole spheres this call evaluates (step_kernel splits them over two waves; the single-wave step all 4)
+template <int Q0 = 0, int Q1 = H12_NFOOT_PTS>
 H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const float* pf, const float* vb, Leg& lg,
                                 AInertia& IA, float* pAcc, float* fw, SoleSums& ss) {
   float ww[3], v0[3];  // foot angular velocity and origin velocity, world axes
@@ -686,39 +773,43 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
   int nmask = 0;
   const float alpha = P.h * P.cc, hb = P.h * P.fc;
 #pragma unroll
-  for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+  for (int q = Q0; q < Q1; ++q) {
     float r[3];
     mv(R, h12m::FOOT[q], r);
     const float depth = h12m::FOOT_R - (r[2] + pf[2]);
     float vw[3];
     cross(ww, r, vw);
     vw[0] += v0[0]; vw[1] += v0[1]; vw[2] += v0[2];
-    if (!(depth - (P.impl ? P.h * vw[2] : 0.f) > 0.f)) continue;  // predicted end-of-step depth (contact_sphere)
+    // branch-free (round 5): an inactive sphere contributes zeros -- the early-out branches made the compiler re-zero
+    // the ~26 accumulators on every skip path (~95 v_mov per call); the same float operations on the active ones
     const bool was = (lg.cmask >> q) & 1;
     // an opening contact is pushed out at most at max_depenetration_velocity (contact_sphere)
-    const float fn = P.ck * (was ? depth : fminf(depth, P.dcap)) - P.cc * vw[2];
-    if (!(fn > 0.f)) continue;
+    const float fn0 = P.ck * (was ? depth : fminf(depth, P.dcap)) - P.cc * vw[2];
+    // active when predicted below the ground at the end of the step (contact_sphere) and pushing
+    const bool on = (depth - (P.impl ? P.h * vw[2] : 0.f) > 0.f) && fn0 > 0.f;
+    const float fn = on ? fn0 : 0.f;
     const float x0 = r[0] + pf[0], x1 = r[1] + pf[1];
     float ax = was ? lg.anc[q][0] : x0, ay = was ? lg.anc[q][1] : x1;
     float ft0 = -P.fk * (x0 - ax) - P.fc * vw[0];
     float ft1 = -P.fk * (x1 - ay) - P.fc * vw[1];
     const float ftn2 = ft0 * ft0 + ft1 * ft1, cap = lg.mus * fn;
     const bool stick = !(ftn2 > cap * cap);
-    if (!stick) {
+    {
       const float sc = lg.mud * fn * __builtin_amdgcn_rsqf(ftn2);
-      ft0 *= sc;
-      ft1 *= sc;
       const float ik = frcp(P.fk);
-      ax = x0 + ft0 * ik;
-      ay = x1 + ft1 * ik;
+      const float s0 = ft0 * sc, s1 = ft1 * sc;
+      ax = stick ? ax : x0 + s0 * ik;
+      ay = stick ? ay : x1 + s1 * ik;
+      ft0 = on ? (stick ? ft0 : s0) : 0.f;
+      ft1 = on ? (stick ? ft1 : s1) : 0.f;
     }
-    lg.anc[q][0] = ax;
-    lg.anc[q][1] = ay;
-    nmask |= 1 << q;
+    lg.anc[q][0] = on ? ax : lg.anc[q][0];
+    lg.anc[q][1] = on ? ay : lg.anc[q][1];
+    nmask |= (on ? 1 : 0) << q;
     float Fw[3] = {ft0, ft1, fn};
     if (P.impl) {  // g M_w e_z = g (beta + gamma) e_z on a plane
-      const float beta = stick ? hb : 0.f, gam = alpha - beta;
-      Fw[2] += P.g * alpha;
+      const float beta = (on && stick) ? hb : 0.f, gam = on ? alpha - beta : 0.f;
+      Fw[2] += on ? P.g * alpha : 0.f;
       ss.sb += beta;
       ss.sg += gam;
 #pragma unroll
@@ -737,7 +828,8 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
     F[0] += Fw[0]; F[1] += Fw[1]; F[2] += Fw[2];
     T[0] += rf[0]; T[1] += rf[1]; T[2] += rf[2];
   }
-  lg.cmask = nmask;
+  constexpr int OWN = ((1 << Q1) - 1) & ~((1 << Q0) - 1);
+  lg.cmask = (lg.cmask & ~OWN) | nmask;
   float fl[3], tl[3];
   mtv(R, F, fl);
   mtv(R, T, tl);
@@ -1061,24 +1153,34 @@ H12_DEV void self_contacts(const KParams& P, int leg, float mu, const float (&Rk
   self_finish(P, leg, act, Rk, pk, Rf, pf, wk, wf, fr);
 }
 
-// ---- the helper waves (step_kernel: two more waves per block, on other SIMDs of the CU).  The forces of an inner
-// step that do not depend on its ground contacts -- the joint torques beyond the PD term (limit penalty,
-// max-velocity damper, damping, friction loss) with their implicit inertias, the rigid-body bias forces of the 6
-// links, and the leg-leg self-contact wrenches -- are computed from the state at the start of the inner step by
-// helper waves while the physics wave runs pass 1, the ground contacts and the articulated-inertia chain of
-// pass 2.  Per inner step (workgroup barriers S, R1, R2):
-//   physics wave: pass 1, knee / sole contacts | R1 | inertia chain | R2 | bias-force chain, base solve, pass 3,
-//                 integration, next state to LDS | S
-//   helper wave:  S | joint terms | R1 | pass 1, bias forces | R2
+// ---- the helper waves (step_kernel: two or three more waves per block, on other SIMDs of the CU).  The forces of an
+// inner step that do not depend on the articulated-inertia chain are computed from the state at the start of the inner
+// step by helper waves while the physics wave runs the joint torques and the articulated-inertia chain of pass 2.
+// Round 5: the velocity-product accelerations move into the rigid-body bias forces (the AV form: link_av, link_ia<AV>),
+// so the physics wave needs neither the link velocities nor the link poses -- only the joint sin / cos; the soles'
+// ground contacts go to the helper wave and a fourth (CONTACT) wave takes the knee / torso contacts and the bias forces
+// of the lower leg.  Per inner step (workgroup barriers S, R1, R2):
+//   physics wave: joint sin / cos, delayed PD + joint terms | R1 | inertia chain (+ sole / knee contact inertias) | R2 |
+//                 bias-force chain, base solve, pass 3, integration, next state to LDS | S
+//   helper wave:  S | pass 1, heel sole contacts (force, added inertia, stiction anchors) | R1 | a^v and bias forces
+//                 of links 0-2, base body bias force (flat: torso contact) | R2
+//   contact wave: S | pass 1, toe sole contacts, knee contact (terrain: torso contact) | R1 | a^v of the leg, bias
+//                 forces of links 3-5 with the sole / knee added inertias' M a^v | R2
 //   self wave:    S | pass 1, self-contact broad phase + staging | R1 | pair jobs, wrenches | R2
 // (the self wave is launched only with self-collision).
 struct HelpLds {
   float4 st[8][BLOCK];    // state: base pos (3), quat (4), v (3), w (3); leg q (6), qd (6) (lane frame); env origin (3);
-                          // added torso mass (1)
-  float4 jt[9][BLOCK];    // joint terms: tq (6, incl. the delayed PD), dl (6); knee contact: wrench (6), reported force
-                          // (3), ImplC (5), z (1); spare (1); the delayed-PD torque alone (6), spare (2)
-  float4 pd[6][BLOCK];    // per env step: a_t, a_{t-1}, a_{t-2} of the leg (lane frame, 18), packed lags, steps since reset
-  float4 bias[11][BLOCK]; // bias forces of the 6 links (6 x 6), base body bias force (6; lane 0, else 0)
+                          // added torso mass (1), sole mu_d (1), mu_s (1), spare (1)
+  float4 jt[4][BLOCK];    // knee contact: wrench (6), reported force (3), ImplC (5), z (1); spare (1)
+  float4 bias_h[6][BLOCK];  // helper: bias forces b_0..b_2 (18), base body bias force (6; lane 0, else 0)
+  float4 bias_c[5][BLOCK];  // contact wave: bias forces b_3..b_5 (18; the knee / sole added inertias' M a^v in), spare
+  float4 cw1[2][11][BLOCK];  // before R1, per half of the soles (spheres 0-1: helper; 2-3: contact wave): their added
+                          // inertia (AInertia, 21), minus their wrench (6), their force (3, body coords), the implicit
+                          // report (flat: sum beta, sum gamma, sum beta p, sum gamma p, u = 11; terrain: beta[2],
+                          // gamma[2], u[2][3] = 10)
+  float4 cw2[3][BLOCK];   // contact wave before R2: a^v of links 3 and 5 (12)
+  float4 cst[3][BLOCK];   // sole contact state across the env step: anchors (8, lane frame), contact mask bits of
+                          // spheres 0-1 (helper) and 2-3 (contact wave) as two ints
   float4 selfw[3][BLOCK]; // knee self wrench (6), foot self wrench (6)
   uint4 rnd[4][BLOCK];    // the env's reset / command-resample Philox blocks of this step (reset_draws)
   float4 torso[4][BLOCK]; // torso-box ground contact (lane 0 of the pair): wrench (6), reported force (3), ImplC
@@ -1167,27 +1269,54 @@ H12_DEV void fuse_drain(const FuseCtx& f, int it) {
   if (f.on && it == 1) __builtin_amdgcn_s_waitcnt(0);
 }
 
-// CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the joint-term
-// hand-off array (free once the last inner step has read it; the LDS footprint stays the three-wave block's)
+// CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the contact wave's
+// R1 hand-off array (free once the last inner step's physics wave has read it)
 typedef float CatLds[H12_NCSTR_COLS + 1][ENVS_PER_BLOCK];
-static_assert(sizeof(CatLds) <= sizeof(HelpLds::jt), "CaT values fit the joint-term array");
-H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().jt[0][0]); }
+static_assert(sizeof(CatLds) <= sizeof(HelpLds::cw1), "CaT values fit the contact hand-off array");
+H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().cw1[0][0][0]); }
+// Hand-off arrays between the waves of a block: declared as float4 [n4][BLOCK], used FIELD-MAJOR as float [4 n4][BLOCK]
+// (value i of lane l at i * 256 + 4 l bytes): the writes / reads pair into ds_write2_b32 / ds_read2_b32 with two
+// independent data registers, where float4-per-lane ds_write_b128 needs its 4 values moved into an aligned register
+// quad first (round 5: ~100 v_mov per inner step)
 H12_DEV void put4(float4 (*dst)[BLOCK], int l, const float* x, int n4) {
-  for (int c = 0; c < n4; ++c) dst[c][l] = make_float4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
+  float (*d)[BLOCK] = reinterpret_cast<float (*)[BLOCK]>(dst);
+  for (int i = 0; i < 4 * n4; ++i) d[i][l] = x[i];
 }
 H12_DEV void get4(const float4 (*src)[BLOCK], int l, float* x, int n4) {
-  for (int c = 0; c < n4; ++c) {
-    const float4 y = src[c][l];
-    x[4 * c] = y.x; x[4 * c + 1] = y.y; x[4 * c + 2] = y.z; x[4 * c + 3] = y.w;
-  }
+  const float (*d)[BLOCK] = reinterpret_cast<const float (*)[BLOCK]>(src);
+  for (int i = 0; i < 4 * n4; ++i) x[i] = d[i][l];
 }
 H12_DEV void put_state(int l, const Base& b, const Leg& lg, const float* org) {
   float x[32] = {b.pos[0], b.pos[1], b.pos[2], b.quat[0], b.quat[1], b.quat[2], b.quat[3],
                  b.vlin[0], b.vlin[1], b.vlin[2], b.wang[0], b.wang[1], b.wang[2]};
   for (int k = 0; k < NL; ++k) { x[13 + k] = lg.q[k]; x[19 + k] = lg.qd[k]; }
   x[25] = org[0]; x[26] = org[1]; x[27] = org[2];
-  x[28] = lg.dmass; x[29] = lg.mud; x[30] = x[31] = 0.f;
+  x[28] = lg.dmass; x[29] = lg.mud; x[30] = lg.mus; x[31] = 0.f;
   put4(help_lds().st, l, x, 8);
+}
+// the sole contact state (stiction anchors, contact mask; lane frame) of the env step: the physics wave hands it to the
+// contact wave before the first inner step and reads it back after the last (barrier L)
+H12_DEV void put_cst(int l, const Leg& lg) {
+  float x[12];
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) { x[2 * q] = lg.anc[q][0]; x[2 * q + 1] = lg.anc[q][1]; }
+  x[8] = __int_as_float(lg.cmask);
+  x[9] = __int_as_float(0);
+  x[10] = x[11] = 0.f;
+  put4(help_lds().cst, l, x, 3);
+}
+H12_DEV void get_cst(int l, Leg& lg) {
+  float x[12];
+  get4(help_lds().cst, l, x, 3);
+  for (int q = 0; q < H12_NFOOT_PTS; ++q) { lg.anc[q][0] = x[2 * q]; lg.anc[q][1] = x[2 * q + 1]; }
+  lg.cmask = __float_as_int(x[8]) | __float_as_int(x[9]);
+}
+// the owner of sole spheres Q0, Q0 + 1 hands their final anchors and contact bits back (field-major rows: the two
+// owners write disjoint floats)
+template <int Q0>
+H12_DEV void put_cst_half(int l, const Leg& lg) {
+  float (*d)[BLOCK] = reinterpret_cast<float (*)[BLOCK]>(help_lds().cst);
+  for (int q = Q0; q < Q0 + 2; ++q) { d[2 * q][l] = lg.anc[q][0]; d[2 * q + 1][l] = lg.anc[q][1]; }
+  d[8 + Q0 / 2][l] = __int_as_float(lg.cmask & (3 << Q0));
 }
 
 H12_DEV void rng(const KParams& P, uint32_t g, uint32_t lo, uint32_t hi, int stream, int block, uint32_t out[4]);
@@ -1228,22 +1357,6 @@ H12_DEV void pd_torque(const KParams& P, const PdIn& d, const Leg& lg, int st, f
     }
   }
 }
-H12_DEV void put_pd(int l, const PdIn& d) {
-  float x[24];
-  for (int k = 0; k < NL; ++k) { x[k] = d.act[k]; x[6 + k] = d.act1[k]; x[12 + k] = d.act2[k]; }
-  x[18] = (float)d.lagpk;
-  x[19] = (float)d.since_reset;
-  x[20] = x[21] = x[22] = x[23] = 0.f;
-  put4(help_lds().pd, l, x, 6);
-}
-H12_DEV void get_pd(int l, PdIn& d) {
-  float x[24];
-  get4(help_lds().pd, l, x, 6);
-  for (int k = 0; k < NL; ++k) { d.act[k] = x[k]; d.act1[k] = x[6 + k]; d.act2[k] = x[12 + k]; }
-  d.lagpk = (int)x[18];
-  d.since_reset = (int)x[19];
-}
-
 // joint torques beyond the PD term (tq) and the implicit joint inertia of the active limits (dl), from q / qd
 H12_DEV void joint_terms(const KParams& P, const Leg& lg, float h, float* tq, float* dl) {
 #pragma unroll
@@ -1323,7 +1436,8 @@ H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], c
 // the lowest corner touches: their heightfield lookups stay off a standing robot's helper wave) --
 // the face whose normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso
 // lying on a face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same
-// order).  Evaluated by the helper wave (helper_torso: before R1 on terrain, between R1 and R2 on flat ground).
+// order).  Evaluated by helper_torso: the helper wave before R1 on terrain, the contact wave between R1 and R2 on flat
+// ground.
 H12_DEV void torso_corner(const float (&R0)[3][3], float* corner) {
   for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
 }
@@ -1383,6 +1497,7 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
   get4(help_lds().st, l, x, 8);
   lg.dmass = x[28];
   lg.mud = x[29];
+  lg.mus = x[30];
   for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; org[i] = x[25 + i]; }
   for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
   for (int k = 0; k < NL; ++k) { lg.q[k] = x[13 + k]; lg.qd[k] = x[19 + k]; }
@@ -1415,10 +1530,61 @@ H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const
   put4(help_lds().torso, l, t, 4);
 }
 
+// Half of the soles' ground contacts of the leg (spheres Q0, Q0 + 1: penalty force, stiction anchors, the implicit added
+// inertia; step_kernel's helper / contact wave, before R1) into the cw1[Q0 / 2] hand-off: dI (foot coords), minus the
+// wrench, the force, the implicit report
+template <int K, int Q0>
+H12_DEV void sole_handoff(const KParams& P, int l, float sg, Leg& lg, const float (&R)[3][3], const float* p,
+                          const float* v5, const float* org) {
+  AInertia dI;
+  for (int i = 0; i < 6; ++i) { dI.A[i] = 0.f; dI.C[i] = 0.f; }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) dI.B[i][j] = 0.f;
+  float o[44];
+  float* pc = o + 21;  // minus the sole wrench (foot coords)
+  float* fw = o + 27;  // the soles' force (body coords; only its norm is used)
+  for (int i = 21; i < 44; ++i) o[i] = 0.f;
+  if constexpr (!Feat<K>::terrain) {
+    SoleSums ss;
+    sole_contacts_flat<Q0, Q0 + 2>(P, R, p, v5, lg, dI, pc, fw, ss);
+    o[30] = ss.sb; o[31] = ss.sg;
+    for (int a = 0; a < 3; ++a) { o[32 + a] = ss.pb[a]; o[35 + a] = ss.pg[a]; o[38 + a] = R[2][a]; }
+  } else {
+    float fext[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int nmask = 0;
+#pragma unroll
+    for (int q = Q0; q < Q0 + 2; ++q) {
+      const bool was = (lg.cmask >> q) & 1;
+      ImplC ic;
+      if (contact_sphere<true, true>(P, R, p, v5, h12m::FOOT[q], h12m::FOOT_R, fext, fw, lg.anc[q], was, sg, org,
+                                     lg.mus, lg.mud, ic)) {
+        nmask |= 1 << q;
+        if (P.impl) {
+          ai_add_contact(dI, h12m::FOOT[q], ic.u, ic.beta, ic.gamma);
+          const int j = q - Q0;
+          o[30 + j] = ic.beta; o[32 + j] = ic.gamma;
+          o[34 + 3 * j] = ic.u[0]; o[35 + 3 * j] = ic.u[1]; o[36 + 3 * j] = ic.u[2];
+        }
+      }
+    }
+    lg.cmask = (lg.cmask & ~(3 << Q0)) | nmask;
+    for (int i = 0; i < 6; ++i) pc[i] = -fext[i];
+  }
+  const float* di = &dI.A[0];
+  static_assert(sizeof(AInertia) == 21 * sizeof(float), "AInertia layout");
+  for (int i = 0; i < 21; ++i) o[i] = di[i];
+  put4(help_lds().cw1[Q0 / 2], l, o, 11);
+}
+
+// The helper wave: before R1 its own pass 1 and the heel spheres' ground contacts (sole_handoff; their anchors and
+// contact bits stay in its registers through the env step, LDS cst hand-off with the physics wave before the first /
+// after the last inner step); after R1 the bias forces of links 0-2 (AV form), the base body's and, on flat ground,
+// the torso box's contact.
 template <int K>
 H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint32_t lo, uint32_t hi, const FuseCtx& fc) {
   const int l = threadIdx.x - BLOCK;
   const int leg = l & 1;
+  const float sg = leg ? -1.f : 1.f;
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
   // the Philox blocks a reset (ST_RESET 0, 1) or a command resample (ST_CMD 0, 1) of this step would draw: they
@@ -1432,63 +1598,137 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
     rng(P, g, lo, hi, ST_CMD, 0, r); H.rnd[2][l] = make_uint4(r[0], r[1], r[2], r[3]);
     rng(P, g, lo, hi, ST_CMD, 1, r); H.rnd[3][l] = make_uint4(r[0], r[1], r[2], r[3]);
   }
-  PdIn pd;
-  float tau_pd[NL];
+  Leg lg;
+  H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
-    __syncthreads();  // S: the state of this inner step
+    SYNC_W(0);  // S: the state of this inner step
     Base b;
-    Leg lg;
     float org[3];
-    float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
+    float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
     if (active) {
       get_state(l, b, lg, org);
-      if (it == 0) get_pd(l, pd);
-      // the delayed PD torque is computed at the first inner step of each physics step and held over it
-      if (it % P.inner == 0) pd_torque(P, pd, lg, it / P.inner, tau_pd);
-      float jt[36];
-      joint_terms(P, lg, P.h, jt, jt + 6);
-      for (int k = 0; k < NL; ++k) { jt[k] += tau_pd[k]; jt[28 + k] = tau_pd[k]; }
-      jt[34] = jt[35] = 0.f;
+      if (it == 0) get_cst(l, lg);
+      float Rk[3][3], pk[3], R[3][3], p[3];
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
-      ImplC ick;
-      for (int i = 12; i < 21; ++i) jt[i] = 0.f;
-      knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt + 12, jt + 18, ick, jt[26]);
-      jt[21] = ick.beta; jt[22] = ick.gamma; jt[23] = ick.u[0]; jt[24] = ick.u[1]; jt[25] = ick.u[2]; jt[27] = 0.f;
-      put4(H.jt, l, jt, 9);
-      // torso-box ground contact (the base body; lane 0 of the pair) from the step's state: data-dependent work
-      // (a fallen robot's) kept off the physics wave's chain.  On terrain before R1 (the R1 -> R2 window is then the
-      // helper's critical one: its ground lookups cost Rough / C5 2.7 us per step there), on flat ground after R1
-      // (there the window before R1 is: 1.1 us per step)
-      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
+      sole_handoff<K, 0>(P, l, sg, lg, R, p, v[5], org);  // the heel spheres
     }
-    __syncthreads();  // R1: joint terms, knee contact (terrain: torso contact)
+    SYNC_W(1);  // R1: sole contacts (helper, contact wave), knee contact (contact wave)
     if (active) {
-      float pb[NL][6], o[44];
-      leg_bias(v, pb);
-      for (int k = 0; k < NL; ++k)
-        for (int i = 0; i < 6; ++i) o[6 * k + i] = pb[k][i];
+      // bias forces b_i = I_i a^v_i + v_i x* I_i v_i of links 0-2 (the AV form; links 3-5: the contact wave) and the
+      // base body's v x* I v (a^v of the base is 0)
+      float o[24], av[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      bias<0>(v[0], o);
+      link_av<0>(lg, cs, v, av);
+      rigid_mul_add<0>(av, o);
+      bias<1>(v[1], o + 6);
+      link_av<1>(lg, cs, v, av);
+      rigid_mul_add<1>(av, o + 6);
+      bias<2>(v[2], o + 12);
+      link_av<2>(lg, cs, v, av);
+      rigid_mul_add<2>(av, o + 12);
       const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
       AInertia Rg;
-      base_body<K>(P, lg, v0, Rg, o + 36);
-      if (leg) for (int i = 36; i < 42; ++i) o[i] = 0.f;
-      o[42] = o[43] = 0.f;
-      put4(H.bias, l, o, 11);
+      base_body<K>(P, lg, v0, Rg, o + 18);
+      if (leg) for (int i = 18; i < 24; ++i) o[i] = 0.f;
+      put4(H.bias_h, l, o, 6);
       if constexpr (!Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
     }
     fuse_drain(fc, it);
-    __syncthreads();  // R2: bias forces (flat: torso contact)
+    SYNC_W(2);  // R2: bias forces (flat: torso contact)
     fuse_early(fc, it, n_steps, l, blockDim.x - BLOCK);
   }
+  H12_BW_STORE();
+  if (active) put_cst_half<0>(l, lg);  // the env step's final heel anchors / contact bits (read after L)
 }
 
+// The contact wave (round 5): before R1 its own pass 1, the toe spheres' and the knee capsule's ground contacts
+// (terrain: the torso box's too); after R1 the leg's velocity-product accelerations a^v and the bias forces of links
+// 3-5, including the M a^v of the implicit knee and sole contacts (the AV form: a contact's added inertia M sees the
+// link's acceleration a~ + a^v; the soles' added inertia from both halves' cw1 hand-offs).
 template <int K>
-H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) {
+H12_DEV void contact_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) {
   const int l = threadIdx.x - 2 * BLOCK;
   const int leg = l & 1;
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
+  Leg lg;
+  H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
-    __syncthreads();  // S: the state of this inner step
+    SYNC_W(0);  // S: the state of this inner step
+    float cs[NL][2], v[NL][6];
+    Base b;
+    float org[3], R0[3][3], vb[3], pb0[3];
+    ImplC ick;
+    float knee_pz = 0.f;
+    if (active) {
+      get_state(l, b, lg, org);
+      if (it == 0) get_cst(l, lg);
+      float Rk[3][3], pk[3], R[3][3], p[3];
+      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
+      sole_handoff<K, 2>(P, l, leg ? -1.f : 1.f, lg, R, p, v[5], org);  // the toe spheres
+      float jt[16];
+      for (int i = 0; i < 9; ++i) jt[i] = 0.f;
+      knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt, jt + 6, ick, knee_pz);
+      jt[9] = ick.beta; jt[10] = ick.gamma; jt[11] = ick.u[0]; jt[12] = ick.u[1]; jt[13] = ick.u[2];
+      jt[14] = knee_pz; jt[15] = 0.f;
+      put4(H.jt, l, jt, 4);
+      // torso-box ground contact (the base body; lane 0 of the pair): data-dependent work (a fallen robot's) kept off
+      // the physics wave's chain; on terrain before R1, on flat ground after R1
+      if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
+    }
+    SYNC_W(1);  // R1: the helper's sole contacts
+    if (active) {
+      float o[20], av[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, av3[6];
+      link_av<0>(lg, cs, v, av);
+      link_av<1>(lg, cs, v, av);
+      link_av<2>(lg, cs, v, av);
+      link_av<3>(lg, cs, v, av);
+      for (int i = 0; i < 6; ++i) { av3[i] = av[i]; o[i] = 0.f; }
+      bias<3>(v[3], o);
+      rigid_mul_add<3>(av, o);
+      if (P.impl && ick.beta + ick.gamma > 0.f) {  // the knee contact's added point inertia sees a^v_3 too
+        const float pkz[3] = {0.f, 0.f, knee_pz};
+        point_inertia_mul_add(av, pkz, ick.u, ick.beta, ick.gamma, o);
+      }
+      link_av<4>(lg, cs, v, av);
+      bias<4>(v[4], o + 6);
+      rigid_mul_add<4>(av, o + 6);
+      link_av<5>(lg, cs, v, av);
+      bias<5>(v[5], o + 12);
+      rigid_mul_add<5>(av, o + 12);
+      {  // the soles' added inertia (both halves, cw1) times a^v_5
+        float x[24], y[24];
+        get4(H.cw1[0], l, x, 6);
+        get4(H.cw1[1], l, y, 6);
+        AInertia& dI = *reinterpret_cast<AInertia*>(x);
+        ai_add(dI, *reinterpret_cast<const AInertia*>(y));
+        float ma[6];
+        ai_mul(dI, av, ma);
+        for (int i = 0; i < 6; ++i) o[12 + i] += ma[i];
+      }
+      o[18] = o[19] = 0.f;
+      put4(H.bias_c, l, o, 5);
+      float w[12];
+      for (int i = 0; i < 6; ++i) { w[i] = av3[i]; w[6 + i] = av[i]; }
+      put4(H.cw2, l, w, 3);
+    }
+    fuse_drain(fc, it);
+    SYNC_W(2);  // R2
+    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, blockDim.x - BLOCK);
+  }
+  H12_BW_STORE();
+  if (active) put_cst_half<2>(l, lg);  // the env step's final toe anchors / contact bits (read after L)
+}
+
+template <int K>
+H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) {
+  const int l = threadIdx.x - 3 * BLOCK;
+  const int leg = l & 1;
+  const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
+  HelpLds& H = help_lds();
+  H12_BW_DECL;
+  for (int it = 0; it < n_steps; ++it) {
+    SYNC_W(0);  // S: the state of this inner step
     float Rk[3][3], pk[3], R[3][3], p[3];
     uint64_t act = 0;
     if (active) {
@@ -1500,7 +1740,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
       act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);
     }
-    __syncthreads();  // R1
+    SYNC_W(1);  // R1
     if (active) {
       float w[12];
       Forces fr = {};
@@ -1508,19 +1748,18 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       put4(H.selfw, l, w, 3);
     }
     fuse_drain(fc, it);
-    __syncthreads();  // R2: self-contact wrenches
+    SYNC_W(2);  // R2: self-contact wrenches
     fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, blockDim.x - BLOCK);
   }
+  H12_BW_STORE();
 }
 
-// One inner step of length h for the lane's leg and the shared base.  tau_pd: actuator torques of the
-// lane's 6 joints (lane frame): an input without a helper wave, the helper's delayed-PD torque on return with one.  Adds this lane's contact forces into fr.  HW: the block has a helper wave
-// (step_kernel; the state of this step is in LDS and, with more, the next one is put there), else the
-// contact-independent forces are evaluated in this wave.
-template <int K, bool HW>
-H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_pd, float h, Forces& fr,
-                        const float* org, bool more) {
-  PHX_INIT();
+// One inner step of length h for the lane's leg and the shared base, the whole step in ONE wave (physics_kernel, the
+// MuJoCo-mode parity hook; step_kernel's waves split it, inner_step_hw): tau_pd, the actuator torques of the lane's 6
+// joints (lane frame).  Adds this lane's contact forces into fr.
+template <int K>
+H12_DEV void inner_step_1w(const KParams& P, int leg, Base& b, Leg& lg, const float* tau_pd, float h, Forces& fr,
+                           const float* org) {
   const float sg = leg ? -1.f : 1.f;
   float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6], Rk[3][3], pk[3], R[3][3], p[3];
   leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
@@ -1528,7 +1767,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   float fext_knee[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   ImplC ick;      // knee contact linearisation (added to link 3 in pass 2)
   float knee_pz;  // z of the knee contact point (KNEE0 or KNEE1; x = y = 0)
-  if constexpr (!HW) knee_contact<K>(P, sg, Rk, pk, v[3], org, fext_knee, fr.knee, ick, knee_pz);
+  knee_contact<K>(P, sg, Rk, pk, v[3], org, fext_knee, fr.knee, ick, knee_pz);
   // ---- foot: 4 anchored sole spheres on the ankle-roll link; the inertia chain of pass 2 starts at link 5
   int smask = 0;                      // implicit: sole spheres whose stiction spring sticks
   float fu[H12_NFOOT_PTS][3];         // implicit: ground normal at each sole sphere, foot coords
@@ -1558,26 +1797,13 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     lg.cmask = nmask;
     for (int i = 0; i < 6; ++i) pc[i] = -fext[i];
   }
-  // ---- joint torques beyond PD, implicit limit inertias (helper wave: from the state of this step)
+  // ---- joint torques beyond PD, implicit limit inertias
   float tau[NL], dl[NL];
-  PHX(10);
-  if constexpr (HW) {
-    __syncthreads();  // R1
-    PHX(8);
-    float jt[36];
-    get4(help_lds().jt, threadIdx.x, jt, 9);
-    // tq includes the delayed PD (computed by the helper wave); tau_pd receives the PD torque alone
-    for (int k = 0; k < NL; ++k) { tau[k] = jt[k]; dl[k] = jt[6 + k]; tau_pd[k] = jt[28 + k]; }
-    for (int i = 0; i < 6; ++i) fext_knee[i] = jt[12 + i];
-    for (int a = 0; a < 3; ++a) fr.knee[a] += jt[18 + a];
-    ick.beta = jt[21]; ick.gamma = jt[22]; ick.u[0] = jt[23]; ick.u[1] = jt[24]; ick.u[2] = jt[25];
-    knee_pz = jt[26];
-  } else {
+  {
     float tq[NL];
     joint_terms(P, lg, h, tq, dl);
     for (int k = 0; k < NL; ++k) tau[k] = tau_pd[k] + tq[k];
   }
-  PHX(11);
   // ---- pass 2, articulated-inertia chain (leaf -> root)
   float U[NL][6], Dinv[NL], u[NL], Ic[NL][6];
   link_ia<5>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
@@ -1586,34 +1812,10 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
   link_ia<2>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
   link_ia<1>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
   link_ia<0>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
-  // ---- the contact-independent forces: bias forces, self-contact wrenches (helper wave)
-  if constexpr (HW) {  // the inertia chain stays ahead of R2 (else the compiler sinks most of it past the barrier)
-    for (int i = 0; i < 6; ++i) { pin(IA.A[i]); pin(IA.C[i]); }
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) pin(IA.B[i][j]);
-    for (int k = 0; k < NL; ++k)
-      for (int i = 0; i < 6; ++i) pin(Ic[k][i]);
-  }
-  PHX(12);
   float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float pbase[6];  // base body bias force (lane 0; 0 on lane 1)
   AInertia Rg;     // base body inertia (lane 0)
-  if constexpr (HW) {
-    __syncthreads();  // R2
-    PHX(9);
-    float o[44];
-    get4(help_lds().bias, threadIdx.x, o, 11);
-    for (int k = 0; k < NL; ++k)
-      for (int i = 0; i < 6; ++i) pbias[k][i] = o[6 * k + i];
-    for (int i = 0; i < 6; ++i) pbase[i] = o[36 + i];
-    ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
-    if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
-    if (P.self_coll) {
-      float w[12];
-      get4(help_lds().selfw, threadIdx.x, w, 3);
-      for (int i = 0; i < 6; ++i) { wk[i] = w[i]; wf[i] = w[6 + i]; }
-    }
-  } else {
+  {
     leg_bias(v, pbias);
     base_body<K>(P, lg, v0, Rg, pbase);
     if (P.self_coll) {  // pelvis-relative geometry, as the self wave's (subtracted here: one pass 1 in this wave)
@@ -1623,7 +1825,6 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
       self_contacts(P, leg, lg.mud, Rk, pkr, v[3], R, pr, v[5], wk, wf, fs);
     }
   }
-  PHX(13);
   for (int i = 0; i < 6; ++i) fext_knee[i] += wk[i];
   for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
   // ---- pass 2, bias-force chain (leaf -> root)
@@ -1652,14 +1853,7 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     torso_corner(R0, corner);
     float ft[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     bool c;
-    if constexpr (HW) {  // evaluated by the helper wave before R2
-      float t[16];
-      get4(help_lds().torso, threadIdx.x, t, 4);
-      for (int i = 0; i < 6; ++i) ft[i] = t[i];
-      for (int a = 0; a < 3; ++a) fr.torso[a] += t[6 + a];
-      ict.beta = t[9]; ict.gamma = t[10]; ict.u[0] = t[11]; ict.u[1] = t[12]; ict.u[2] = t[13];
-      c = t[14] != 0.f;
-    } else {
+    {
       float dummy[2];
       c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, ft, fr.torso, dummy, false, 1.f, org,
                                                    P.mus, P.mud, ict);
@@ -1714,16 +1908,6 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     }
   }
   // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates
-  if constexpr (HW) {
-    // the step's start pose, velocities and joint angles read back from the helper waves' LDS copy (put_state, the
-    // same floats): their registers die after pass 1 instead of being parked in AGPRs through the ABA passes
-    // (-63 VALU per inner step, +0.9 % env-steps/s, profiles/r4/r4zf_state_reload_ab.txt)
-    float x[20];
-    get4(help_lds().st, threadIdx.x, x, 5);
-    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }
-    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
-    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];
-  }
   if (!P.fix_base) {
     float nd[6];
     for (int i = 0; i < 6; ++i) nd[i] = a0[i] + ag[i];
@@ -1746,15 +1930,240 @@ H12_DEV void inner_step(const KParams& P, int leg, Base& b, Leg& lg, float* tau_
     lg.qd[k] = over ? fminf(lg.qd[k], 0.f) : (under ? fmaxf(lg.qd[k], 0.f) : lg.qd[k]);
     lg.q[k] = fminf(fmaxf(q, lo), hi);
   }
-  if constexpr (HW) {
-    if (more) {
-      put_state(threadIdx.x, b, lg, org);
-      __syncthreads();  // S: the next inner step's state
+}
+
+
+
+// One inner step of step_kernel's PHYSICS wave (round 5): the critical chain only -- the joint sin / cos, the delayed PD
+// and joint terms, the articulated-inertia chain and, after R2, the bias-force chain, the base solve, pass 3 and the
+// integration.  The ABA runs in the AV form (link_ia<AV>): the velocity-product accelerations are in the rigid-body bias
+// forces the helper / contact waves hand over, so this wave needs no link velocities or poses; the sole contacts are
+// the helper wave's (their added inertia, wrench and force arrive at R1), the knee contact the contact wave's.  tau_pd: the
+// delayed-PD torque of the current physics step (computed here at its first inner step from pd, held over it); with
+// `more` the next inner step's state is put to LDS (barrier S).
+template <int K>
+H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const PdIn& pd, int it, float* tau_pd, float h,
+                           Forces& fr, const float* org, bool more H12_BW_PARAM) {
+  PHX_INIT();
+  const float sg = leg ? -1.f : 1.f;
+  HelpLds& H = help_lds();
+  float cs[NL][2];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) fsincos(lg.q[k], &cs[k][1], &cs[k][0]);
+  // ---- joint torques: the delayed PD (held over the physics step), limit penalty, max-velocity damper, damping,
+  // friction loss; implicit limit inertias
+  if (it % P.inner == 0) pd_torque(P, pd, lg, it / P.inner, tau_pd);
+  float tau[NL], dl[NL];
+  {
+    float tq[NL];
+    joint_terms(P, lg, h, tq, dl);
+    for (int k = 0; k < NL; ++k) tau[k] = tau_pd[k] + tq[k];
+  }
+  PHX(10);
+  SYNC_W(1);  // R1: sole contacts (helper), knee contact (contact wave)
+  PHX(8);
+  float fext_knee[6];
+  ImplC ick;
+  float knee_pz;
+  {
+    float jt[16];
+    get4(H.jt, threadIdx.x, jt, 4);
+    for (int i = 0; i < 6; ++i) fext_knee[i] = jt[i];
+    for (int a = 0; a < 3; ++a) fr.knee[a] += jt[6 + a];
+    ick.beta = jt[9]; ick.gamma = jt[10]; ick.u[0] = jt[11]; ick.u[1] = jt[12]; ick.u[2] = jt[13];
+    knee_pz = jt[14];
+  }
+  // ---- pass 2, articulated-inertia chain (leaf -> root), from the foot's rigid inertia + the soles' added inertia
+  AInertia IA;
+  {
+    float x[32], y[32];
+    get4(H.cw1[0], threadIdx.x, x, 8);
+    get4(H.cw1[1], threadIdx.x, y, 8);
+    ai_rigid(IA, h12m::IBAR[5], h12m::MC[5], h12m::M[5]);
+    ai_add(IA, *reinterpret_cast<const AInertia*>(x));
+    ai_add(IA, *reinterpret_cast<const AInertia*>(y));
+    for (int a = 0; a < 3; ++a) fr.foot[a] += x[27 + a] + y[27 + a];
+  }
+  PHX(11);
+  float U[NL][6], Dinv[NL], u[NL], Ic[NL][6];
+  float v[NL][6];  // unused in the AV form
+  link_ia<5, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<4, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<3, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<2, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<1, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  link_ia<0, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
+  // the inertia chain stays ahead of R2 (else the compiler sinks most of it past the barrier)
+  for (int i = 0; i < 6; ++i) { pin(IA.A[i]); pin(IA.C[i]); }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) pin(IA.B[i][j]);
+  PHX(12);
+  SYNC_W(2);  // R2: bias forces (helper: links 0-2 + base; contact wave: links 3-5), torso contact, self wrenches
+  PHX(9);
+  float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float pbase[6];  // base body bias force (lane 0; 0 on lane 1)
+  {
+    float o[24], c[20];
+    get4(H.bias_h, threadIdx.x, o, 6);
+    get4(H.bias_c, threadIdx.x, c, 5);
+    for (int i = 0; i < 6; ++i) {
+      pbias[0][i] = o[i]; pbias[1][i] = o[6 + i]; pbias[2][i] = o[12 + i]; pbase[i] = o[18 + i];
+      pbias[3][i] = c[i]; pbias[4][i] = c[6 + i]; pbias[5][i] = c[12 + i];
     }
+  }
+  AInertia Rg;  // base body inertia (lane 0)
+  ai_rigid(Rg, h12m::BASE_IBAR, h12m::BASE_MC, h12m::BASE_M);
+  if (Feat<K>::ext && P.env_mass) ai_add_point_mass(Rg, lg.dmass, h12m::TORSO_COM);
+  if (P.self_coll) {
+    float w[12];
+    get4(H.selfw, threadIdx.x, w, 3);
+    for (int i = 0; i < 6; ++i) { wk[i] = w[i]; wf[i] = w[6 + i]; }
+  }
+  PHX(13);
+  for (int i = 0; i < 6; ++i) fext_knee[i] += wk[i];
+  for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
+  // ---- pass 2, bias-force chain (leaf -> root)
+  float pAcc[6];
+  {
+    float pa[8], pb[8];
+    get4(&H.cw1[0][5], threadIdx.x, pa, 2);  // floats 20..27 of each half's hand-off: the soles' -wrench at 21..26
+    get4(&H.cw1[1][5], threadIdx.x, pb, 2);
+    for (int i = 0; i < 6; ++i) pAcc[i] = pbias[5][i] + (pa[1 + i] + pb[1 + i]) - wf[i];
+  }
+  link_p<5, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<4, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<3, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<2, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<1, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  link_p<0, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
+  // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
+  IA.A[3] *= sg; IA.A[5] *= sg;  // xy, yz of the angular block (s = (sg,1,sg))
+  IA.C[3] *= sg; IA.C[5] *= sg;  // xy, yz of the linear block (s = (1,sg,1))
+  for (int i = 0; i < 6; ++i) pAcc[i] *= s6(i, sg);
+  // ---- lane 0 adds the base body: rigid inertia, bias force, torso-box contact (helper wave)
+  float R0[3][3];
+  quat_R(b.quat, R0);
+  float ag[6] = {0.f, 0.f, 0.f, -P.g * R0[2][0], -P.g * R0[2][1], -P.g * R0[2][2]};
+  ImplC ict;  // torso contact linearisation (lane 0)
+  float corner[3];
+  ict.beta = ict.gamma = 0.f;
+  if (leg == 0) {
+    ai_add(IA, Rg);
+    for (int i = 0; i < 6; ++i) pAcc[i] += pbase[i];
+    torso_corner(R0, corner);
+    float t[16];
+    get4(H.torso, threadIdx.x, t, 4);
+    for (int a = 0; a < 3; ++a) fr.torso[a] += t[6 + a];
+    ict.beta = t[9]; ict.gamma = t[10]; ict.u[0] = t[11]; ict.u[1] = t[12]; ict.u[2] = t[13];
+    const bool c = t[14] != 0.f;
+    if (c && P.impl) ai_add_contact(IA, corner, ict.u, ict.beta, ict.gamma);
+    for (int i = 0; i < 6; ++i) pAcc[i] -= t[i];
+  }
+  // ---- pair sum in fixed (left + right) order: both lanes hold bit-identical base quantities
+  AInertia IB;
+  float pB[6];
+  {
+    auto comb = [&](float x) {
+      float y = pair_swap(x);
+      return leg ? (y + x) : (x + y);
+    };
+    for (int i = 0; i < 6; ++i) { IB.A[i] = comb(IA.A[i]); IB.C[i] = comb(IA.C[i]); pB[i] = comb(pAcc[i]); }
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) IB.B[i][j] = comb(IA.B[i][j]);
+  }
+  float a0[6];
+  if (P.fix_base) {
+    for (int i = 0; i < 6; ++i) a0[i] = -ag[i];
+  } else {
+    float rhs[6] = {-pB[0], -pB[1], -pB[2], -pB[3], -pB[4], -pB[5]};
+    solve6(IB, rhs, a0);
+  }
+  if (P.impl && leg == 0 && ict.gamma + ict.beta > 0.f) impl_force(a0, corner, ict.u, ict.beta, ict.gamma, fr.torso);
+  // ---- pass 3 (root -> leaf) in the lane frame: a~ (the implicit contact reports use a~ + a^v)
+  float avk[12];
+  get4(H.cw2, threadIdx.x, avk, 3);
+  float a[6];
+  for (int i = 0; i < 6; ++i) a[i] = s6(i, sg) * a0[i];
+  float qdd[NL];
+  link_pass3<0, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<1, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<2, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<3, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  if (P.impl && ick.gamma + ick.beta > 0.f) {  // implicit part of the knee contact force
+    const float pk[3] = {0.f, 0.f, knee_pz};
+    float ah[6];
+    for (int i = 0; i < 6; ++i) ah[i] = a[i] + avk[i];
+    impl_force(ah, pk, ick.u, ick.beta, ick.gamma, fr.knee);
+  }
+  link_pass3<4, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3<5, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  if (P.impl) {  // implicit part of the sole forces (a~ + a^v = the foot's acceleration, shifted frame)
+    float ah[6], r[2][16];
+    for (int i = 0; i < 6; ++i) ah[i] = a[i] + avk[6 + i];
+    get4(&H.cw1[0][7], threadIdx.x, r[0], 4);  // floats 28..43 of each half: the report at 30..
+    get4(&H.cw1[1][7], threadIdx.x, r[1], 4);
+    if constexpr (!Feat<K>::terrain) {
+      SoleSums ss;
+      ss.sb = r[0][2] + r[1][2];
+      ss.sg = r[0][3] + r[1][3];
+      if (ss.sb + ss.sg > 0.f) {
+        for (int i = 0; i < 3; ++i) { ss.pb[i] = r[0][4 + i] + r[1][4 + i]; ss.pg[i] = r[0][7 + i] + r[1][7 + i]; }
+        const float Rf[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {r[0][10], r[0][11], r[0][12]}};
+        sole_impl_force_flat(ah, Rf, ss, fr.foot);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < H12_NFOOT_PTS; ++q) {
+        const float* rh = r[q / 2];
+        const int j = q % 2;
+        const float beta = rh[2 + j], gamma = rh[4 + j];
+        const float uq[3] = {rh[6 + 3 * j], rh[7 + 3 * j], rh[8 + 3 * j]};
+        if (beta + gamma > 0.f) impl_force(ah, h12m::FOOT[q], uq, beta, gamma, fr.foot);
+      }
+    }
+  }
+  // ---- semi-implicit Euler (mj_Euler conventions), base in real coordinates.  The step's start pose, velocities and
+  // joint angles are read back from the helper waves' LDS copy (put_state, the same floats): their registers die
+  // after the sin / cos instead of being parked through the ABA passes
+  {
+    float x[20];
+    get4(H.st, threadIdx.x, x, 5);
+    for (int i = 0; i < 3; ++i) { b.pos[i] = x[i]; b.vlin[i] = x[7 + i]; b.wang[i] = x[10 + i]; }
+    for (int i = 0; i < 4; ++i) b.quat[i] = x[3 + i];
+    for (int k = 0; k < NL; ++k) lg.q[k] = x[13 + k];
+  }
+  if (!P.fix_base) {
+    float nd[6];
+    for (int i = 0; i < 6; ++i) nd[i] = a0[i] + ag[i];
+    float vb[3];
+    mtv(R0, b.vlin, vb);
+    float wxv[3];
+    cross(b.wang, vb, wxv);
+    float al[3] = {nd[3] + wxv[0], nd[4] + wxv[1], nd[5] + wxv[2]}, aw[3];
+    mv(R0, al, aw);
+    for (int i = 0; i < 3; ++i) { b.vlin[i] += h * aw[i]; b.wang[i] += h * nd[i]; }
+    for (int i = 0; i < 3; ++i) b.pos[i] += h * b.vlin[i];
+    quat_integrate(b.quat, b.wang, h);
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    lg.qd[k] += h * qdd[k];
+    float q = lg.q[k] + h * lg.qd[k];
+    // hard-limit residual (oracle limit_projection): beyond the range by more than lproj -> back to the tolerance,
+    // outward velocity zeroed; branch-free
+    const float hi = h12m::QHI[k] + P.lproj, lo = h12m::QLO[k] - P.lproj;
+    const bool over = q > hi, under = q < lo;
+    lg.qd[k] = over ? fminf(lg.qd[k], 0.f) : (under ? fmaxf(lg.qd[k], 0.f) : lg.qd[k]);
+    lg.q[k] = fminf(fmaxf(q, lo), hi);
+  }
+  if (more) {
+    put_state(threadIdx.x, b, lg, org);
+    SYNC_W(0);  // S: the next inner step's state
   }
   PHX(14);
 }
-
 // ------------------------------------------------------------------ state load / store
 // Workspace access through buffer resources built from the kernargs (wave-uniform): the env's byte offset
 // e*4 is the one per-lane VGPR (voffset), the field offset f*n*4 an SGPR (soffset).  Flat global accesses
@@ -2820,8 +3229,8 @@ H12_DEV void obs_frame_fused(const KParams& P, const EnvSt& s, int leg, int r, b
 }
 
 template <int K>
-__global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
-  if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step, helper_wave, self_wave)
+__global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step_hw, helper_wave, contact_wave, self_wave)
     const int nsteps = P.decimation * P.inner;
     FuseCtx fc = {};
     if (A.fuse) {
@@ -2835,7 +3244,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
                      (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi,
                      fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
-      if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) {
+      {
         __syncthreads();  // L: the physics wave's episode-log values (and CaT constraint values)
         if (Feat<K>::ext && P.cat) {
           // CaT: this block's column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs
@@ -2875,9 +3284,10 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       }
       if (lv) A.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;
     } else {
-      self_wave<K>(P, W.n, nsteps, fc);
+      if (threadIdx.x < 3 * BLOCK) contact_wave<K>(P, W.n, nsteps, fc);
+      else self_wave<K>(P, W.n, nsteps, fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
-      if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) __syncthreads();  // L
+      __syncthreads();  // L (the helper's final sole contact state is in LDS)
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();  // F
@@ -2915,22 +3325,22 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     float fmax_knee = 0.f, fmax_torso = 0.f, fmax_foot = 0.f, flast_foot = 0.f;
     uint32_t cflags = 0;  // foot contact flag of every physics step (ContactSensor replay)
     const float wgt = frcp((float)P.inner);
-    {  // the helper wave computes the delayed PD (pd_torque) from these and each inner step's state
-      PdIn d;
-      for (int k = 0; k < NL; ++k) { d.act[k] = s.act[k]; d.act1[k] = s.act1[k]; d.act2[k] = a_t2[k]; }
-      d.lagpk = (s.lag[0] & 7) | (s.lag[1] & 7) << 3 | (s.lag[2] & 7) << 6;
-      d.since_reset = s.since_reset;
-      put_pd(threadIdx.x, d);
-    }
+    PdIn pd;  // the delayed PD's inputs (pd_torque, once per physics step in inner_step_hw)
+    for (int k = 0; k < NL; ++k) { pd.act[k] = s.act[k]; pd.act1[k] = s.act1[k]; pd.act2[k] = a_t2[k]; }
+    pd.lagpk = (s.lag[0] & 7) | (s.lag[1] & 7) << 3 | (s.lag[2] & 7) << 6;
+    pd.since_reset = s.since_reset;
     put_state(threadIdx.x, s.b, s.lg, s.origin);
-    __syncthreads();  // S: the first inner step's state for the helper wave
+    put_cst(threadIdx.x, s.lg);
+    H12_BW_DECL;
+    SYNC_W(0);  // S: the first inner step's state (and the sole contact state) for the other waves
     for (int st = 0; st < dec; ++st) {
       const bool last = st == dec - 1;
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = s.lg.qd[k];
       Forces fr = {};
       for (int it = 0; it < P.inner; ++it)
-        inner_step<K, true>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin, !last || it < P.inner - 1);
+        inner_step_hw<K>(P, leg, s.b, s.lg, pd, st * P.inner + it, tau, P.h, fr, s.origin,
+                         !last || it < P.inner - 1 H12_BW_ARG);
       if (last)
         for (int k = 0; k < NL; ++k) jacc[k] = (s.lg.qd[k] - jacc[k]) * frcp(P.dt);
       // ContactSensor: net force = mean over the inner steps of the physics step
@@ -2944,6 +3354,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
       }
     }
     PH(1);
+    H12_BW_STORE();
     // ContactSensor._update_buffers_impl replayed per physics step (threshold 1 N, elapsed = dt)
     for (int st = 0; st < dec; ++st) {
       bool is_c = (cflags >> st) & 1u;
@@ -2989,7 +3400,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
     // the same L2 lines: +4.2 us per step).  In this wave the wave-reduced atomics cost a resetting wave ~0.5 us,
     // and the step time is the slowest wave's.  The assembly kernel that follows folds the partials into log_acc
     // (log_load / log_fold).
-    if (A.log_part || (Feat<K>::ext && P.cat) || A.fuse) {
+    {
       if (A.log_part && leg == 0) {
         float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
         for (int t = 0; t < NT; ++t) L[t][lane_pair] = reset ? s.epsum[t] : 0.f;
@@ -3000,6 +3411,7 @@ __global__ void __launch_bounds__(3 * BLOCK) step_kernel(KParams P, Workspace W,
         L[H12_NREW + 4][lane_pair] = reset ? s.metric[1] : 0.f;
       }
       __syncthreads();  // L: the helper wave sums them into this block's partial slots
+      get_cst(threadIdx.x, s.lg);  // the helper's final stiction anchors / sole contact mask
     }
     PH(4);
     if (reset) {
@@ -3313,7 +3725,7 @@ __global__ void __launch_bounds__(BLOCK) physics_kernel(KParams P, Workspace W, 
       tau[k] = fminf(fmaxf(v, -P.elim[k]), P.elim[k]);
     }
     Forces fr = {};
-    for (int it = 0; it < P.inner; ++it) inner_step<K, false>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin, false);
+    for (int it = 0; it < P.inner; ++it) inner_step_1w<K>(P, leg, s.b, s.lg, tau, P.h, fr, s.origin);
   }
   store_env<K>(P, W, e, leg, s);
 }
@@ -4100,7 +4512,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   hipEvent_t k0, k1;
   timing_events(h, 0, &k0, &k1);
   // every block carries a helper wave and, with self-collision, a self-contact wave (helper_wave, self_wave)
-  LAUNCH_KT(step_kernel, k0, k1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 3 : 2) * BLOCK),
+  LAUNCH_KT(step_kernel, k0, k1, dim3(n_blocks(h)), dim3((h->P.self_coll ? 4 : 3) * BLOCK),
             A.fuse ? sizeof(FuseLds) : 0, st, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
@@ -4298,6 +4710,13 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
   }
   return 0;
 }
+#ifdef H12_PHASE_LIGHT
+int h12env_barrier_waits(unsigned long long* out, int nblocks) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 12 * (size_t)nblocks));
+  return 0;
+}
+#endif
 int h12env_wave_times(unsigned long long* out, int nwaves) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave), sizeof(unsigned long long) * 11 * (size_t)nwaves));
