@@ -1310,6 +1310,26 @@ H12_DEV void get_cst(int l, Leg& lg) {
   for (int q = 0; q < H12_NFOOT_PTS; ++q) { lg.anc[q][0] = x[2 * q]; lg.anc[q][1] = x[2 * q + 1]; }
   lg.cmask = __float_as_int(x[8]) | __float_as_int(x[9]);
 }
+// After the physics loop (round 5): the reward terms' inputs beyond the final state (put_state) for the helper wave,
+// which computes the rewards while the physics wave resets and observes; in the second sole hand-off array (free
+// once the last inner step's physics wave has read it)
+struct RewIn {
+  float act[NL], act1[NL], tau[NL], jacc[NL], cmd[3], air, con, fmax_foot, metric[2];
+  int term, tout;
+};
+H12_DEV void put_rin(int l, const RewIn& r) {
+  static_assert(sizeof(RewIn) <= 36 * sizeof(float), "reward inputs fit 9 float4");
+  float x[36];
+  const float* f = reinterpret_cast<const float*>(&r);
+  for (int i = 0; i < 36; ++i) x[i] = i < (int)(sizeof(RewIn) / sizeof(float)) ? f[i] : 0.f;
+  put4(help_lds().cw1[1], l, x, 9);
+}
+H12_DEV void get_rin(int l, RewIn& r) {
+  float x[36];
+  get4(help_lds().cw1[1], l, x, 9);
+  float* f = reinterpret_cast<float*>(&r);
+  for (int i = 0; i < (int)(sizeof(RewIn) / sizeof(float)); ++i) f[i] = x[i];
+}
 // the owner of sole spheres Q0, Q0 + 1 hands their final anchors and contact bits back (field-major rows: the two
 // owners write disjoint floats)
 template <int Q0>
@@ -2237,7 +2257,34 @@ H12_DEV void load_phys(const KParams& P, const Workspace& W, int e, int leg, Env
 }
 
 // MDP part of the state (loaded after the physics loop)
+// the episode reward sums of an env (step_kernel: the helper wave's, which computes the rewards)
 template <int K>
+H12_DEV void load_epsum(const KParams& P, const Workspace& W, int e, float* epsum) {
+  for (int t = 0; t < H12_NREW_FLAT; ++t) epsum[t] = ldf(W, H12_F_EPSUM + t, e);
+  for (int t = H12_NREW_FLAT; t < H12_NREW; ++t)
+    epsum[t] = (Feat<K>::ext && P.rsl) ? ldf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e) : 0.f;
+}
+// ... stored by the two lanes of the env (field t from the left lane, t + 6 from the right: one instruction per pair)
+template <int K>
+H12_DEV void store_epsum(const KParams& P, const Workspace& W0, int e, int leg, const float* epsum) {
+  Workspace W = W0;
+  asm volatile("" : "+s"(W.n));
+  const uint32_t lm = 0u - (uint32_t)leg;
+  auto lsel = [lm](float a, float b) {
+    const uint32_t ua = __float_as_uint(a);
+    return __uint_as_float(ua ^ ((ua ^ __float_as_uint(b)) & lm));
+  };
+#pragma unroll
+  for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(epsum[t], epsum[t + 6]), 6 * leg);
+  if (Feat<K>::ext && P.rsl) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      stf(W, H12_F_EPSUM2 + t, e, lsel(epsum[H12_NREW_FLAT + t], epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+  }
+}
+
+// EPS: with the episode reward sums (step_kernel's physics wave leaves them to the helper wave)
+template <int K, bool EPS = true>
 H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvSt& s) {
   for (int i = 0; i < 3; ++i) s.cmd[i] = ldf(W, H12_F_CMD + i, e);
   s.heading = ldf(W, H12_F_HEADING, e);
@@ -2246,9 +2293,9 @@ H12_DEV void load_mdp(const KParams& P, const Workspace& W, int e, int leg, EnvS
   s.con = ldf(W, H12_F_CONTACT, e, leg);
   s.last_air = ldf(W, H12_F_LAST_AIR, e, leg);
   s.last_con = ldf(W, H12_F_LAST_CONTACT, e, leg);
-  for (int t = 0; t < H12_NREW_FLAT; ++t) s.epsum[t] = ldf(W, H12_F_EPSUM + t, e);
-  for (int t = H12_NREW_FLAT; t < H12_NREW; ++t)
-    s.epsum[t] = (Feat<K>::ext && P.rsl) ? ldf(W, H12_F_EPSUM2 + t - H12_NREW_FLAT, e) : 0.f;
+  if (EPS) load_epsum<K>(P, W, e, s.epsum);
+  else
+    for (int t = 0; t < H12_NREW; ++t) s.epsum[t] = 0.f;
   s.push_t = (Feat<K>::ext && P.push) ? ldf(W, H12_F_PUSH_TIME, e) : 0.f;
   s.metric[0] = ldf(W, H12_F_METRIC, e);
   s.metric[1] = ldf(W, H12_F_METRIC + 1, e);
@@ -2268,10 +2315,11 @@ H12_DEV void load_env(const KParams& P, const Workspace& W, int e, int leg, EnvS
   load_mdp<K>(P, W, e, leg, s);
 }
 
-// PARTS: bit 0 the physics state (base pose / velocity, q, qd, stiction anchors), bit 1 everything else
-template <int K, int PARTS = 3>
+// PARTS: bit 0 the physics state (base pose / velocity, q, qd, stiction anchors), bit 1 everything else but the episode
+// reward sums, bit 2 those (step_kernel: the helper wave stores them)
+template <int K, int PARTS = 7>
 H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, const EnvSt& s) {
-  constexpr bool PH_ = PARTS & 1, RE_ = PARTS & 2;
+  constexpr bool PH_ = PARTS & 1, RE_ = PARTS & 2, EP_ = PARTS & 4;
   const float sg = leg ? -1.f : 1.f;
   // an opaque copy of n made here: the field offsets of the stores are then computed here, not shared with the
   // loads at the top of the kernel (68 SGPRs kept live across the physics loop spill to VGPR lanes)
@@ -2306,12 +2354,14 @@ H12_DEV void store_env(const KParams& P, const Workspace& W0, int e, int leg, co
       static_assert(H12_F_HEADING == H12_F_CMD + 3 && H12_F_CMD_TIME == H12_F_CMD + 4, "command fields contiguous");
       stf(W, H12_F_CMD, e, lsel(s.cmd[0], s.heading), 3 * leg);
       stf(W, H12_F_CMD + 1, e, lsel(s.cmd[1], s.cmd_time), 3 * leg);
+      if (EP_) {
 #pragma unroll
-      for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(s.epsum[t], s.epsum[t + 6]), 6 * leg);
-      if (Feat<K>::ext && P.rsl) {
+        for (int t = 0; t < 6; ++t) stf(W, H12_F_EPSUM + t, e, lsel(s.epsum[t], s.epsum[t + 6]), 6 * leg);
+        if (Feat<K>::ext && P.rsl) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          stf(W, H12_F_EPSUM2 + t, e, lsel(s.epsum[H12_NREW_FLAT + t], s.epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+          for (int t = 0; t < 4; ++t)
+            stf(W, H12_F_EPSUM2 + t, e, lsel(s.epsum[H12_NREW_FLAT + t], s.epsum[H12_NREW_FLAT + t + 4]), 4 * leg);
+        }
       }
       if (leg == 0) {
         stf(W, H12_F_CMD + 2, e, s.cmd[2]);
@@ -3240,12 +3290,16 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     }
     const int ft = threadIdx.x - BLOCK, fnt = blockDim.x - BLOCK;  // lane among the helper waves
     if (threadIdx.x < 2 * BLOCK) {
-      helper_wave<K>(P, W.n, nsteps,
-                     (uint32_t)(A.env_offset + step_block() * ENVS_PER_BLOCK + ((threadIdx.x - BLOCK) >> 1)), A.lo, A.hi,
-                     fc);
+      const int hl = threadIdx.x - BLOCK, hleg = hl & 1;
+      const int he = step_block() * ENVS_PER_BLOCK + (hl >> 1);
+      // the episode reward sums: this wave computes the rewards after the physics loop (round 5); loaded here, their
+      // memory round trip overlaps the loop
+      float ep[H12_NREW];
+      if (he < W.n) load_epsum<K>(P, W, he, ep);
+      helper_wave<K>(P, W.n, nsteps, (uint32_t)(A.env_offset + he), A.lo, A.hi, fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
       {
-        __syncthreads();  // L: the physics wave's episode-log values (and CaT constraint values)
+        __syncthreads();  // L: the final state and the reward inputs (and CaT constraint values)
         if (Feat<K>::ext && P.cat) {
           // CaT: this block's column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs
           // only), one value per column and block -- cat_reduce_kernel folds the blocks
@@ -3265,12 +3319,57 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
           }
         }
       }
+      // ---- rewards on the pre-reset state (mdp_terms: the 12 Flat / 20 extended terms), the episode sums, the reward
+      // output and the episode-log values of the resetting envs -- the physics wave's until round 4: it resets and
+      // observes meanwhile (light stamps: sensor + rewards were ~1.0 us of its post-loop 3.7 us)
+      constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+      if (he < W.n) {
+        EnvSt rs;
+        float org[3];
+        RewIn ri;
+        get_state(hl, rs.b, rs.lg, org);
+        get_rin(hl, ri);
+        for (int k = 0; k < NL; ++k) { rs.act[k] = ri.act[k]; rs.act1[k] = ri.act1[k]; }
+        for (int a = 0; a < 3; ++a) rs.cmd[a] = ri.cmd[a];
+        rs.air = ri.air;
+        rs.con = ri.con;
+        float R[3][3];
+        quat_R(rs.b.quat, R);
+        float terms[H12_NREW];
+        mdp_terms<K>(P, rs, hleg, R, ri.tau, ri.jacc, ri.fmax_foot, ri.term, terms);
+        float r = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float v = terms[t] * P.rew_w[t] * P.step_dt;
+          r += v;
+          ep[t] += v;
+        }
+        const bool reset = ri.term || ri.tout;
+        if (hleg == 0) A.rew[he] = r;
+        // episode log: the resetting envs' sums go to LDS and lane v below adds value v over the block into this block's
+        // own partial slot (value-major [LOG_NPART][blocks]; one shared accumulator made every wave's atomics queue on
+        // the same L2 lines: +4.2 us per step).  The assembly kernel that follows folds the partials into log_acc
+        // (log_load / log_fold).
+        if (A.log_part && hleg == 0) {
+          float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
+          const int j = hl >> 1;
+          for (int t = 0; t < NT; ++t) L[t][j] = reset ? ep[t] : 0.f;
+          L[H12_NREW][j] = reset ? 1.f : 0.f;
+          L[H12_NREW + 1][j] = (reset && ri.tout) ? 1.f : 0.f;
+          L[H12_NREW + 2][j] = (reset && ri.term) ? 1.f : 0.f;
+          L[H12_NREW + 3][j] = reset ? ri.metric[0] : 0.f;  // CommandTerm.reset: metrics of the ended episode
+          L[H12_NREW + 4][j] = reset ? ri.metric[1] : 0.f;
+        }
+        if (reset)
+          for (int t = 0; t < H12_NREW; ++t) ep[t] = 0.f;  // _reset_idx: the episode sums restart
+        store_epsum<K>(P, W, he, hleg, ep);
+      }
+      wave_sync();  // the episode-log values of this wave's lanes
       // lane v: value v summed over the block's envs, stored into this block's partial slot (value-major
       // [LOG_NPART][blocks]: each block owns its slots, so a plain store of every used value, zeros included); on
       // the fused path after the rows, off barrier F's path
       float lacc = 0.f;
       const int v = threadIdx.x - BLOCK;
-      constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
       const bool lv = A.log_part && v < LOG_NSTEP && (v < NT || v >= H12_NREW);
       if (lv) {
         const int ne = min(ENVS_PER_BLOCK, W.n - step_block() * ENVS_PER_BLOCK);
@@ -3309,8 +3408,9 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
   if (active) {
     EnvSt s;
     load_phys<K>(P, W, e, leg, s);
-    // the MDP part of the state is loaded here too: its memory round trip overlaps the physics loop
-    load_mdp<K>(P, W, e, leg, s);
+    // the MDP part of the state is loaded here too: its memory round trip overlaps the physics loop (the episode sums:
+    // the helper wave's)
+    load_mdp<K, false>(P, W, e, leg, s);
     PH(0);
     // ActionManager.process_action: prev <- action, action <- a ; a_{t-2} kept for the delay ring
     float a_t2[NL];
@@ -3371,48 +3471,34 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     const bool tout = s.eplen >= P.max_len;
     int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
     const int term = ill | pair_swap_i(ill);
-    // ---- rewards on the pre-reset state
-    float R[3][3];
-    quat_R(s.b.quat, R);
-    float terms[H12_NREW];
-    mdp_terms<K>(P, s, leg, R, tau, jacc, fmax_foot, term, terms);
-    constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
-    float r = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float v = terms[t] * P.rew_w[t] * P.step_dt;
-      r += v;
-      s.epsum[t] += v;
+    // ---- rewards on the pre-reset state: the helper wave's (round 5), while this wave resets and observes -- the final
+    // state and the terms' other inputs to LDS
+    put_state(threadIdx.x, s.b, s.lg, s.origin);
+    {
+      RewIn ri;
+      for (int k = 0; k < NL; ++k) { ri.act[k] = s.act[k]; ri.act1[k] = s.act1[k]; ri.tau[k] = tau[k]; ri.jacc[k] = jacc[k]; }
+      for (int a = 0; a < 3; ++a) ri.cmd[a] = s.cmd[a];
+      ri.air = s.air; ri.con = s.con; ri.fmax_foot = fmax_foot;
+      ri.metric[0] = s.metric[0]; ri.metric[1] = s.metric[1];
+      ri.term = term; ri.tout = tout ? 1 : 0;
+      put_rin(threadIdx.x, ri);
     }
-    if (Feat<K>::ext && P.cat) cat_constraints<true>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
+    if (Feat<K>::ext && P.cat) {
+      float R[3][3];
+      quat_R(s.b.quat, R);
+      cat_constraints<true>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
+    }
     PH(3);
     const bool reset = term || tout;
     if (leg == 0) {
-      A.rew[e] = r;
       A.term[e] = (uint8_t)term;
       A.trunc[e] = (uint8_t)tout;
     }
     if (A.applied_torque)
       for (int k = 0; k < NL; ++k) A.applied_torque[(size_t)e * NJ + NL * leg + k] = jsign(k, sg) * tau[k];
     if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;
-    // ---- episode log: the resetting envs' sums go to LDS and the helper wave adds them into this block's own
-    // partial slots (value-major [LOG_NPART][blocks]; one shared accumulator made every wave's atomics queue on
-    // the same L2 lines: +4.2 us per step).  In this wave the wave-reduced atomics cost a resetting wave ~0.5 us,
-    // and the step time is the slowest wave's.  The assembly kernel that follows folds the partials into log_acc
-    // (log_load / log_fold).
-    {
-      if (A.log_part && leg == 0) {
-        float(&L)[LOG_NSTEP][ENVS_PER_BLOCK] = help_lds().logv;
-        for (int t = 0; t < NT; ++t) L[t][lane_pair] = reset ? s.epsum[t] : 0.f;
-        L[H12_NREW][lane_pair] = reset ? 1.f : 0.f;
-        L[H12_NREW + 1][lane_pair] = (reset && tout) ? 1.f : 0.f;
-        L[H12_NREW + 2][lane_pair] = (reset && term) ? 1.f : 0.f;
-        L[H12_NREW + 3][lane_pair] = reset ? s.metric[0] : 0.f;  // CommandTerm.reset: metrics of the ended episode
-        L[H12_NREW + 4][lane_pair] = reset ? s.metric[1] : 0.f;
-      }
-      __syncthreads();  // L: the helper wave sums them into this block's partial slots
-      get_cst(threadIdx.x, s.lg);  // the helper's final stiction anchors / sole contact mask
-    }
+    __syncthreads();  // L: the helper wave computes the rewards, the episode sums and the episode-log values
+    get_cst(threadIdx.x, s.lg);  // the helper / contact waves' final stiction anchors and sole contact masks
     PH(4);
     if (reset) {
       uint32_t pre[16];
@@ -3447,7 +3533,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       obs_frame<K>(P, s, leg, e, W.n, A.frame);
     }
     PH(6);
-    store_env<K>(P, W, e, leg, s);
+    store_env<K, 3>(P, W, e, leg, s);  // the episode sums are the helper wave's
     PH(7);
     PH_WAVE_END();
   }
