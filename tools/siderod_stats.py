@@ -54,14 +54,19 @@ def main():
     front = np.array([rods[2][1], rods[3][1]])                                           # side rods' front ends
     assert np.allclose(front[:, 0], 0.132, atol=1e-6) and np.allclose(np.abs(front[:, 1]), 0.038, atol=1e-6)
     fields = [F[k] for k in ("POS", "QUAT", "VLIN", "WANG", "Q", "QD")]
-    stats = dict(foot_steps=0, sphere_contact=0, front_pen=0, front_only=0, front_deepest=0)
+    stats = dict(foot_steps=0, sphere_contact=0, front_pen=0, front_only=0, front_deepest=0, first_contacts=0,
+                 first_contacts_preceded_by_front_only=0)
     dfront, vfront_only, dsph_when_front = [], [], []
-    prev = None
+    slide_build = 0.0  # sum over modelled-contact foot-steps of the foot origin's horizontal speed
+    prev = prev_foot = None
+    prev_state = None  # per env and foot: 0 no contact, 1 front end only, 2 modelled contact
     for t in range(a.steps):
         env.step(rng.normal(size=(n, 12)).astype(np.float32), t + 1)
         X = np.concatenate([env.F[o:o + k] for o, k in fields]).T.astype(np.float64)
         poses = [O.body_poses(m, X[i]) for i in range(n)]
         cur = np.array([[(R[b] @ front.T).T + p[b] for b in (6, 12)] for R, p in poses])  # (n, 2, 2, 3)
+        foot = np.array([[p[b] for b in (6, 12)] for R, p in poses])                      # (n, 2, 3)
+        state = np.zeros((n, 2), np.int8)
         if t >= 50:
             for i, (R, p) in enumerate(poses):
                 for f, b in enumerate((6, 12)):
@@ -71,6 +76,12 @@ def main():
                     stats["foot_steps"] += 1
                     sc = bool((ds > 0).any())
                     stats["sphere_contact"] += sc
+                    state[i, f] = 2 if sc else (1 if (df > 0).any() else 0)
+                    if sc and prev_foot is not None:
+                        slide_build += float(np.linalg.norm(foot[i, f, :2] - prev_foot[i, f, :2]) / 0.02)
+                    if sc and prev_state is not None and prev_state[i, f] != 2:
+                        stats["first_contacts"] += 1
+                        stats["first_contacts_preceded_by_front_only"] += int(prev_state[i, f] == 1)
                     if (df > 0).any():
                         stats["front_pen"] += 1
                         dfront.append(float(df.max()))
@@ -82,8 +93,10 @@ def main():
                                 vfront_only.append(float(np.linalg.norm(cur[i, f, k, :2] - prev[i, f, k, :2]) / 0.02))
                         if df.max() > ds.max():
                             stats["front_deepest"] += 1
-        prev = cur
+        prev, prev_foot = cur, foot
+        prev_state = state if t >= 50 else None
     fs = max(1, stats["foot_steps"])
+    env_steps = fs / 2
     q = lambda x, p: float(np.quantile(np.array(x), p)) if x else None  # noqa: E731
     res = {"envs": n, "steps": a.steps, "window": f"env steps 51..{a.steps} (sampled once per env step), N(0,1) random "
                                                   "actions, Flat task (the bench workload), CPU oracle",
@@ -97,7 +110,17 @@ def main():
            "front_end_depth_m": {"p50": q(dfront, 0.5), "p95": q(dfront, 0.95), "max": max(dfront) if dfront else None},
            "deepest_modelled_sphere_depth_when_front_penetrates_m": {"p50": q(dsph_when_front, 0.5)},
            "front_only_horizontal_speed_m_per_s": {"p50": q(vfront_only, 0.5), "p95": q(vfront_only, 0.95),
-                                                   "n": len(vfront_only)}}
+                                                   "n": len(vfront_only)},
+           # feet_slide (weight -0.25, x step_dt 0.02; V/mdp/rewards.py feet_slide, C12 flat cfg): the contribution the
+           # build misses in front-end-only contacts (the front end's speed standing in for the foot body's), against the
+           # build's own (the foot origin's speed in its modelled-contact foot-steps); per env-step
+           "feet_slide_per_env_step": {"build": -0.25 * 0.02 * slide_build / env_steps,
+                                       "missed_front_only": -0.25 * 0.02 * float(np.sum(vfront_only)) / env_steps},
+           # feet_air_time: a foot's first contact (ContactSensor first_contact) that the reference's side rod would have
+           # made one or more env steps earlier (its front end alone touching in the preceding sample)
+           "air_time_first_contacts": {"n": stats["first_contacts"],
+                                       "preceded_by_front_only": stats["first_contacts_preceded_by_front_only"],
+                                       "fraction": stats["first_contacts_preceded_by_front_only"] / max(1, stats["first_contacts"])}}
     s = json.dumps(res, indent=1)
     print(s)
     if a.out:
