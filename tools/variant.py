@@ -73,7 +73,13 @@ PATCHES = {
                "  const int e = (threadIdx.x >> 1) < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1) "
                ": 0x3fffffff;", 2)],
 }
-PATCHES_HEAD: dict = {}
+PATCHES_HEAD: dict = {
+    # the helper waves' shifted-row stores with the default (write-back) policy instead of nt: the newest-slot floats
+    # written after barrier F then merge into the L2 lines of their rows (round 4's +1.29 MB of partial-line writes)
+    "rows_wb": [("""                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
+                                         ST_POL);""", """                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
+                                         0);""")],
+}
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
