@@ -1070,9 +1070,26 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   const uint64_t live = __ballot(1);
   const int nlive = __popcll(live);
   const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-  const int njobs = 25 * __popcll(act);
+  const int ncand = __popcll(act);
+  // foot-foot fast path (round 5): when every candidate env of the wave has only its feet' bounds near (the common
+  // case), its 16 rod-rod jobs alone are enumerated -- 4 envs per pass of 64 lanes instead of 2 of 25 jobs; the
+  // blocks with several candidate envs set the step's tail (light stamps: without self-collision p95 / max of the
+  // physics loop 22.2 / 23.6 us against 24.2 / 26.7)
+  const int lf = me < ncand ? L.flags[me] : 0;
+  const bool ffonly = __ballot(me < ncand && (lf & 7) != 0) == 0;
+  const int njobs = (ffonly ? 16 : 25) * ncand;
   for (int jb = me; jb < njobs; jb += nlive) {
-    const int rank = jb / 25, k = jb - 25 * rank, i = k / 5, j = k - 5 * i;
+    int rank, i, j;
+    if (ffonly) {
+      rank = jb >> 4;
+      i = 1 + ((jb >> 2) & 3);
+      j = 1 + (jb & 3);
+    } else {
+      rank = jb / 25;
+      const int k = jb - 25 * rank;
+      i = k / 5;
+      j = k - 5 * i;
+    }
     const int e = L.slot[rank], fl = L.flags[rank];
     if (!((fl >> (2 * (i > 0) + (j > 0))) & 1)) continue;
     const float4* gl = L.geo[e][0];
