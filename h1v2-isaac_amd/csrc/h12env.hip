@@ -155,12 +155,12 @@ __device__ unsigned long long g_wave[1024][11];
 #define PHX(i) (void)0
 #endif
 // experiment builds only (-DH12_PHASE_PROFILE -DH12_PHASE_LIGHT): the shader-clock cycles each wave of step_kernel waits
-// in the inner steps' barriers S / R1 / R2, accumulated in registers and stored once per wave ([block][role][barrier];
+// in the inner steps' barriers S / R1 / R2 (and separately the first S, index 3), accumulated in registers and stored once per wave ([block][role][barrier];
 // roles 0 physics, 1 helper, 2 contact, 3 self): the wave that waits ~0 at a barrier is the one the block waited for
 #if defined(H12_PHASE_PROFILE) && defined(H12_PHASE_LIGHT)
-__device__ unsigned long long g_bw[1024][4][3];
-#define H12_BW_DECL unsigned long long _bw[3] = {0ull, 0ull, 0ull}
-#define H12_BW_PARAM , unsigned long long (&_bw)[3]
+__device__ unsigned long long g_bw[1024][4][4];
+#define H12_BW_DECL unsigned long long _bw[4] = {0ull, 0ull, 0ull, 0ull}
+#define H12_BW_PARAM , unsigned long long (&_bw)[4]
 #define H12_BW_ARG , _bw
 #define SYNC_W(k)                                                                \
   do {                                                                           \
@@ -171,7 +171,7 @@ __device__ unsigned long long g_bw[1024][4][3];
 #define H12_BW_STORE()                                                           \
   do {                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
-      for (int _k = 0; _k < 3; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k]; \
+      for (int _k = 0; _k < 4; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k]; \
   } while (0)
 #else
 #define H12_BW_DECL (void)0
@@ -565,6 +565,19 @@ H12_DEV void bias(const float* v, float* p) {
 }
 
 // ---- ABA pass 1 for leg link LINK: spatial velocity v[LINK] from the parent's vp, world pose
+// the spatial velocity alone
+template <int LINK>
+H12_DEV void link_vel(const Leg& lg, const float (&cs)[NL][2], const float* vp, float (&v)[NL][6]) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  const float c = cs[LINK][0], s = cs[LINK][1];
+  float t[3];
+  cross(r, vp, t);
+  float lin[3] = {vp[3] - t[0], vp[4] - t[1], vp[5] - t[2]};
+  rotT<A>(c, s, vp, v[LINK]);
+  rotT<A>(c, s, lin, v[LINK] + 3);
+  v[LINK][A] += lg.qd[LINK];
+}
 template <int LINK>
 H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, float (&v)[NL][6], float (&R)[3][3],
                         float* p) {
@@ -574,12 +587,7 @@ H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, floa
   fsincos(lg.q[LINK], &s, &c);
   cs[LINK][0] = c;
   cs[LINK][1] = s;
-  float t[3];
-  cross(r, vp, t);
-  float lin[3] = {vp[3] - t[0], vp[4] - t[1], vp[5] - t[2]};
-  rotT<A>(c, s, vp, v[LINK]);
-  rotT<A>(c, s, lin, v[LINK] + 3);
-  v[LINK][A] += lg.qd[LINK];
+  link_vel<LINK>(lg, cs, vp, v);
   float Rr[3];
   mv(R, r, Rr);
   p[0] += Rr[0]; p[1] += Rr[1]; p[2] += Rr[2];
@@ -599,27 +607,37 @@ H12_DEV void link_pass1(const Leg& lg, float (&cs)[NL][2], const float* vp, floa
 // link_av; computed by the helper / contact waves), so the articulated-body recursion runs with c = 0: no Ic = Ia c
 // here, no c in link_p / link_pass3 (exact algebra: the accelerations a~ = a - a^v obey a~_i = X_i a~_parent + S qdd_i;
 // DESIGN.md section 2)
-template <int LINK, bool AV = false>
+// AV: U kept as (angular, linear) pairs U[LINK][k] = (U_k, U_3+k) (f32x2 [NL][3]) for the packed link_p_pk /
+// link_pass3_pk; otherwise float [NL][6]
+template <int LINK, bool AV = false, typename UT>
 H12_DEV void link_ia(const KParams& P, const Leg& lg, const float (&cs)[NL][2], const float (&v)[NL][6],
-                     const ImplC& ick, float knee_pz, const float* dl, AInertia& IA, float (&U)[NL][6],
+                     const ImplC& ick, float knee_pz, const float* dl, AInertia& IA, UT& U,
                      float (&Dinv)[NL], float (&Ic)[NL][6], float h) {
   constexpr int A = AX[LINK];
   float Ua[3] = {sget(IA.A, 0, A), sget(IA.A, 1, A), sget(IA.A, 2, A)};
   float Ul[3] = {IA.B[A][0], IA.B[A][1], IA.B[A][2]};
   float D = IA.A[A] + h12m::ARM[LINK] + h * P.dimpl[LINK] + dl[LINK];
   float di = frcp(D);
-  U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
-  U[LINK][3] = Ul[0]; U[LINK][4] = Ul[1]; U[LINK][5] = Ul[2];
   Dinv[LINK] = di;
-  // Ia = IA - U U^T / D
-  float Uad[3] = {Ua[0] * di, Ua[1] * di, Ua[2] * di};
-  float Uld[3] = {Ul[0] * di, Ul[1] * di, Ul[2] * di};
-  IA.A[0] -= Ua[0] * Uad[0]; IA.A[1] -= Ua[1] * Uad[1]; IA.A[2] -= Ua[2] * Uad[2];
-  IA.A[3] -= Ua[0] * Uad[1]; IA.A[4] -= Ua[0] * Uad[2]; IA.A[5] -= Ua[1] * Uad[2];
-  IA.C[0] -= Ul[0] * Uld[0]; IA.C[1] -= Ul[1] * Uld[1]; IA.C[2] -= Ul[2] * Uld[2];
-  IA.C[3] -= Ul[0] * Uld[1]; IA.C[4] -= Ul[0] * Uld[2]; IA.C[5] -= Ul[1] * Uld[2];
+  // Ia = IA - U U^T / D; the A and C blocks share the index pattern: packed (A, C) pairs
+  const f32x2 u2[3] = {pk2(Ua[0], Ul[0]), pk2(Ua[1], Ul[1]), pk2(Ua[2], Ul[2])};
+  if constexpr (AV) {
+    U[LINK][0] = u2[0]; U[LINK][1] = u2[1]; U[LINK][2] = u2[2];
+  } else {
+    U[LINK][0] = Ua[0]; U[LINK][1] = Ua[1]; U[LINK][2] = Ua[2];
+    U[LINK][3] = Ul[0]; U[LINK][4] = Ul[1]; U[LINK][5] = Ul[2];
+  }
+  const f32x2 ud2[3] = {u2[0] * di, u2[1] * di, u2[2] * di};
+  constexpr int SI[6] = {0, 1, 2, 0, 0, 1}, SJ[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    f32x2 ac = pk2(IA.A[k], IA.C[k]);
+    ac -= u2[SI[k]] * ud2[SJ[k]];
+    IA.A[k] = ac.x;
+    IA.C[k] = ac.y;
+  }
   for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * Uld[j];
+    for (int j = 0; j < 3; ++j) IA.B[i][j] -= Ua[i] * ud2[j].y;
   if constexpr (!AV) {
     float cb[6];
     vprod<A>(v[LINK], lg.qd[LINK], cb);
@@ -664,6 +682,53 @@ H12_DEV void link_p(const float (&cs)[NL][2], const float (&U)[NL][6], const flo
     if constexpr (LINK - 1 == 3)
       for (int i = 0; i < 6; ++i) pAcc[i] -= fext_knee[i];
   }
+}
+
+// rot<A> of (angular, linear) pairs: both halves of a spatial vector turn alike, one packed op per pair of scalar ones
+template <int A>
+H12_DEV void rot_pk(float c, float s, const f32x2* in, f32x2* out) {
+  const f32x2 x = in[0], y = in[1], z = in[2];
+  if constexpr (A == 0) { out[0] = x; out[1] = c * y - s * z; out[2] = s * y + c * z; }
+  else if constexpr (A == 1) { out[0] = c * x + s * z; out[1] = y; out[2] = -s * x + c * z; }
+  else { out[0] = c * x - s * y; out[1] = s * x + c * y; out[2] = z; }
+}
+// link_p of the AV form on (angular, linear) pairs p[k] = (pAcc_k, pAcc_3+k), U as pairs (link_ia<.., true>)
+template <int LINK>
+H12_DEV void link_p_pk(const float (&cs)[NL][2], const f32x2 (&U)[NL][3], const float (&Dinv)[NL], const float* tau,
+                       const f32x2 (&pb)[NL][3], f32x2 (&p)[3], float (&u)[NL]) {
+  constexpr int A = AX[LINK];
+  const float uu = tau[LINK] - p[A].x;
+  u[LINK] = uu;
+  const float ud = uu * Dinv[LINK];
+  f32x2 pa[3], q[3];
+  for (int k = 0; k < 3; ++k) pa[k] = p[k] + U[LINK][k] * ud;
+  rot_pk<A>(cs[LINK][0], cs[LINK][1], pa, q);
+  const float* r = h12m::R[LINK];
+  const float fr[3] = {q[0].y, q[1].y, q[2].y};
+  float rf[3];
+  cross(r, fr, rf);
+  for (int k = 0; k < 3; ++k) p[k] = pk2(q[k].x + rf[k], q[k].y);
+  if constexpr (LINK > 0)
+    for (int k = 0; k < 3; ++k) p[k] += pb[LINK - 1][k];
+}
+// link_pass3 of the AV form on (angular, linear) pairs a[k] = (a_k, a_3+k)
+template <int LINK>
+H12_DEV void link_pass3_pk(const float (&cs)[NL][2], const f32x2 (&U)[NL][3], const float (&Dinv)[NL],
+                           const float (&u)[NL], f32x2 (&a)[3], float* qdd) {
+  constexpr int A = AX[LINK];
+  const float* r = h12m::R[LINK];
+  const float aw[3] = {a[0].x, a[1].x, a[2].x};
+  float t[3];
+  cross(r, aw, t);
+  f32x2 in[3];
+  for (int k = 0; k < 3; ++k) in[k] = pk2(a[k].x, a[k].y - t[k]);
+  rot_pk<A>(cs[LINK][0], -cs[LINK][1], in, a);
+  f32x2 ua = U[LINK][0] * a[0];
+  ua += U[LINK][1] * a[1];
+  ua += U[LINK][2] * a[2];
+  const float x = (u[LINK] - (ua.x + ua.y)) * Dinv[LINK];
+  qdd[LINK] = x;
+  a[A].x += x;
 }
 
 // ---- ABA pass 3 for leg link LINK (root -> leaf)
@@ -967,11 +1032,13 @@ H12_DEV void swap3(const float* a, float* b) { b[0] = pair_swap(a[0]); b[1] = pa
 
 // LDS staging of one wave (block = one wave): per env and leg 16 float4 -- knee segment (2), sole rods (8),
 // knee w / v / origin (3), foot w / v / origin (3), real frame -- and the per-body wrench accumulators
-// (F, moment about the world origin).
+// (F, moment about the world origin).  Field-major ([field][env][leg], lane 2 env + leg): the staging writes and the
+// own-body reads are lane-consecutive (an [env][leg][field] layout put every lane of a ds_write_b128 on the same
+// banks; light stamps: the staging cost the self wave ~0.5 us per inner step)
 constexpr int SG_KNEE = 0, SG_ROD = 2, SG_KKIN = 10, SG_FKIN = 13, SG_N = 16;
 struct SelfLds {
-  float4 geo[ENVS_PER_BLOCK][2][SG_N];
-  float acc[ENVS_PER_BLOCK][2][2][8];  // [env][leg][body: 0 knee, 1 foot][F xyz, pad, m xyz, pad]
+  float4 geo[SG_N][ENVS_PER_BLOCK][2];
+  float acc[2][8][ENVS_PER_BLOCK][2];  // [body: 0 knee, 1 foot][F xyz, pad, m xyz, pad][env][leg]
   int slot[ENVS_PER_BLOCK], flags[ENVS_PER_BLOCK];
 };
 
@@ -994,9 +1061,11 @@ H12_DEV SelfLds& self_lds() {
 // self-contact anywhere in the wave).  Phase 2 (self_finish): the pair jobs and each lane's wrenches.  Rk/pk, vk:
 // knee pose (lane frame) and body velocity, Rf/pf, vf: the foot's.  Pair-uniform control flow at every DPP
 // swap; wave-uniform at every wave_sync.
-H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
-                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
-  SelfLds& L = self_lds();
+// self_broad: the broad phase alone (returns the wave's candidate mask; flags: the env's candidate bits, k01: this
+// leg's knee segment, real frame).  step_kernel's self wave runs it before R1 and the staging (self_stage_geo, which
+// needs the link velocities) after R1 in candidate waves only.
+H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, const float (&Rf)[3][3], const float* pf,
+                            float* k01, int& flags) {
   const float sg = leg ? -1.f : 1.f;
   // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
   float k0[3], k1[3], b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
@@ -1017,35 +1086,40 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&R
   const int f0 = capsules_near(La, Lb, Rk0, Rk1, rl + h12m::KNEE_R) ? 1 : 0;
   const int f1 = capsules_near(La, Lb, Rb0, Rb1, rl + h12m::FB_R) ? 1 : 0;
   const int mine = (f0 | f1 << 1) << (2 * leg);   // bits: 0 kk, 1 kf, 2 fk, 3 ff (left capsule major)
-  const int flags = mine | pair_swap_i(mine);
-  const uint64_t act = __ballot(flags != 0 && leg == 0);
-  if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
-  // ---- stage this leg's capsules and body kinematics (real frame)
+  flags = mine | pair_swap_i(mine);
+  for (int a = 0; a < 3; ++a) { k01[a] = k0[a]; k01[3 + a] = k1[a]; }
+  return __ballot(flags != 0 && leg == 0);
+}
+// the staging of a candidate wave (act != 0, wave-uniform): this leg's capsules and body kinematics (real frame)
+H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const float* k01, const float (&Rk)[3][3],
+                            const float* pk, const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
+  SelfLds& L = self_lds();
+  const float sg = leg ? -1.f : 1.f;
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
   {
-    float4* g = L.geo[el][leg];
-    g[SG_KNEE] = make_float4(k0[0], k0[1], k0[2], mu);  // w: this leg's (sole) dynamic friction coefficient
-    g[SG_KNEE + 1] = make_float4(k1[0], k1[1], k1[2], 0.f);
+    auto g = [&](int f) -> float4& { return L.geo[f][el][leg]; };
+    g(SG_KNEE) = make_float4(k01[0], k01[1], k01[2], mu);  // w: this leg's (sole) dynamic friction coefficient
+    g(SG_KNEE + 1) = make_float4(k01[3], k01[4], k01[5], 0.f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float a0[3], a1[3];
       body_point_real(Rf, pf, h12m::ROD[r][0], sg, a0);
       body_point_real(Rf, pf, h12m::ROD[r][1], sg, a1);
-      g[SG_ROD + 2 * r] = make_float4(a0[0], a0[1], a0[2], 0.f);
-      g[SG_ROD + 2 * r + 1] = make_float4(a1[0], a1[1], a1[2], 0.f);
+      g(SG_ROD + 2 * r) = make_float4(a0[0], a0[1], a0[2], 0.f);
+      g(SG_ROD + 2 * r + 1) = make_float4(a1[0], a1[1], a1[2], 0.f);
     }
     // world angular velocity (a pseudo-vector: w_real = det(M) M w_lane, det M = sg), origin velocity, origin
     float w[3], v[3];
     mv(Rk, vk, w); mv(Rk, vk + 3, v);
-    g[SG_KKIN] = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
-    g[SG_KKIN + 1] = make_float4(v[0], sg * v[1], v[2], 0.f);
-    g[SG_KKIN + 2] = make_float4(pk[0], sg * pk[1], pk[2], 0.f);
+    g(SG_KKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+    g(SG_KKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
+    g(SG_KKIN + 2) = make_float4(pk[0], sg * pk[1], pk[2], 0.f);
     mv(Rf, vf, w); mv(Rf, vf + 3, v);
-    g[SG_FKIN] = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
-    g[SG_FKIN + 1] = make_float4(v[0], sg * v[1], v[2], 0.f);
-    g[SG_FKIN + 2] = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
-    float* ac = L.acc[el][leg][0];
-    for (int i = 0; i < 16; ++i) ac[i] = 0.f;
+    g(SG_FKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+    g(SG_FKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
+    g(SG_FKIN + 2) = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
+    for (int b = 0; b < 2; ++b)
+      for (int a = 0; a < 3; ++a) { L.acc[b][a][el][leg] = 0.f; L.acc[b][4 + a][el][leg] = 0.f; }
     if (leg == 0 && flags) {
       const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
       L.slot[rank] = el;
@@ -1053,6 +1127,14 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&R
     }
   }
   wave_sync();
+}
+H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
+                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
+  float k01[6];
+  int flags;
+  const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags);
+  if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
+  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf);
   return act;
 }
 
@@ -1092,23 +1174,22 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
     }
     const int e = L.slot[rank], fl = L.flags[rank];
     if (!((fl >> (2 * (i > 0) + (j > 0))) & 1)) continue;
-    const float4* gl = L.geo[e][0];
-    const float4* gr = L.geo[e][1];
+    auto gl = [&](int f) -> const float4& { return L.geo[f][e][0]; };
+    auto gr = [&](int f) -> const float4& { return L.geo[f][e][1]; };
     // Coulomb cap: material multiply combine (PhysX friction_combine_mode 'multiply').  With the startup material
     // randomisation (randomize_rigid_body_material, C12/rsl_env_cfg.py:213-223, T/.../cat_env_cfg.py:236) it is
     // the product of the two legs' randomised coefficients, otherwise the fixed 0.6 x 0.6 (self_mu)
-    const float smu = P.env_mu ? gl[SG_KNEE].w * gr[SG_KNEE].w : P.smu;
-    const float4 la = gl[i == 0 ? SG_KNEE : SG_ROD + 2 * (i - 1)], lb = gl[i == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (i - 1) + 1];
-    const float4 ra = gr[j == 0 ? SG_KNEE : SG_ROD + 2 * (j - 1)], rb = gr[j == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (j - 1) + 1];
+    const float smu = P.env_mu ? gl(SG_KNEE).w * gr(SG_KNEE).w : P.smu;
+    const float4 la = gl(i == 0 ? SG_KNEE : SG_ROD + 2 * (i - 1)), lb = gl(i == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (i - 1) + 1);
+    const float4 ra = gr(j == 0 ? SG_KNEE : SG_ROD + 2 * (j - 1)), rb = gr(j == 0 ? SG_KNEE + 1 : SG_ROD + 2 * (j - 1) + 1);
     const float pa[3] = {la.x, la.y, la.z}, pb[3] = {lb.x, lb.y, lb.z}, qa[3] = {ra.x, ra.y, ra.z}, qb[3] = {rb.x, rb.y, rb.z};
     const float rs = (i == 0 ? h12m::KNEE_R : h12m::FOOT_R) + (j == 0 ? h12m::KNEE_R : h12m::FOOT_R);
     SegPts sp;
     seg_points(pa, pb, qa, qb, sp);
-    const float4* kl = gl + (i == 0 ? SG_KKIN : SG_FKIN);
-    const float4* kr = gr + (j == 0 ? SG_KKIN : SG_FKIN);
-    const float4 wl = kl[0], vl = kl[1], ol = kl[2], wr = kr[0], vr_ = kr[1], orr = kr[2];
-    float* al = L.acc[e][0][i > 0];
-    float* ar = L.acc[e][1][j > 0];
+    const int kl = i == 0 ? SG_KKIN : SG_FKIN, kr = j == 0 ? SG_KKIN : SG_FKIN;
+    const float4 wl = gl(kl), vl = gl(kl + 1), ol = gl(kl + 2), wr = gr(kr), vr_ = gr(kr + 1), orr = gr(kr + 2);
+    auto al = [&](int a) -> float& { return L.acc[i > 0][a][e][0]; };
+    auto ar = [&](int a) -> float& { return L.acc[j > 0][a][e][1]; };
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // unrolled: sp's arrays stay in registers
       if (q >= sp.n) break;
@@ -1139,15 +1220,17 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
       float m[3];
       cross(x, F, m);
       for (int a = 0; a < 3; ++a) {
-        atomicAdd(&al[a], F[a]); atomicAdd(&al[4 + a], m[a]);
-        atomicAdd(&ar[a], -F[a]); atomicAdd(&ar[4 + a], -m[a]);
+        atomicAdd(&al(a), F[a]); atomicAdd(&al(4 + a), m[a]);
+        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(4 + a), -m[a]);
       }
     }
   }
   wave_sync();
   // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
   const float ms[3] = {1.f, sg, 1.f};
-  auto own_body = [&](const float* ac, const float* po, const float (&Rb)[3][3], float* w, float* rep) {
+  auto own_body = [&](int b, const float* po, const float (&Rb)[3][3], float* w, float* rep) {
+    float ac[8];
+    for (int a = 0; a < 3; ++a) { ac[a] = L.acc[b][a][el][leg]; ac[4 + a] = L.acc[b][4 + a][el][leg]; }
     const float Fr[3] = {ac[0], ac[1], ac[2]};
     const float por[3] = {po[0], sg * po[1], po[2]};
     float pxF[3];
@@ -1158,8 +1241,8 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
     mtv(Rb, Tl, tb);
     for (int a = 0; a < 3; ++a) { w[a] = tb[a]; w[3 + a] = fb[a]; rep[a] += fb[a]; }
   };
-  own_body(L.acc[el][leg][0], pk, Rk, wk, fr.knee);
-  own_body(L.acc[el][leg][1], pf, Rf, wf, fr.foot);
+  own_body(0, pk, Rk, wk, fr.knee);
+  own_body(1, pf, Rf, wf, fr.foot);
   wave_sync();  // the staging area is rewritten by the next physics step
 }
 
@@ -1281,6 +1364,10 @@ H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
                                   pb[2 + ((cd & 4u) ? 12 : 3)], pb[3 + ((cd & 8u) ? 12 : 3)]));
   }
 }
+// step_kernel's helper threads (its launch: (self_coll ? 4 : 3) x BLOCK).  From the kernel parameters: blockDim.x is a
+// load from the dispatch packet, and its s_waitcnt vmcnt(0) also waited for the episode sums' loads issued before it,
+// ~0.5 us of HBM latency ahead of the first barrier S (light stamps: the helper wave was the block's last there)
+H12_DEV int helper_threads(const KParams& P) { return (P.self_coll ? 3 : 2) * BLOCK; }
 // before the R2 barrier of inner step 1: this wave's LDS-DMA has landed (the other waves' reads follow R2)
 H12_DEV void fuse_drain(const FuseCtx& f, int it) {
   if (f.on && it == 1) __builtin_amdgcn_s_waitcnt(0);
@@ -1453,7 +1540,6 @@ H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, 
   link_pass1<4>(lg, cs, v[3], v, R, p);
   link_pass1<5>(lg, cs, v[4], v, R, p);
 }
-
 // knee capsule contact with the ground: lower end point, evaluated at the knee link pose (Rk / pk / vk)
 template <int K>
 H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], const float* pk, const float* vk,
@@ -1467,6 +1553,20 @@ H12_DEV void knee_contact(const KParams& P, float sg, const float (&Rk)[3][3], c
   float dummy[2];
   contact_sphere<false, Feat<K>::terrain>(P, Rk, pk, vk, pl, h12m::KNEE_R, fext_knee, rep, dummy, false, sg, org, P.mus,
                                           P.mud, ick);
+}
+// where step_kernel evaluates the knee capsule's ground contact with self-collision on: the self-contact wave (true) or
+// the contact wave (false; always without a self wave)
+constexpr bool KNEE_ON_SELF = false;
+// knee_contact into the physics wave's R1 hand-off (H.jt: the external wrench, the report, the linearisation)
+template <int K>
+H12_DEV void knee_handoff(const KParams& P, int l, int leg, const float (&Rk)[3][3], const float* pk, const float* vk,
+                          const float* org, ImplC& ick, float& knee_pz) {
+  float jt[16];
+  for (int i = 0; i < 9; ++i) jt[i] = 0.f;
+  knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, vk, org, jt, jt + 6, ick, knee_pz);
+  jt[9] = ick.beta; jt[10] = ick.gamma; jt[11] = ick.u[0]; jt[12] = ick.u[1]; jt[13] = ick.u[2];
+  jt[14] = knee_pz; jt[15] = 0.f;
+  put4(help_lds().jt, l, jt, 4);
 }
 // Torso box (URDF box collider h12_12dof.urdf:387, welded to the pelvis) on the ground: the lowest corner is the
 // implicit contact (torso_corner, contact_sphere); the other three corners of the lowest face (on terrain only while
@@ -1625,20 +1725,21 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
   // the Philox blocks a reset (ST_RESET 0, 1) or a command resample (ST_CMD 0, 1) of this step would draw: they
-  // depend only on the env id and the step counter, so they are drawn here while the physics wave loads its state
-  // (a resetting wave otherwise spends ~1.5 us on them after the physics loop, and the step time is the slowest
-  // wave's)
-  if (active) {
+  // depend only on the env id and the step counter, so they are drawn during the physics loop (a resetting wave
+  // otherwise spends ~1.5 us on them after the loop, and the step time is the slowest wave's) -- block k after
+  // barrier R2 of inner step k, where this wave waits for the physics wave's bias chain anyway.  Before the first
+  // barrier S (rounds 3-5) their 80 quarter-rate integer multiplies per block made the whole block wait ~1 us for
+  // this wave (light stamps, profiles/r5/)
+  auto draw = [&](int k) {
+    if (!active) return;
     uint32_t r[4];
-    rng(P, g, lo, hi, ST_RESET, 0, r); H.rnd[0][l] = make_uint4(r[0], r[1], r[2], r[3]);
-    rng(P, g, lo, hi, ST_RESET, 1, r); H.rnd[1][l] = make_uint4(r[0], r[1], r[2], r[3]);
-    rng(P, g, lo, hi, ST_CMD, 0, r); H.rnd[2][l] = make_uint4(r[0], r[1], r[2], r[3]);
-    rng(P, g, lo, hi, ST_CMD, 1, r); H.rnd[3][l] = make_uint4(r[0], r[1], r[2], r[3]);
-  }
+    rng(P, g, lo, hi, k < 2 ? ST_RESET : ST_CMD, k & 1, r);
+    H.rnd[k][l] = make_uint4(r[0], r[1], r[2], r[3]);
+  };
   Leg lg;
   H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
-    SYNC_W(0);  // S: the state of this inner step
+    SYNC_W(it ? 0 : 3);  // S: the state of this inner step
     Base b;
     float org[3];
     float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
@@ -1672,8 +1773,10 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
     }
     fuse_drain(fc, it);
     SYNC_W(2);  // R2: bias forces (flat: torso contact)
-    fuse_early(fc, it, n_steps, l, blockDim.x - BLOCK);
+    fuse_early(fc, it, n_steps, l, helper_threads(P));
+    if (it < 4) draw(it);
   }
+  for (int k = n_steps; k < 4; ++k) draw(k);
   H12_BW_STORE();
   if (active) put_cst_half<0>(l, lg);  // the env step's final heel anchors / contact bits (read after L)
 }
@@ -1691,7 +1794,7 @@ H12_DEV void contact_wave(const KParams& P, int n, int n_steps, const FuseCtx& f
   Leg lg;
   H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
-    SYNC_W(0);  // S: the state of this inner step
+    SYNC_W(it ? 0 : 3);  // S: the state of this inner step
     float cs[NL][2], v[NL][6];
     Base b;
     float org[3], R0[3][3], vb[3], pb0[3];
@@ -1703,18 +1806,19 @@ H12_DEV void contact_wave(const KParams& P, int n, int n_steps, const FuseCtx& f
       float Rk[3][3], pk[3], R[3][3], p[3];
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p);
       sole_handoff<K, 2>(P, l, leg ? -1.f : 1.f, lg, R, p, v[5], org);  // the toe spheres
-      float jt[16];
-      for (int i = 0; i < 9; ++i) jt[i] = 0.f;
-      knee_contact<K>(P, leg ? -1.f : 1.f, Rk, pk, v[3], org, jt, jt + 6, ick, knee_pz);
-      jt[9] = ick.beta; jt[10] = ick.gamma; jt[11] = ick.u[0]; jt[12] = ick.u[1]; jt[13] = ick.u[2];
-      jt[14] = knee_pz; jt[15] = 0.f;
-      put4(H.jt, l, jt, 4);
+      if (!(KNEE_ON_SELF && P.self_coll)) knee_handoff<K>(P, l, leg, Rk, pk, v[3], org, ick, knee_pz);
       // torso-box ground contact (the base body; lane 0 of the pair): data-dependent work (a fallen robot's) kept off
       // the physics wave's chain; on terrain before R1, on flat ground after R1
       if constexpr (Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);
     }
     SYNC_W(1);  // R1: the helper's sole contacts
     if (active) {
+      if (KNEE_ON_SELF && P.self_coll) {  // the knee contact's linearisation, from the self wave's hand-off
+        float jt[16];
+        get4(H.jt, l, jt, 4);
+        ick.beta = jt[9]; ick.gamma = jt[10]; ick.u[0] = jt[11]; ick.u[1] = jt[12]; ick.u[2] = jt[13];
+        knee_pz = jt[14];
+      }
       float o[20], av[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, av3[6];
       link_av<0>(lg, cs, v, av);
       link_av<1>(lg, cs, v, av);
@@ -1751,7 +1855,7 @@ H12_DEV void contact_wave(const KParams& P, int n, int n_steps, const FuseCtx& f
     }
     fuse_drain(fc, it);
     SYNC_W(2);  // R2
-    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, blockDim.x - BLOCK);
+    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, helper_threads(P));
   }
   H12_BW_STORE();
   if (active) put_cst_half<2>(l, lg);  // the env step's final toe anchors / contact bits (read after L)
@@ -1765,7 +1869,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
   HelpLds& H = help_lds();
   H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
-    SYNC_W(0);  // S: the state of this inner step
+    SYNC_W(it ? 0 : 3);  // S: the state of this inner step
     float Rk[3][3], pk[3], R[3][3], p[3];
     uint64_t act = 0;
     if (active) {
@@ -1775,7 +1879,19 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       get_state(l, b, lg, org);
       float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
+      // broad phase and, in a candidate wave, the staging (after R1 instead, the staging made this wave the last at R2:
+      // -3 %, profiles/r5/r5p_*)
       act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);
+      if constexpr (KNEE_ON_SELF) {
+        // the knee capsule's ground contact (the contact wave's without a self wave): the knee origin back at the base
+        // position (env-local on terrain, lane frame)
+        float pka[3] = {b.pos[0], b.pos[1], b.pos[2]};
+        if constexpr (Feat<K>::terrain) { pka[0] -= org[0]; pka[1] -= org[1]; pka[2] -= org[2]; }
+        pka[0] += pk[0]; pka[1] = (leg ? -pka[1] : pka[1]) + pk[1]; pka[2] += pk[2];
+        ImplC ick;
+        float knee_pz;
+        knee_handoff<K>(P, l, leg, Rk, pka, v[3], org, ick, knee_pz);
+      }
     }
     SYNC_W(1);  // R1
     if (active) {
@@ -1786,7 +1902,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
     }
     fuse_drain(fc, it);
     SYNC_W(2);  // R2: self-contact wrenches
-    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, blockDim.x - BLOCK);
+    fuse_early(fc, it, n_steps, threadIdx.x - BLOCK, helper_threads(P));
   }
   H12_BW_STORE();
 }
@@ -2022,7 +2138,8 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     for (int a = 0; a < 3; ++a) fr.foot[a] += x[27 + a] + y[27 + a];
   }
   PHX(11);
-  float U[NL][6], Dinv[NL], u[NL], Ic[NL][6];
+  f32x2 U[NL][3];  // (angular, linear) pairs
+  float Dinv[NL], u[NL], Ic[NL][6];
   float v[NL][6];  // unused in the AV form
   link_ia<5, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
   link_ia<4, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);
@@ -2038,6 +2155,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   SYNC_W(2);  // R2: bias forces (helper: links 0-2 + base; contact wave: links 3-5), torso contact, self wrenches
   PHX(9);
   float pbias[NL][6], wk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, wf[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x2 pb[NL][3];  // pbias as (angular, linear) pairs, the knee's external wrench subtracted from link 3's
   float pbase[6];  // base body bias force (lane 0; 0 on lane 1)
   {
     float o[24], c[20];
@@ -2059,20 +2177,27 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   PHX(13);
   for (int i = 0; i < 6; ++i) fext_knee[i] += wk[i];
   for (int a = 0; a < 3; ++a) { fr.knee[a] += wk[3 + a]; fr.foot[a] += wf[3 + a]; }
-  // ---- pass 2, bias-force chain (leaf -> root)
+  for (int j = 0; j < NL; ++j)
+    for (int k = 0; k < 3; ++k)
+      pb[j][k] = j == 3 ? pk2(pbias[j][k] - fext_knee[k], pbias[j][3 + k] - fext_knee[3 + k])
+                        : pk2(pbias[j][k], pbias[j][3 + k]);
+  // ---- pass 2, bias-force chain (leaf -> root), on (angular, linear) pairs
   float pAcc[6];
   {
-    float pa[8], pb[8];
+    float pa[8], pc[8];
     get4(&H.cw1[0][5], threadIdx.x, pa, 2);  // floats 20..27 of each half's hand-off: the soles' -wrench at 21..26
-    get4(&H.cw1[1][5], threadIdx.x, pb, 2);
-    for (int i = 0; i < 6; ++i) pAcc[i] = pbias[5][i] + (pa[1 + i] + pb[1 + i]) - wf[i];
+    get4(&H.cw1[1][5], threadIdx.x, pc, 2);
+    f32x2 p[3];
+    for (int k = 0; k < 3; ++k)
+      p[k] = pk2(pbias[5][k] + (pa[1 + k] + pc[1 + k]) - wf[k], pbias[5][3 + k] + (pa[4 + k] + pc[4 + k]) - wf[3 + k]);
+    link_p_pk<5>(cs, U, Dinv, tau, pb, p, u);
+    link_p_pk<4>(cs, U, Dinv, tau, pb, p, u);
+    link_p_pk<3>(cs, U, Dinv, tau, pb, p, u);
+    link_p_pk<2>(cs, U, Dinv, tau, pb, p, u);
+    link_p_pk<1>(cs, U, Dinv, tau, pb, p, u);
+    link_p_pk<0>(cs, U, Dinv, tau, pb, p, u);
+    for (int k = 0; k < 3; ++k) { pAcc[k] = p[k].x; pAcc[3 + k] = p[k].y; }
   }
-  link_p<5, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
-  link_p<4, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
-  link_p<3, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
-  link_p<2, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
-  link_p<1, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
-  link_p<0, true>(cs, U, Dinv, Ic, tau, pbias, fext_knee, pAcc, u);
   // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) IA.B[i][j] *= s6(i, sg) * s6(3 + j, sg);
@@ -2121,24 +2246,24 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   // ---- pass 3 (root -> leaf) in the lane frame: a~ (the implicit contact reports use a~ + a^v)
   float avk[12];
   get4(H.cw2, threadIdx.x, avk, 3);
-  float a[6];
-  for (int i = 0; i < 6; ++i) a[i] = s6(i, sg) * a0[i];
+  f32x2 ap[3];  // (angular, linear) pairs
+  for (int k = 0; k < 3; ++k) ap[k] = pk2(s6(k, sg) * a0[k], s6(3 + k, sg) * a0[3 + k]);
   float qdd[NL];
-  link_pass3<0, true>(lg, cs, v, U, Dinv, u, a, qdd);
-  link_pass3<1, true>(lg, cs, v, U, Dinv, u, a, qdd);
-  link_pass3<2, true>(lg, cs, v, U, Dinv, u, a, qdd);
-  link_pass3<3, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3_pk<0>(cs, U, Dinv, u, ap, qdd);
+  link_pass3_pk<1>(cs, U, Dinv, u, ap, qdd);
+  link_pass3_pk<2>(cs, U, Dinv, u, ap, qdd);
+  link_pass3_pk<3>(cs, U, Dinv, u, ap, qdd);
   if (P.impl && ick.gamma + ick.beta > 0.f) {  // implicit part of the knee contact force
     const float pk[3] = {0.f, 0.f, knee_pz};
     float ah[6];
-    for (int i = 0; i < 6; ++i) ah[i] = a[i] + avk[i];
+    for (int k = 0; k < 3; ++k) { ah[k] = ap[k].x + avk[k]; ah[3 + k] = ap[k].y + avk[3 + k]; }
     impl_force(ah, pk, ick.u, ick.beta, ick.gamma, fr.knee);
   }
-  link_pass3<4, true>(lg, cs, v, U, Dinv, u, a, qdd);
-  link_pass3<5, true>(lg, cs, v, U, Dinv, u, a, qdd);
+  link_pass3_pk<4>(cs, U, Dinv, u, ap, qdd);
+  link_pass3_pk<5>(cs, U, Dinv, u, ap, qdd);
   if (P.impl) {  // implicit part of the sole forces (a~ + a^v = the foot's acceleration, shifted frame)
     float ah[6], r[2][16];
-    for (int i = 0; i < 6; ++i) ah[i] = a[i] + avk[6 + i];
+    for (int k = 0; k < 3; ++k) { ah[k] = ap[k].x + avk[6 + k]; ah[3 + k] = ap[k].y + avk[9 + k]; }
     get4(&H.cw1[0][7], threadIdx.x, r[0], 4);  // floats 28..43 of each half: the report at 30..
     get4(&H.cw1[1][7], threadIdx.x, r[1], 4);
     if constexpr (!Feat<K>::terrain) {
@@ -3305,7 +3430,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       fc = {A.obs_prev + (size_t)e0 * row, A.obs + (size_t)e0 * row, A.fuse_code, row,
             e0 + ENVS_PER_BLOCK <= W.n && nsteps >= 2};
     }
-    const int ft = threadIdx.x - BLOCK, fnt = blockDim.x - BLOCK;  // lane among the helper waves
+    const int ft = threadIdx.x - BLOCK, fnt = helper_threads(P);  // lane among the helper waves
     if (threadIdx.x < 2 * BLOCK) {
       const int hl = threadIdx.x - BLOCK, hleg = hl & 1;
       const int he = step_block() * ENVS_PER_BLOCK + (hl >> 1);
@@ -3340,6 +3465,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       // output and the episode-log values of the resetting envs -- the physics wave's until round 4: it resets and
       // observes meanwhile (light stamps: sensor + rewards were ~1.0 us of its post-loop 3.7 us)
       constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
+      float r = 0.f;
       if (he < W.n) {
         EnvSt rs;
         float org[3];
@@ -3354,7 +3480,6 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
         quat_R(rs.b.quat, R);
         float terms[H12_NREW];
         mdp_terms<K>(P, rs, hleg, R, ri.tau, ri.jacc, ri.fmax_foot, ri.term, terms);
-        float r = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const float v = terms[t] * P.rew_w[t] * P.step_dt;
@@ -3362,7 +3487,6 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
           ep[t] += v;
         }
         const bool reset = ri.term || ri.tout;
-        if (hleg == 0) A.rew[he] = r;
         // episode log: the resetting envs' sums go to LDS and lane v below adds value v over the block into this block's
         // own partial slot (value-major [LOG_NPART][blocks]; one shared accumulator made every wave's atomics queue on
         // the same L2 lines: +4.2 us per step).  The assembly kernel that follows folds the partials into log_acc
@@ -3379,7 +3503,6 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
         }
         if (reset)
           for (int t = 0; t < H12_NREW; ++t) ep[t] = 0.f;  // _reset_idx: the episode sums restart
-        store_epsum<K>(P, W, he, hleg, ep);
       }
       wave_sync();  // the episode-log values of this wave's lanes
       // lane v: value v summed over the block's envs, stored into this block's partial slot (value-major
@@ -3397,6 +3520,11 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
         __builtin_amdgcn_s_waitcnt(0);  // this wave's shifted-row stores have completed (fuse_late rewrites some)
         __syncthreads();                // F: the physics wave's noisy frames and refill flags
         fuse_late(P, A, fc, W.n, ft, fnt);
+      }
+      // the reward and the episode sums last: their stores issued before barrier F held the vmcnt(0) ahead of it
+      if (he < W.n) {
+        if (hleg == 0) A.rew[he] = r;
+        store_epsum<K>(P, W, he, hleg, ep);
       }
       if (lv) A.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;
     } else {
@@ -3449,7 +3577,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     put_state(threadIdx.x, s.b, s.lg, s.origin);
     put_cst(threadIdx.x, s.lg);
     H12_BW_DECL;
-    SYNC_W(0);  // S: the first inner step's state (and the sole contact state) for the other waves
+    SYNC_W(3);  // S: the first inner step's state (and the sole contact state) for the other waves
     for (int st = 0; st < dec; ++st) {
       const bool last = st == dec - 1;
       if (last)
@@ -4816,7 +4944,7 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 #ifdef H12_PHASE_LIGHT
 int h12env_barrier_waits(unsigned long long* out, int nblocks) {
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 12 * (size_t)nblocks));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 16 * (size_t)nblocks));
   return 0;
 }
 #endif

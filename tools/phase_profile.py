@@ -87,14 +87,14 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
         rows, raw, rsets, clk, bw, ends, light = [], [], [], [], [], [], []
         bws = []
         has_bw = hasattr(lib, "h12env_barrier_waits")
-        bwbuf = (C.c_ulonglong * (12 * waves))()
+        bwbuf = (C.c_ulonglong * (16 * waves))()
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
             lib.h12env_wave_times(wt, waves)
-            if has_bw:  # light build: per block, role (physics, helper, contact, self) and barrier (S, R1, R2)
+            if has_bw:  # light build: per block, role (physics, helper, contact, self) and barrier (S, R1, R2, first S)
                 lib.h12env_barrier_waits(bwbuf, waves)
-                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 3).astype(np.float64) / 2370.0)
+                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 4).astype(np.float64) / 2370.0)
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
@@ -143,9 +143,9 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
                 for grp, sel in (("waves_with_reset", rw), ("waves_without_reset", ~rw)) if sel.any()}
             res["light_phases_us_median"]["fraction_of_waves_with_reset"] = round(float(rw.mean()), 3)
         if bws:  # median over blocks and launches of the us each wave role waited per launch in each barrier kind
-            B = np.concatenate(bws)  # (launches x blocks, 4, 3)
+            B = np.concatenate(bws)  # (launches x blocks, 4, 4)
             res["barrier_wait_us_per_launch_median"] = {
-                role: {bar: round(float(np.median(B[:, r, k])), 3) for k, bar in enumerate(("S", "R1", "R2"))}
+                role: {bar: round(float(np.median(B[:, r, k])), 3) for k, bar in enumerate(("S", "R1", "R2", "S first"))}
                 for r, role in enumerate(("physics", "helper", "contact", "self"))}
         if ends:
             E = np.concatenate(ends) / 100.0  # us from the physics wave's start: physics / helper / self wave ends

@@ -5,6 +5,7 @@ tools/_variants/<tag>/ (with include/ beside it, so the relative includes resolv
 tools/_variants/lib_<tag>.so, loaded with H12ENV_LIB=... by bench.py / tools/phase_profile.py.
 
     python tools/variant.py <tag> [--profile]      # builds the variant named <tag> from PATCHES below
+    python tools/variant.py r5prev@HEAD            # the committed kernel, unpatched (A/B baseline)
 """
 from __future__ import annotations
 
@@ -74,6 +75,9 @@ PATCHES = {
                ": 0x3fffffff;", 2)],
 }
 PATCHES_HEAD: dict = {
+    # the knee capsule's ground contact on the self-contact wave (round 5 experiment: that wave became the last at R1,
+    # -1.5 %, profiles/r5/r5q_*)
+    "knee_self": [("constexpr bool KNEE_ON_SELF = false;", "constexpr bool KNEE_ON_SELF = true;")],
     # the helper waves' shifted-row stores with the default (write-back) policy instead of nt: the newest-slot floats
     # written after barrier F then merge into the L2 lines of their rows (round 4's +1.29 MB of partial-line writes)
     "rows_wb": [("""                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
@@ -94,7 +98,7 @@ def source_at(rev: str | None, rel: str) -> str:
 
 def patched(tag: str) -> tuple[str, str]:
     """(original, patched) h12env.hip of variant tag"""
-    rev, patches = ALL[tag]
+    rev, patches = ALL[tag] if tag in ALL else (tag.split("@", 1)[1] or None, [])
     src = orig = source_at(rev, SOURCES[0])
     for old, new, *cnt in patches:  # (old, new[, expected number of matches, default 1])
         want = cnt[0] if cnt else 1
@@ -107,8 +111,9 @@ def patched(tag: str) -> tuple[str, str]:
 def build(tag: str, profile: bool, isa: bool = False) -> Path:
     from h12env.build import ARCH, hipcc
 
-    rev = ALL[tag][0]
+    rev = ALL[tag][0] if tag in ALL else (tag.split("@", 1)[1] or None)
     _, src = patched(tag)
+    tag = tag.split("@", 1)[0]
     top = ROOT / "tools" / "_variants" / tag
     if top.exists():
         shutil.rmtree(top)
@@ -144,7 +149,8 @@ def build(tag: str, profile: bool, isa: bool = False) -> Path:
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("tag", choices=sorted(ALL))
+    ap.add_argument("tag", help=f"one of {sorted(ALL)}, or <name>@<git revision>: that revision's unpatched "
+                    "sources as tools/_variants/lib_<name>.so (the A/B baseline; <name>@ alone: the working tree's)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--isa", action="store_true", help="print the Flat step kernel's static ISA report")
     a = ap.parse_args()
