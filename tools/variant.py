@@ -75,6 +75,9 @@ PATCHES = {
                ": 0x3fffffff;", 2)],
 }
 PATCHES_HEAD: dict = {
+    # probe: the episode sums loaded after the helper wave's loop (is their load the helper's delay at the first S?)
+    "epsum_late": [("      if (he < W.n) load_epsum<K>(P, W, he, ep);\n      helper_wave<K>(P, W.n, nsteps, (uint32_t)(A.env_offset + he), A.lo, A.hi, fc);",
+                    "      helper_wave<K>(P, W.n, nsteps, (uint32_t)(A.env_offset + he), A.lo, A.hi, fc);\n      if (he < W.n) load_epsum<K>(P, W, he, ep);")],
     # the knee capsule's ground contact on the self-contact wave (round 5 experiment: that wave became the last at R1,
     # -1.5 %, profiles/r5/r5q_*)
     "knee_self": [("constexpr bool KNEE_ON_SELF = false;", "constexpr bool KNEE_ON_SELF = true;")],
