@@ -1038,8 +1038,12 @@ H12_DEV void swap3(const float* a, float* b) { b[0] = pair_swap(a[0]); b[1] = pa
 constexpr int SG_KNEE = 0, SG_ROD = 2, SG_KKIN = 10, SG_FKIN = 13, SG_N = 16;
 struct SelfLds {
   float4 geo[SG_N][ENVS_PER_BLOCK][2];
-  float acc[2][8][ENVS_PER_BLOCK][2];  // [body: 0 knee, 1 foot][F xyz, pad, m xyz, pad][env][leg]
+  // [set: 0 self wave, 1 contact wave (self_jobs_shared)][body: 0 knee, 1 foot][F xyz, m xyz][env][leg]: one set per
+  // wave, summed in fixed order, so the float atomics' order stays deterministic
+  float acc[2][2][6][ENVS_PER_BLOCK][2];
   int slot[ENVS_PER_BLOCK], flags[ENVS_PER_BLOCK];
+  int ncand;  // step_kernel: the candidate envs of this inner step (the contact wave shares the jobs, self_jobs)
+  int done;   // step_kernel: the inner steps whose jobs the contact wave has finished (its release to the self wave)
 };
 
 // LDS hand-off among the lanes of ONE wave (the compiler's lowering of a one-wave block's __syncthreads without
@@ -1119,7 +1123,7 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
     g(SG_FKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
     g(SG_FKIN + 2) = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
     for (int b = 0; b < 2; ++b)
-      for (int a = 0; a < 3; ++a) { L.acc[b][a][el][leg] = 0.f; L.acc[b][4 + a][el][leg] = 0.f; }
+      for (int a = 0; a < 6; ++a) L.acc[0][b][a][el][leg] = 0.f;
     if (leg == 0 && flags) {
       const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
       L.slot[rank] = el;
@@ -1133,34 +1137,26 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&R
   float k01[6];
   int flags;
   const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags);
+  if ((threadIdx.x & 63) == 0) self_lds().ncand = __popcll(act);
   if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
   self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf);
   return act;
 }
 
-// Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
-// added to the reported knee / foot contact forces (fr).  act: self_stage's result.
-H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&Rk)[3][3], const float* pk,
-                         const float (&Rf)[3][3], const float* pf, float* wk, float* wf, Forces& fr) {
-  for (int i = 0; i < 6; ++i) { wk[i] = 0.f; wf[i] = 0.f; }
-  if (act == 0) return;
+// The pair jobs of the staged candidate envs: job = (env rank, left capsule i, right capsule j), this lane's jobs
+// g0, g0 + stride, ... (one wave: its live lanes; step_kernel's self + contact waves: 2 x the live lanes).  Each job
+// adds its contact wrenches into both bodies' LDS accumulators (atomics).
+H12_DEV void self_jobs(const KParams& P, int ncand, int g0, int stride, int set) {
   SelfLds& L = self_lds();
-  const float sg = leg ? -1.f : 1.f;
-  const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
-  // ---- pair jobs of the candidate envs over the wave's live lanes (a ragged last block has fewer):
-  // job = (env rank, left capsule i, right capsule j)
-  const uint64_t live = __ballot(1);
-  const int nlive = __popcll(live);
-  const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-  const int ncand = __popcll(act);
   // foot-foot fast path (round 5): when every candidate env of the wave has only its feet' bounds near (the common
   // case), its 16 rod-rod jobs alone are enumerated -- 4 envs per pass of 64 lanes instead of 2 of 25 jobs; the
   // blocks with several candidate envs set the step's tail (light stamps: without self-collision p95 / max of the
   // physics loop 22.2 / 23.6 us against 24.2 / 26.7)
-  const int lf = me < ncand ? L.flags[me] : 0;
-  const bool ffonly = __ballot(me < ncand && (lf & 7) != 0) == 0;
+  const int lr = threadIdx.x & 63;
+  const int lf = lr < ncand ? L.flags[lr] : 0;
+  const bool ffonly = __ballot(lr < ncand && (lf & 7) != 0) == 0;
   const int njobs = (ffonly ? 16 : 25) * ncand;
-  for (int jb = me; jb < njobs; jb += nlive) {
+  for (int jb = g0; jb < njobs; jb += stride) {
     int rank, i, j;
     if (ffonly) {
       rank = jb >> 4;
@@ -1188,8 +1184,8 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
     seg_points(pa, pb, qa, qb, sp);
     const int kl = i == 0 ? SG_KKIN : SG_FKIN, kr = j == 0 ? SG_KKIN : SG_FKIN;
     const float4 wl = gl(kl), vl = gl(kl + 1), ol = gl(kl + 2), wr = gr(kr), vr_ = gr(kr + 1), orr = gr(kr + 2);
-    auto al = [&](int a) -> float& { return L.acc[i > 0][a][e][0]; };
-    auto ar = [&](int a) -> float& { return L.acc[j > 0][a][e][1]; };
+    auto al = [&](int a) -> float& { return L.acc[set][i > 0][a][e][0]; };
+    auto ar = [&](int a) -> float& { return L.acc[set][j > 0][a][e][1]; };
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // unrolled: sp's arrays stay in registers
       if (q >= sp.n) break;
@@ -1220,23 +1216,47 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
       float m[3];
       cross(x, F, m);
       for (int a = 0; a < 3; ++a) {
-        atomicAdd(&al(a), F[a]); atomicAdd(&al(4 + a), m[a]);
-        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(4 + a), -m[a]);
+        atomicAdd(&al(a), F[a]); atomicAdd(&al(3 + a), m[a]);
+        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(3 + a), -m[a]);
       }
     }
+  }
+}
+
+// Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
+// added to the reported knee / foot contact forces (fr).  act: self_stage's result.  shared (step_kernel): the contact
+// wave runs every other 64-job pass of the inner step it (self_jobs_shared), and its release (L.done > it) is awaited
+// before the accumulators are read.
+H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&Rk)[3][3], const float* pk,
+                         const float (&Rf)[3][3], const float* pf, float* wk, float* wf, Forces& fr,
+                         bool shared = false, int it = 0) {
+  for (int i = 0; i < 6; ++i) { wk[i] = 0.f; wf[i] = 0.f; }
+  if (act == 0) return;
+  SelfLds& L = self_lds();
+  const float sg = leg ? -1.f : 1.f;
+  const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
+  // over the wave's live lanes (a ragged last block has fewer)
+  const uint64_t live = __ballot(1);
+  const int nlive = __popcll(live);
+  const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+  self_jobs(P, __popcll(act), me, shared ? 2 * nlive : nlive, 0);
+  if (shared) {  // the contact wave's jobs: its release store follows its atomics (an LDS spin, no barrier)
+    // bounded (~2 ms) so that a broken release can only corrupt the wrenches, never hang the GPU
+    for (int k = 0; k < (1 << 16) && *reinterpret_cast<volatile int*>(&L.done) <= it; ++k) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
   }
   wave_sync();
   // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
   const float ms[3] = {1.f, sg, 1.f};
   auto own_body = [&](int b, const float* po, const float (&Rb)[3][3], float* w, float* rep) {
-    float ac[8];
-    for (int a = 0; a < 3; ++a) { ac[a] = L.acc[b][a][el][leg]; ac[4 + a] = L.acc[b][4 + a][el][leg]; }
+    float ac[6];
+    for (int a = 0; a < 6; ++a) ac[a] = shared ? L.acc[0][b][a][el][leg] + L.acc[1][b][a][el][leg] : L.acc[0][b][a][el][leg];
     const float Fr[3] = {ac[0], ac[1], ac[2]};
     const float por[3] = {po[0], sg * po[1], po[2]};
     float pxF[3];
     cross(por, Fr, pxF);
     float Fl[3], Tl[3], fb[3], tb[3];
-    for (int a = 0; a < 3; ++a) { Fl[a] = ms[a] * Fr[a]; Tl[a] = sg * ms[a] * (ac[4 + a] - pxF[a]); }
+    for (int a = 0; a < 3; ++a) { Fl[a] = ms[a] * Fr[a]; Tl[a] = sg * ms[a] * (ac[3 + a] - pxF[a]); }
     mtv(Rb, Fl, fb);
     mtv(Rb, Tl, tb);
     for (int a = 0; a < 3; ++a) { w[a] = tb[a]; w[3 + a] = fb[a]; rep[a] += fb[a]; }
@@ -1244,6 +1264,28 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   own_body(0, pk, Rk, wk, fr.knee);
   own_body(1, pf, Rf, wf, fr.foot);
   wave_sync();  // the staging area is rewritten by the next physics step
+}
+
+// step_kernel's contact wave after R1 (self-collision on): every other 64-job pass of the inner step's self-contact
+// jobs, then its release L.done = it + 1 once its LDS atomics are done (self_finish(shared) spins on it).  The blocks
+// with several candidate envs set the step's tail: the physics wave waited 1.65 us per launch at R2 in the slowest 5 %
+// of the blocks against 0.13 in the median ones (light stamps, profiles/r5/r5t_*); the contact wave waits ~1.9 us
+// per launch there anyway
+H12_DEV void self_jobs_shared(const KParams& P, int it) {
+  SelfLds& L = self_lds();
+  const int ncand = L.ncand;
+  if (ncand) {
+    const int l = threadIdx.x & (BLOCK - 1);
+    for (int b = 0; b < 2; ++b)
+      for (int a = 0; a < 6; ++a) L.acc[1][b][a][l >> 1][l & 1] = 0.f;  // this wave's set, before its atomics
+    wave_sync();
+    const uint64_t live = __ballot(1);
+    const int nlive = __popcll(live);
+    const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+    self_jobs(P, ncand, nlive + me, 2 * nlive, 1);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) *reinterpret_cast<volatile int*>(&L.done) = it + 1;
 }
 
 H12_DEV void self_contacts(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
@@ -1813,6 +1855,7 @@ H12_DEV void contact_wave(const KParams& P, int n, int n_steps, const FuseCtx& f
     }
     SYNC_W(1);  // R1: the helper's sole contacts
     if (active) {
+      if (P.self_coll) self_jobs_shared(P, it);  // first: the self-contact wave waits for its release
       if (KNEE_ON_SELF && P.self_coll) {  // the knee contact's linearisation, from the self wave's hand-off
         float jt[16];
         get4(H.jt, l, jt, 4);
@@ -1867,6 +1910,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
   const int leg = l & 1;
   const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;
   HelpLds& H = help_lds();
+  if ((threadIdx.x & 63) == 0) self_lds().done = 0;  // before the first barrier S: the contact wave's release count
   H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
     SYNC_W(it ? 0 : 3);  // S: the state of this inner step
@@ -1897,7 +1941,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
     if (active) {
       float w[12];
       Forces fr = {};
-      self_finish(P, leg, act, Rk, pk, R, p, w, w + 6, fr);
+      self_finish(P, leg, act, Rk, pk, R, p, w, w + 6, fr, true, it);
       put4(H.selfw, l, w, 3);
     }
     fuse_drain(fc, it);

@@ -117,6 +117,8 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
         if os.environ.get("H12_WAVE_DUMP"):
             np.save(os.environ["H12_WAVE_DUMP"], np.asarray(raw))
             np.save(os.environ["H12_WAVE_DUMP"].replace(".npy", "_resets.npy"), np.asarray(rsets))
+            if bws:  # (launches, blocks, role, barrier) waits in us: which role a slow block waited for
+                np.save(os.environ["H12_WAVE_DUMP"].replace(".npy", "_bw.npy"), np.asarray(bws))
         res["wave_realtime_us_median"] = dict(zip(keys, (np.median(np.asarray(rows), axis=0) / 100.0).round(2).tolist()))
         R = np.asarray(raw)  # (launches, waves, 7)
         per = {}
