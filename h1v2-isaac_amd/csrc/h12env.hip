@@ -158,25 +158,31 @@ __device__ unsigned long long g_wave[1024][11];
 // in the inner steps' barriers S / R1 / R2 (and separately the first S, index 3), accumulated in registers and stored once per wave ([block][role][barrier];
 // roles 0 physics, 1 helper, 2 contact, 3 self): the wave that waits ~0 at a barrier is the one the block waited for
 #if defined(H12_PHASE_PROFILE) && defined(H12_PHASE_LIGHT)
-__device__ unsigned long long g_bw[1024][4][4];
-#define H12_BW_DECL unsigned long long _bw[4] = {0ull, 0ull, 0ull, 0ull}
-#define H12_BW_PARAM , unsigned long long (&_bw)[4]
+// [4..7]: the cycles each role spends between its previous barrier and barrier k (its own work before k)
+__device__ unsigned long long g_bw[1024][4][12];
+#define H12_BW_DECL unsigned long long _bw[13] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_readcyclecounter(), 0ull, 0ull, 0ull, 0ull}
+#define H12_BW_PARAM , unsigned long long (&_bw)[13]
 #define H12_BW_ARG , _bw
 #define SYNC_W(k)                                                                \
   do {                                                                           \
     const unsigned long long _t0 = __builtin_readcyclecounter();                \
+    _bw[4 + (k)] += _t0 - _bw[8];                                                \
     __syncthreads();                                                             \
-    _bw[k] += __builtin_readcyclecounter() - _t0;                               \
+    _bw[8] = __builtin_readcyclecounter();                                       \
+    _bw[k] += _bw[8] - _t0;                                                      \
   } while (0)
+// [9 + i]: the physics wave's time from its last barrier exit to mark i (PHL), summed: offsets inside a segment
+#define PHL(i) (_bw[9 + (i)] += __builtin_readcyclecounter() - _bw[8])
 #define H12_BW_STORE()                                                           \
   do {                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
-      for (int _k = 0; _k < 4; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k]; \
+      for (int _k = 0; _k < 12; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k + (_k >= 8)]; \
   } while (0)
 #else
 #define H12_BW_DECL (void)0
 #define H12_BW_PARAM
 #define H12_BW_ARG
+#define PHL(i) (void)0
 #define SYNC_W(k) __syncthreads()
 #define H12_BW_STORE() (void)0
 #endif
@@ -2240,6 +2246,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     link_p_pk<2>(cs, U, Dinv, tau, pb, p, u);
     link_p_pk<1>(cs, U, Dinv, tau, pb, p, u);
     link_p_pk<0>(cs, U, Dinv, tau, pb, p, u);
+    PHL(0);
     for (int k = 0; k < 3; ++k) { pAcc[k] = p[k].x; pAcc[3 + k] = p[k].y; }
   }
   // ---- un-mirror the leg's contribution to the base (I' = S I S, p' = S p)
@@ -2286,6 +2293,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     float rhs[6] = {-pB[0], -pB[1], -pB[2], -pB[3], -pB[4], -pB[5]};
     solve6(IB, rhs, a0);
   }
+  PHL(1);
   if (P.impl && leg == 0 && ict.gamma + ict.beta > 0.f) impl_force(a0, corner, ict.u, ict.beta, ict.gamma, fr.torso);
   // ---- pass 3 (root -> leaf) in the lane frame: a~ (the implicit contact reports use a~ + a^v)
   float avk[12];
@@ -2305,6 +2313,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   }
   link_pass3_pk<4>(cs, U, Dinv, u, ap, qdd);
   link_pass3_pk<5>(cs, U, Dinv, u, ap, qdd);
+  PHL(2);
   if (P.impl) {  // implicit part of the sole forces (a~ + a^v = the foot's acceleration, shifted frame)
     float ah[6], r[2][16];
     for (int k = 0; k < 3; ++k) { ah[k] = ap[k].x + avk[6 + k]; ah[3 + k] = ap[k].y + avk[9 + k]; }
@@ -4988,7 +4997,7 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 #ifdef H12_PHASE_LIGHT
 int h12env_barrier_waits(unsigned long long* out, int nblocks) {
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 16 * (size_t)nblocks));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 48 * (size_t)nblocks));
   return 0;
 }
 #endif

@@ -87,14 +87,14 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
         rows, raw, rsets, clk, bw, ends, light = [], [], [], [], [], [], []
         bws = []
         has_bw = hasattr(lib, "h12env_barrier_waits")
-        bwbuf = (C.c_ulonglong * (16 * waves))()
+        bwbuf = (C.c_ulonglong * (48 * waves))()
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
             lib.h12env_wave_times(wt, waves)
             if has_bw:  # light build: per block, role (physics, helper, contact, self) and barrier (S, R1, R2, first S)
                 lib.h12env_barrier_waits(bwbuf, waves)
-                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 4).astype(np.float64) / 2370.0)
+                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 12).astype(np.float64) / 2370.0)
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
@@ -149,6 +149,16 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             res["barrier_wait_us_per_launch_median"] = {
                 role: {bar: round(float(np.median(B[:, r, k])), 3) for k, bar in enumerate(("S", "R1", "R2", "S first"))}
                 for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            # each role's own work before each barrier kind (summed over the launch's inner steps; "S first": the
+            # work from the wave's start)
+            res["work_before_barrier_us_per_launch_median"] = {
+                role: {bar: round(float(np.median(B[:, r, 4 + k])), 3) for k, bar in enumerate(("S", "R1", "R2", "S first"))}
+                for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            # the physics wave after R2, summed over the inner steps: from the barrier exit to the end of the bias
+            # chain, of the base solve and of pass 3 (the rest up to S / the loop end: integration, state hand-off)
+            res["physics_after_r2_marks_us_per_launch_median"] = {
+                m: round(float(np.median(B[:, 0, 8 + i])), 3)
+                for i, m in enumerate(("bias chain", "+ base combine / solve", "+ pass 3 / implicit reports"))}
         if ends:
             E = np.concatenate(ends) / 100.0  # us from the physics wave's start: physics / helper / self wave ends
             res["wave_role_end_us"] = {"physics_median": round(float(np.median(E[:, 0])), 2),
