@@ -173,6 +173,8 @@ __device__ unsigned long long g_bw[1024][4][12];
   } while (0)
 // [9 + i]: the physics wave's time from its last barrier exit to mark i (PHL), summed: offsets inside a segment
 #define PHL(i) (_bw[9 + (i)] += __builtin_readcyclecounter() - _bw[8])
+// the self wave: the most candidate envs of an inner step (in its mark slot 0) and their sum (slot 1)
+#define PHN(n) (_bw[9] = max(_bw[9], (unsigned long long)(n)), _bw[10] += (unsigned long long)(n))
 #define H12_BW_STORE()                                                           \
   do {                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
@@ -183,6 +185,7 @@ __device__ unsigned long long g_bw[1024][4][12];
 #define H12_BW_PARAM
 #define H12_BW_ARG
 #define PHL(i) (void)0
+#define PHN(n) (void)0
 #define SYNC_W(k) __syncthreads()
 #define H12_BW_STORE() (void)0
 #endif
@@ -1948,6 +1951,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       float w[12];
       Forces fr = {};
       self_finish(P, leg, act, Rk, pk, R, p, w, w + 6, fr, true, it);
+      PHN(__popcll(act));
       put4(H.selfw, l, w, 3);
     }
     fuse_drain(fc, it);
