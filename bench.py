@@ -578,7 +578,8 @@ def main():
                 # the contract prices the dominant kernel against HBM (the north_star's roofline); the
                 # binding limit of step_kernel at 4096 envs is VALU issue latency ("issue" below)
                 "bound": "hbm",
-                "binding": "valu-issue latency (one wave per SIMD, 1/8 of the SIMDs at 4096 envs)",
+                "binding": ("valu-issue latency of the physics wave's serial chain (one wave per SIMD; 4096 envs fill "
+                            "128 of the 256 CUs with one 4-wave block each)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
