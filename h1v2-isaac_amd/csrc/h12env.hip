@@ -178,7 +178,13 @@ __device__ unsigned long long g_bw[1024][4][12];
 #define H12_BW_STORE()                                                           \
   do {                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
-      for (int _k = 0; _k < 12; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k + (_k >= 8)]; \
+      for (int _k = 0; _k < 11; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k + (_k >= 8)]; \
+  } while (0)
+// slot 11: the wave's arrival at barrier F (s_memrealtime, 100 MHz: comparable across the waves of a block)
+#define H12_BW_F_ARRIVAL()                                                       \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
+      g_bw[blockIdx.x][threadIdx.x >> 6][11] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define H12_BW_DECL (void)0
@@ -188,6 +194,7 @@ __device__ unsigned long long g_bw[1024][4][12];
 #define PHN(n) (void)0
 #define SYNC_W(k) __syncthreads()
 #define H12_BW_STORE() (void)0
+#define H12_BW_F_ARRIVAL() (void)0
 #endif
 
 thread_local char g_err[512] = "";
@@ -3575,6 +3582,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       }
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);  // this wave's shifted-row stores have completed (fuse_late rewrites some)
+        H12_BW_F_ARRIVAL();
         __syncthreads();                // F: the physics wave's noisy frames and refill flags
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
@@ -3591,6 +3599,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       __syncthreads();  // L (the helper's final sole contact state is in LDS)
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);
+        H12_BW_F_ARRIVAL();
         __syncthreads();  // F
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
@@ -3730,6 +3739,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     PH(5);
     if (A.fuse) {
       obs_frame_fused(P, s, leg, lane_pair, term || tout);
+      H12_BW_F_ARRIVAL();
       __syncthreads();  // F: the helper waves assemble and store the block's rows
     } else {
       obs_frame<K>(P, s, leg, e, W.n, A.frame);

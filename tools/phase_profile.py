@@ -159,6 +159,14 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             res["physics_after_r2_marks_us_per_launch_median"] = {
                 m: round(float(np.median(B[:, 0, 8 + i])), 3)
                 for i, m in enumerate(("bias chain", "+ base combine / solve", "+ pass 3 / implicit reports"))}
+            # who arrives last at barrier F (slot 11: s_memrealtime at the arrival, 100 MHz): per block, each role's
+            # arrival after the first one's
+            Fa = B[:, :, 11] * 2370.0 / 100.0  # back to realtime ticks, then us
+            Fa = Fa - Fa.min(1, keepdims=True)
+            res["barrier_F_arrival_after_first_us_median"] = {
+                role: round(float(np.median(Fa[:, r])), 3) for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            res["barrier_F_last_role_count"] = {
+                role: int((Fa.argmax(1) == r).sum()) for r, role in enumerate(("physics", "helper", "contact", "self"))}
         if ends:
             E = np.concatenate(ends) / 100.0  # us from the physics wave's start: physics / helper / self wave ends
             res["wave_role_end_us"] = {"physics_median": round(float(np.median(E[:, 0])), 2),
