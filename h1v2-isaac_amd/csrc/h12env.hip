@@ -1112,7 +1112,8 @@ H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, c
 }
 // the staging of a candidate wave (act != 0, wave-uniform): this leg's capsules and body kinematics (real frame)
 H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const float* k01, const float (&Rk)[3][3],
-                            const float* pk, const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
+                            const float* pk, const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
+                            bool zero_acc) {
   SelfLds& L = self_lds();
   const float sg = leg ? -1.f : 1.f;
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
@@ -1120,11 +1121,23 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
     auto g = [&](int f) -> float4& { return L.geo[f][el][leg]; };
     g(SG_KNEE) = make_float4(k01[0], k01[1], k01[2], mu);  // w: this leg's (sole) dynamic friction coefficient
     g(SG_KNEE + 1) = make_float4(k01[3], k01[4], k01[5], 0.f);
+    // the rods' ends share their foot-frame z: c = pf + z Rf e_z once, each end c + x Rf e_x + y Rf e_y (two fma per
+    // component instead of a matrix-vector product)
+    constexpr float RZ = h12m::ROD[0][0][2];
+    static_assert(h12m::ROD[1][0][2] == RZ && h12m::ROD[2][0][2] == RZ && h12m::ROD[3][0][2] == RZ &&
+                  h12m::ROD[0][1][2] == RZ && h12m::ROD[1][1][2] == RZ && h12m::ROD[2][1][2] == RZ &&
+                  h12m::ROD[3][1][2] == RZ, "sole rods in one foot-frame plane");
+    float c[3];
+    for (int i = 0; i < 3; ++i) c[i] = pf[i] + Rf[i][2] * RZ;
+    auto rod_end = [&](const float* pl, float* o) {
+      for (int i = 0; i < 3; ++i) o[i] = c[i] + Rf[i][0] * pl[0] + Rf[i][1] * pl[1];
+      o[1] *= sg;
+    };
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float a0[3], a1[3];
-      body_point_real(Rf, pf, h12m::ROD[r][0], sg, a0);
-      body_point_real(Rf, pf, h12m::ROD[r][1], sg, a1);
+      rod_end(h12m::ROD[r][0], a0);
+      rod_end(h12m::ROD[r][1], a1);
       g(SG_ROD + 2 * r) = make_float4(a0[0], a0[1], a0[2], 0.f);
       g(SG_ROD + 2 * r + 1) = make_float4(a1[0], a1[1], a1[2], 0.f);
     }
@@ -1138,8 +1151,9 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
     g(SG_FKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
     g(SG_FKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
     g(SG_FKIN + 2) = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
-    for (int b = 0; b < 2; ++b)
-      for (int a = 0; a < 6; ++a) L.acc[0][b][a][el][leg] = 0.f;
+    if (zero_acc)
+      for (int b = 0; b < 2; ++b)
+        for (int a = 0; a < 6; ++a) L.acc[0][b][a][el][leg] = 0.f;
     if (leg == 0 && flags) {
       const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
       L.slot[rank] = el;
@@ -1148,15 +1162,25 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
   }
   wave_sync();
 }
+// zero_acc false (step_kernel): the physics wave has zeroed this lane's accumulators before R1 (self_acc_zero)
 H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
-                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf) {
+                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
+                            bool zero_acc = true) {
   float k01[6];
   int flags;
   const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags);
   if ((threadIdx.x & 63) == 0) self_lds().ncand = __popcll(act);
   if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
-  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf);
+  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf, zero_acc);
   return act;
+}
+// step_kernel's physics wave before R1 (it waits there for the helper waves): the self wave's accumulators of this
+// lane's env and leg, zeroed for the inner step's jobs (the previous step's were read before its R2)
+H12_DEV void self_acc_zero() {
+  SelfLds& L = self_lds();
+  const int l = threadIdx.x & (BLOCK - 1);
+  for (int b = 0; b < 2; ++b)
+    for (int a = 0; a < 6; ++a) L.acc[0][b][a][l >> 1][l & 1] = 0.f;
 }
 
 // The pair jobs of the staged candidate envs: job = (env rank, left capsule i, right capsule j), this lane's jobs
@@ -1941,7 +1965,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
       // broad phase and, in a candidate wave, the staging (after R1 instead, the staging made this wave the last at R2:
       // -3 %, profiles/r5/r5p_*)
-      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5]);
+      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5], false);
       if constexpr (KNEE_ON_SELF) {
         // the knee capsule's ground contact (the contact wave's without a self wave): the knee origin back at the base
         // position (env-local on terrain, lane frame)
@@ -2173,6 +2197,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     joint_terms(P, lg, h, tq, dl);
     for (int k = 0; k < NL; ++k) tau[k] = tau_pd[k] + tq[k];
   }
+  if (P.self_coll) self_acc_zero();
   PHX(10);
   SYNC_W(1);  // R1: sole contacts (helper), knee contact (contact wave)
   PHX(8);
