@@ -888,9 +888,12 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
     lg.anc[q][1] = on ? ay : lg.anc[q][1];
     nmask |= (on ? 1 : 0) << q;
     float Fw[3] = {ft0, ft1, fn};
-    if (P.impl) {  // g M_w e_z = g (beta + gamma) e_z on a plane
-      const float beta = (on && stick) ? hb : 0.f, gam = on ? alpha - beta : 0.f;
-      Fw[2] += on ? P.g * alpha : 0.f;
+    // the implicit terms unconditionally, zero without them (beta = gamma = 0): a P.impl branch left every
+    // accumulator (the added inertia, the sums) zero-initialised ahead of it (~40 v_mov in the helper waves)
+    {  // g M_w e_z = g (beta + gamma) e_z on a plane
+      const bool im = P.impl && on;
+      const float beta = (im && stick) ? hb : 0.f, gam = im ? alpha - beta : 0.f;
+      Fw[2] += im ? P.g * alpha : 0.f;
       ss.sb += beta;
       ss.sg += gam;
 #pragma unroll
@@ -917,7 +920,7 @@ H12_DEV void sole_contacts_flat(const KParams& P, const float R[3][3], const flo
   pAcc[0] -= tl[0]; pAcc[1] -= tl[1]; pAcc[2] -= tl[2];
   pAcc[3] -= fl[0]; pAcc[4] -= fl[1]; pAcc[5] -= fl[2];
   fw[0] += fl[0]; fw[1] += fl[1]; fw[2] += fl[2];
-  if (P.impl) {
+  {  // zero without the implicit terms (the sums are)
     const float u[3] = {R[2][0], R[2][1], R[2][2]};
     // C += sum beta I + sum gamma u u^T
     const float gu[3] = {ss.sg * u[0], ss.sg * u[1], ss.sg * u[2]};
@@ -1039,11 +1042,6 @@ H12_DEV bool capsules_near(const float* p1, const float* q1, const float* p2, co
   const float reach = rr + slack;
   return dot3(dv, dv) < reach * reach;
 }
-// real-frame point of a lane-frame body point: M (Rb pl + pb), M = diag(1, sg, 1)
-H12_DEV void body_point_real(const float Rb[3][3], const float* pb, const float* pl, float sg, float* out) {
-  mv(Rb, pl, out);
-  out[0] += pb[0]; out[1] = sg * (out[1] + pb[1]); out[2] += pb[2];
-}
 H12_DEV void swap3(const float* a, float* b) { b[0] = pair_swap(a[0]); b[1] = pair_swap(a[1]); b[2] = pair_swap(a[2]); }
 
 // LDS staging of one wave (block = one wave): per env and leg 16 float4 -- knee segment (2), sole rods (8),
@@ -1084,15 +1082,36 @@ H12_DEV SelfLds& self_lds() {
 // self_broad: the broad phase alone (returns the wave's candidate mask; flags: the env's candidate bits, k01: this
 // leg's knee segment, real frame).  step_kernel's self wave runs it before R1 and the staging (self_stage_geo, which
 // needs the link velocities) after R1 in candidate waves only.
+// The foot's collision points (the sole rods' ends, the bounding capsule's) lie in one foot-frame plane z = SOLE_Z:
+// with c = pf + SOLE_Z Rf e_z (sole_plane), a point is c + x Rf e_x + y Rf e_y, real frame (two fma per component)
+constexpr float SOLE_Z = h12m::ROD[0][0][2];
+static_assert(h12m::ROD[1][0][2] == SOLE_Z && h12m::ROD[2][0][2] == SOLE_Z && h12m::ROD[3][0][2] == SOLE_Z &&
+              h12m::ROD[0][1][2] == SOLE_Z && h12m::ROD[1][1][2] == SOLE_Z && h12m::ROD[2][1][2] == SOLE_Z &&
+              h12m::ROD[3][1][2] == SOLE_Z && h12m::FB0[2] == SOLE_Z && h12m::FB1[2] == SOLE_Z,
+              "sole rods and foot bound in one foot-frame plane");
+static_assert(h12m::KNEE0[0] == 0.f && h12m::KNEE0[1] == 0.f && h12m::KNEE1[0] == 0.f && h12m::KNEE1[1] == 0.f,
+              "knee segment along the knee link's z axis");
+H12_DEV void sole_plane(const float (&Rf)[3][3], const float* pf, float* c) {
+  for (int i = 0; i < 3; ++i) c[i] = pf[i] + Rf[i][2] * SOLE_Z;
+}
+H12_DEV void sole_point(const float (&Rf)[3][3], const float* c, const float* pl, float sg, float* o) {
+  for (int i = 0; i < 3; ++i) o[i] = c[i] + Rf[i][0] * pl[0] + Rf[i][1] * pl[1];
+  o[1] *= sg;
+}
+H12_DEV void knee_point(const float (&Rk)[3][3], const float* pk, float z, float sg, float* o) {
+  for (int i = 0; i < 3; ++i) o[i] = pk[i] + Rk[i][2] * z;
+  o[1] *= sg;
+}
 H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, const float (&Rf)[3][3], const float* pf,
-                            float* k01, int& flags) {
+                            float* k01, int& flags, float* c) {
   const float sg = leg ? -1.f : 1.f;
   // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
   float k0[3], k1[3], b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
-  body_point_real(Rk, pk, h12m::KNEE0, sg, k0);
-  body_point_real(Rk, pk, h12m::KNEE1, sg, k1);
-  body_point_real(Rf, pf, h12m::FB0, sg, b0);
-  body_point_real(Rf, pf, h12m::FB1, sg, b1);
+  knee_point(Rk, pk, h12m::KNEE0[2], sg, k0);
+  knee_point(Rk, pk, h12m::KNEE1[2], sg, k1);
+  sole_plane(Rf, pf, c);
+  sole_point(Rf, c, h12m::FB0, sg, b0);
+  sole_point(Rf, c, h12m::FB1, sg, b1);
   swap3(k0, ok0); swap3(k1, ok1); swap3(b0, ob0); swap3(b1, ob1);
   // own left capsule (lane 0: its knee; lane 1: the partner's = left foot bound) vs the right leg's two
   // value selects (a select between register arrays by pointer would go through scratch)
@@ -1113,7 +1132,7 @@ H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, c
 // the staging of a candidate wave (act != 0, wave-uniform): this leg's capsules and body kinematics (real frame)
 H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const float* k01, const float (&Rk)[3][3],
                             const float* pk, const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
-                            bool zero_acc) {
+                            bool zero_acc, const float* c) {
   SelfLds& L = self_lds();
   const float sg = leg ? -1.f : 1.f;
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
@@ -1121,23 +1140,11 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
     auto g = [&](int f) -> float4& { return L.geo[f][el][leg]; };
     g(SG_KNEE) = make_float4(k01[0], k01[1], k01[2], mu);  // w: this leg's (sole) dynamic friction coefficient
     g(SG_KNEE + 1) = make_float4(k01[3], k01[4], k01[5], 0.f);
-    // the rods' ends share their foot-frame z: c = pf + z Rf e_z once, each end c + x Rf e_x + y Rf e_y (two fma per
-    // component instead of a matrix-vector product)
-    constexpr float RZ = h12m::ROD[0][0][2];
-    static_assert(h12m::ROD[1][0][2] == RZ && h12m::ROD[2][0][2] == RZ && h12m::ROD[3][0][2] == RZ &&
-                  h12m::ROD[0][1][2] == RZ && h12m::ROD[1][1][2] == RZ && h12m::ROD[2][1][2] == RZ &&
-                  h12m::ROD[3][1][2] == RZ, "sole rods in one foot-frame plane");
-    float c[3];
-    for (int i = 0; i < 3; ++i) c[i] = pf[i] + Rf[i][2] * RZ;
-    auto rod_end = [&](const float* pl, float* o) {
-      for (int i = 0; i < 3; ++i) o[i] = c[i] + Rf[i][0] * pl[0] + Rf[i][1] * pl[1];
-      o[1] *= sg;
-    };
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r) {  // the rods' ends from the sole plane's offset c (sole_point)
       float a0[3], a1[3];
-      rod_end(h12m::ROD[r][0], a0);
-      rod_end(h12m::ROD[r][1], a1);
+      sole_point(Rf, c, h12m::ROD[r][0], sg, a0);
+      sole_point(Rf, c, h12m::ROD[r][1], sg, a1);
       g(SG_ROD + 2 * r) = make_float4(a0[0], a0[1], a0[2], 0.f);
       g(SG_ROD + 2 * r + 1) = make_float4(a1[0], a1[1], a1[2], 0.f);
     }
@@ -1166,12 +1173,12 @@ H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const fl
 H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
                             const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
                             bool zero_acc = true) {
-  float k01[6];
+  float k01[6], c[3];
   int flags;
-  const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags);
+  const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags, c);
   if ((threadIdx.x & 63) == 0) self_lds().ncand = __popcll(act);
   if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
-  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf, zero_acc);
+  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf, zero_acc, c);
   return act;
 }
 // step_kernel's physics wave before R1 (it waits there for the helper waves): the self wave's accumulators of this
