@@ -159,17 +159,23 @@ __device__ unsigned long long g_wave[1024][11];
 // roles 0 physics, 1 helper, 2 contact, 3 self): the wave that waits ~0 at a barrier is the one the block waited for
 #if defined(H12_PHASE_PROFILE) && defined(H12_PHASE_LIGHT)
 // [4..7]: the cycles each role spends between its previous barrier and barrier k (its own work before k)
-__device__ unsigned long long g_bw[1024][4][12];
-#define H12_BW_DECL unsigned long long _bw[13] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_readcyclecounter(), 0ull, 0ull, 0ull, 0ull}
-#define H12_BW_PARAM , unsigned long long (&_bw)[13]
+// [12..14]: the same work times of the first inner step alone (from the first barrier S on; the instruction cache
+// starts every launch cold), [13 of _bw]: set once the first inner step's barrier S has passed
+__device__ unsigned long long g_bw[1024][4][16];
+#define H12_BW_DECL                                                                                                   \
+  unsigned long long _bw[18] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_readcyclecounter(),       \
+                                0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull}
+#define H12_BW_PARAM , unsigned long long (&_bw)[18]
 #define H12_BW_ARG , _bw
 #define SYNC_W(k)                                                                \
   do {                                                                           \
     const unsigned long long _t0 = __builtin_readcyclecounter();                \
     _bw[4 + (k)] += _t0 - _bw[8];                                                \
+    if ((k) != 3 && _bw[13] == 0) _bw[14 + (k)] += _t0 - _bw[8];                 \
     __syncthreads();                                                             \
     _bw[8] = __builtin_readcyclecounter();                                       \
     _bw[k] += _bw[8] - _t0;                                                      \
+    if ((k) == 0) _bw[13] = 1;                                                   \
   } while (0)
 // [9 + i]: the physics wave's time from its last barrier exit to mark i (PHL), summed: offsets inside a segment
 #define PHL(i) (_bw[9 + (i)] += __builtin_readcyclecounter() - _bw[8])
@@ -179,6 +185,8 @@ __device__ unsigned long long g_bw[1024][4][12];
   do {                                                                           \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
       for (int _k = 0; _k < 11; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k + (_k >= 8)]; \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
+      for (int _k = 0; _k < 3; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][12 + _k] = _bw[14 + _k]; \
   } while (0)
 // slot 11: the wave's arrival at barrier F (s_memrealtime, 100 MHz: comparable across the waves of a block)
 #define H12_BW_F_ARRIVAL()                                                       \
@@ -5043,7 +5051,7 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 #ifdef H12_PHASE_LIGHT
 int h12env_barrier_waits(unsigned long long* out, int nblocks) {
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 48 * (size_t)nblocks));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 64 * (size_t)nblocks));
   return 0;
 }
 #endif

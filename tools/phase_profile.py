@@ -87,14 +87,14 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
         rows, raw, rsets, clk, bw, ends, light = [], [], [], [], [], [], []
         bws = []
         has_bw = hasattr(lib, "h12env_barrier_waits")
-        bwbuf = (C.c_ulonglong * (48 * waves))()
+        bwbuf = (C.c_ulonglong * (64 * waves))()
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
             lib.h12env_wave_times(wt, waves)
             if has_bw:  # light build: per block, role (physics, helper, contact, self) and barrier (S, R1, R2, first S)
                 lib.h12env_barrier_waits(bwbuf, waves)
-                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 12).astype(np.float64) / 2370.0)
+                bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 16).astype(np.float64) / 2370.0)
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
@@ -159,6 +159,15 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             res["physics_after_r2_marks_us_per_launch_median"] = {
                 m: round(float(np.median(B[:, 0, 8 + i])), 3)
                 for i, m in enumerate(("bias chain", "+ base combine / solve", "+ pass 3 / implicit reports"))}
+            # the first inner step alone (slots 12-14: work before its S / R1 / R2; the instruction cache is cold at the
+            # launch's start) against the mean inner step of the launch
+            n_in = (3.0, 4.0, 4.0)  # barrier S between the 4 inner steps, R1 / R2 in each
+            res["work_first_inner_step_us_median"] = {
+                role: {bar: round(float(np.median(B[:, r, 12 + k])), 3) for k, bar in enumerate(("S", "R1", "R2"))}
+                for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            res["work_mean_inner_step_us_median"] = {
+                role: {bar: round(float(np.median(B[:, r, 4 + k])) / n_in[k], 3) for k, bar in enumerate(("S", "R1", "R2"))}
+                for r, role in enumerate(("physics", "helper", "contact", "self"))}
             # who arrives last at barrier F (slot 11: s_memrealtime at the arrival, 100 MHz): per block, each role's
             # arrival after the first one's
             Fa = B[:, :, 11] * 2370.0 / 100.0  # back to realtime ticks, then us
