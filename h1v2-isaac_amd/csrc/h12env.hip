@@ -735,6 +735,40 @@ H12_DEV void link_p_pk(const float (&cs)[NL][2], const f32x2 (&U)[NL][3], const 
   if constexpr (LINK > 0)
     for (int k = 0; k < 3; ++k) p[k] += pb[LINK - 1][k];
 }
+// link_pass1 on pairs (leg_pass1: step_kernel's helper waves, whose pass 1 and contacts set barrier R1): the spatial
+// velocity as (angular, linear) pairs (link_pass3_pk's transform, the joint rate for qdd), the world rotation's rows 0 / 1
+// as column pairs C[j] = (R_0j, R_1j) with row 2 apart (R2), the position as (p01, p2): a joint rotation turns two
+// columns, one packed op per pair of rows
+template <int LINK>
+H12_DEV void link_pass1_pk(const Leg& lg, float (&cs)[NL][2], const f32x2* vp, f32x2 (&V)[NL][3], f32x2 (&C)[3],
+                           float (&R2)[3], f32x2& p01, float& p2) {
+  constexpr int A = AX[LINK], J = (A + 1) % 3, Q = (A + 2) % 3;
+  const float* r = h12m::R[LINK];
+  float s, c;
+  fsincos(lg.q[LINK], &s, &c);
+  cs[LINK][0] = c;
+  cs[LINK][1] = s;
+  const float aw[3] = {vp[0].x, vp[1].x, vp[2].x};
+  float t[3];
+  cross(r, aw, t);
+  f32x2 in[3];
+  for (int k = 0; k < 3; ++k) in[k] = pk2(vp[k].x, vp[k].y - t[k]);
+  rot_pk<A>(c, -s, in, V[LINK]);
+  V[LINK][A].x += lg.qd[LINK];
+  // the joint origin (the parent's rotation): p += R r, r sparse
+  for (int k = 0; k < 3; ++k)
+    if (r[k] != 0.f) {
+      p01 += C[k] * r[k];
+      p2 += R2[k] * r[k];
+    }
+  // R <- R R_A(q): columns J, Q turn (rotT<A> of every row)
+  const f32x2 cj = C[J], cq = C[Q];
+  C[J] = c * cj + s * cq;
+  C[Q] = c * cq - s * cj;
+  const float rj = R2[J], rq = R2[Q];
+  R2[J] = c * rj + s * rq;
+  R2[Q] = c * rq - s * rj;
+}
 // link_pass3 of the AV form on (angular, linear) pairs a[k] = (a_k, a_3+k)
 template <int LINK>
 H12_DEV void link_pass3_pk(const float (&cs)[NL][2], const f32x2 (&U)[NL][3], const float (&Dinv)[NL],
@@ -1626,16 +1660,39 @@ H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, 
   if constexpr (Feat<K>::terrain) { pb0[0] -= org[0]; pb0[1] -= org[1]; pb0[2] -= org[2]; }
   if (rel) { pb0[0] = 0.f; pb0[1] = 0.f; pb0[2] = 0.f; }
   p[0] = pb0[0]; p[1] = sg * pb0[1]; p[2] = pb0[2];
-  link_pass1<0>(lg, cs, vl0, v, R, p);
-  link_pass1<1>(lg, cs, v[0], v, R, p);
-  link_pass1<2>(lg, cs, v[1], v, R, p);
-  link_pass1<3>(lg, cs, v[2], v, R, p);
-  for (int i = 0; i < 3; ++i) {
-    pk[i] = p[i];
-    for (int j = 0; j < 3; ++j) Rk[i][j] = R[i][j];
+  // the links on pairs (link_pass1_pk)
+  f32x2 C[3], V0[3], V[NL][3];
+  float R2[3];
+  for (int j = 0; j < 3; ++j) {
+    C[j] = pk2(R[0][j], R[1][j]);
+    R2[j] = R[2][j];
+    V0[j] = pk2(vl0[j], vl0[3 + j]);
   }
-  link_pass1<4>(lg, cs, v[3], v, R, p);
-  link_pass1<5>(lg, cs, v[4], v, R, p);
+  f32x2 p01 = pk2(p[0], p[1]);
+  float p2 = p[2];
+  link_pass1_pk<0>(lg, cs, V0, V, C, R2, p01, p2);
+  link_pass1_pk<1>(lg, cs, V[0], V, C, R2, p01, p2);
+  link_pass1_pk<2>(lg, cs, V[1], V, C, R2, p01, p2);
+  link_pass1_pk<3>(lg, cs, V[2], V, C, R2, p01, p2);
+  for (int j = 0; j < 3; ++j) {
+    Rk[0][j] = C[j].x;
+    Rk[1][j] = C[j].y;
+    Rk[2][j] = R2[j];
+  }
+  pk[0] = p01.x; pk[1] = p01.y; pk[2] = p2;
+  link_pass1_pk<4>(lg, cs, V[3], V, C, R2, p01, p2);
+  link_pass1_pk<5>(lg, cs, V[4], V, C, R2, p01, p2);
+  for (int j = 0; j < 3; ++j) {
+    R[0][j] = C[j].x;
+    R[1][j] = C[j].y;
+    R[2][j] = R2[j];
+  }
+  p[0] = p01.x; p[1] = p01.y; p[2] = p2;
+  for (int l = 0; l < NL; ++l)
+    for (int k = 0; k < 3; ++k) {
+      v[l][k] = V[l][k].x;
+      v[l][3 + k] = V[l][k].y;
+    }
 }
 // knee capsule contact with the ground: lower end point, evaluated at the knee link pose (Rk / pk / vk)
 template <int K>
