@@ -250,8 +250,10 @@ H12_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 H12_DEV float uab(uint32_t x, float a, float b) { return a + (b - a) * u01(x); }
 
 // lane-pair exchange (lanes 2e and 2e+1 hold the two legs of env e): one DPP quad_perm(1,0,3,2)
-// move (a VALU op) instead of __shfl_xor's ds_bpermute round trip through the LDS crossbar
-H12_DEV int pair_swap_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+// move (a VALU op) instead of __shfl_xor's ds_bpermute round trip through the LDS crossbar.  bound_ctrl set: the
+// compiler then folds the move into a consuming VALU op (x + pair_swap(x) -> one v_add_f32_dpp); a quad_perm source
+// is never out of bounds, and the callers keep both lanes of a pair active at every swap
+H12_DEV int pair_swap_i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true); }
 H12_DEV float pair_swap(float x) { return __int_as_float(pair_swap_i(__float_as_int(x))); }
 
 }  // namespace h12

@@ -2394,12 +2394,13 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) IB.B[i][j] = comb(IA.B[i][j]);
   }
+  // branch-free (the fixed base selects afterwards): the pair sums stay in the solve's block, where each DPP swap folds
+  // into its add
   float a0[6];
-  if (P.fix_base) {
-    for (int i = 0; i < 6; ++i) a0[i] = -ag[i];
-  } else {
+  {
     float rhs[6] = {-pB[0], -pB[1], -pB[2], -pB[3], -pB[4], -pB[5]};
     solve6(IB, rhs, a0);
+    for (int i = 0; i < 6; ++i) a0[i] = P.fix_base ? -ag[i] : a0[i];
   }
   PHL(1);
   if (P.impl && leg == 0 && ict.gamma + ict.beta > 0.f) impl_force(a0, corner, ict.u, ict.beta, ict.gamma, fr.torso);
