@@ -160,12 +160,16 @@ __device__ unsigned long long g_wave[1024][11];
 #if defined(H12_PHASE_PROFILE) && defined(H12_PHASE_LIGHT)
 // [4..7]: the cycles each role spends between its previous barrier and barrier k (its own work before k)
 // [12..14]: the same work times of the first inner step alone (from the first barrier S on; the instruction cache
-// starts every launch cold), [13 of _bw]: set once the first inner step's barrier S has passed
+// starts every launch cold), [13 of _bw]: set once the first inner step's barrier S has passed; [15] (_bw[17]): the
+// wave's start (s_memrealtime, 100 MHz)
 __device__ unsigned long long g_bw[1024][4][16];
 #define H12_BW_DECL                                                                                                   \
   unsigned long long _bw[18] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_readcyclecounter(),       \
-                                0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull}
+                                0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_amdgcn_s_memrealtime()}
 #define H12_BW_PARAM , unsigned long long (&_bw)[18]
+// the physics wave's start stamp taken at its entry (its H12_BW_DECL follows the state loads)
+#define H12_BW_ENTRY() const unsigned long long _bw_entry = __builtin_amdgcn_s_memrealtime()
+#define H12_BW_SET_ENTRY() (_bw[17] = _bw_entry)
 #define H12_BW_ARG , _bw
 #define SYNC_W(k)                                                                \
   do {                                                                           \
@@ -187,6 +191,7 @@ __device__ unsigned long long g_bw[1024][4][16];
       for (int _k = 0; _k < 11; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][_k] = _bw[_k + (_k >= 8)]; \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
       for (int _k = 0; _k < 3; ++_k) g_bw[blockIdx.x][threadIdx.x >> 6][12 + _k] = _bw[14 + _k]; \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) g_bw[blockIdx.x][threadIdx.x >> 6][15] = _bw[17];  \
   } while (0)
 // slot 11: the wave's arrival at barrier F (s_memrealtime, 100 MHz: comparable across the waves of a block)
 #define H12_BW_F_ARRIVAL()                                                       \
@@ -196,6 +201,8 @@ __device__ unsigned long long g_bw[1024][4][16];
   } while (0)
 #else
 #define H12_BW_DECL (void)0
+#define H12_BW_ENTRY() (void)0
+#define H12_BW_SET_ENTRY() (void)0
 #define H12_BW_PARAM
 #define H12_BW_ARG
 #define PHL(i) (void)0
@@ -3582,8 +3589,29 @@ H12_DEV void obs_frame_fused(const KParams& P, const EnvSt& s, int leg, int r, b
   }
 }
 
+// Every 64-B line of the kernel arguments into the scalar cache at once, at the start of every wave: the compiler sinks
+// each kernel-argument load to its first use, so the helper waves' way to their first barrier held 3-4 dependent
+// rounds of scalar loads and waits (light stamps: they started their roles 0.8-1.0 us after the physics wave, which
+// waited ~0.5 us for them at the first barrier S).  The loads' values are dropped; the wait is in the same statement.
+static_assert(sizeof(KParams) + sizeof(Workspace) + sizeof(StepArgs) <= 1024, "kernel arguments within 16 lines");
+H12_DEV void kernarg_warm() {
+  const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t d0, d1, d2, d3;
+  asm volatile(
+      "s_load_dword %0, %4, 0x0\n\ts_load_dword %1, %4, 0x40\n\ts_load_dword %2, %4, 0x80\n\t"
+      "s_load_dword %3, %4, 0xc0\n\ts_load_dword %0, %4, 0x100\n\ts_load_dword %1, %4, 0x140\n\t"
+      "s_load_dword %2, %4, 0x180\n\ts_load_dword %3, %4, 0x1c0\n\ts_load_dword %0, %4, 0x200\n\t"
+      "s_load_dword %1, %4, 0x240\n\ts_load_dword %2, %4, 0x280\n\ts_load_dword %3, %4, 0x2c0\n\t"
+      "s_load_dword %0, %4, 0x300\n\ts_load_dword %1, %4, 0x340\n\ts_load_dword %2, %4, 0x380\n\t"
+      "s_load_dword %3, %4, 0x3c0\n\ts_waitcnt lgkmcnt(0)"
+      : "=&s"(d0), "=&s"(d1), "=&s"(d2), "=&s"(d3)
+      : "s"(ka)
+      : "memory");
+}
+
 template <int K>
 __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  kernarg_warm();
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step_hw, helper_wave, contact_wave, self_wave)
     const int nsteps = P.decimation * P.inner;
     FuseCtx fc = {};
@@ -3713,6 +3741,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
   const bool active = e < W.n;
   const uint32_t g = (uint32_t)(A.env_offset + e);
   PH_INIT();
+  H12_BW_ENTRY();
   if (Feat<K>::ext && P.dz && blockIdx.x == 0 && threadIdx.x == 0) P.dz_cnt[(A.dz_slot + 2) % 3] = 0;
   if (active) {
     EnvSt s;
@@ -3741,6 +3770,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     put_state(threadIdx.x, s.b, s.lg, s.origin);
     put_cst(threadIdx.x, s.lg);
     H12_BW_DECL;
+    H12_BW_SET_ENTRY();
     SYNC_W(3);  // S: the first inner step's state (and the sole contact state) for the other waves
     for (int st = 0; st < dec; ++st) {
       const bool last = st == dec - 1;

@@ -168,6 +168,13 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             res["work_mean_inner_step_us_median"] = {
                 role: {bar: round(float(np.median(B[:, r, 4 + k])) / n_in[k], 3) for k, bar in enumerate(("S", "R1", "R2"))}
                 for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            # each role's start after the block's first wave (slot 15: s_memrealtime at the wave's first stamp)
+            St = B[:, :, 15] * 2370.0 / 100.0
+            St = St - St.min(1, keepdims=True)
+            res["wave_start_after_first_us_median"] = {
+                role: round(float(np.median(St[:, r])), 3) for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            res["wave_start_after_first_us_p90"] = {
+                role: round(float(np.quantile(St[:, r], 0.9)), 3) for r, role in enumerate(("physics", "helper", "contact", "self"))}
             # who arrives last at barrier F (slot 11: s_memrealtime at the arrival, 100 MHz): per block, each role's
             # arrival after the first one's
             Fa = B[:, :, 11] * 2370.0 / 100.0  # back to realtime ticks, then us
