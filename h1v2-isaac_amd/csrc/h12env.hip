@@ -1151,14 +1151,20 @@ H12_DEV void knee_point(const float (&Rk)[3][3], const float* pk, float z, float
   for (int i = 0; i < 3; ++i) o[i] = pk[i] + Rk[i][2] * z;
   o[1] *= sg;
 }
-H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, const float (&Rf)[3][3], const float* pf,
-                            float* k01, int& flags, float* c) {
+// the knee segment's ends (k01, real frame) and the sole plane's offset c (sole_plane), shared by the broad phase and
+// the staging
+H12_DEV void self_points(int leg, const float (&Rk)[3][3], const float* pk, const float (&Rf)[3][3], const float* pf,
+                         float* k01, float* c) {
+  const float sg = leg ? -1.f : 1.f;
+  knee_point(Rk, pk, h12m::KNEE0[2], sg, k01);
+  knee_point(Rk, pk, h12m::KNEE1[2], sg, k01 + 3);
+  sole_plane(Rf, pf, c);
+}
+H12_DEV uint64_t self_broad(int leg, const float (&Rf)[3][3], const float* k01, const float* c, int& flags) {
   const float sg = leg ? -1.f : 1.f;
   // ---- broad phase: lane 0 tests (left knee | right knee, right foot), lane 1 (left foot | right knee, right foot)
-  float k0[3], k1[3], b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
-  knee_point(Rk, pk, h12m::KNEE0[2], sg, k0);
-  knee_point(Rk, pk, h12m::KNEE1[2], sg, k1);
-  sole_plane(Rf, pf, c);
+  float k0[3] = {k01[0], k01[1], k01[2]}, k1[3] = {k01[3], k01[4], k01[5]};
+  float b0[3], b1[3], ok0[3], ok1[3], ob0[3], ob1[3];
   sole_point(Rf, c, h12m::FB0, sg, b0);
   sole_point(Rf, c, h12m::FB1, sg, b1);
   swap3(k0, ok0); swap3(k1, ok1); swap3(b0, ob0); swap3(b1, ob1);
@@ -1175,59 +1181,66 @@ H12_DEV uint64_t self_broad(int leg, const float (&Rk)[3][3], const float* pk, c
   const int f1 = capsules_near(La, Lb, Rb0, Rb1, rl + h12m::FB_R) ? 1 : 0;
   const int mine = (f0 | f1 << 1) << (2 * leg);   // bits: 0 kk, 1 kf, 2 fk, 3 ff (left capsule major)
   flags = mine | pair_swap_i(mine);
-  for (int a = 0; a < 3; ++a) { k01[a] = k0[a]; k01[3 + a] = k1[a]; }
   return __ballot(flags != 0 && leg == 0);
 }
-// the staging of a candidate wave (act != 0, wave-uniform): this leg's capsules and body kinematics (real frame)
-H12_DEV void self_stage_geo(int leg, float mu, uint64_t act, int flags, const float* k01, const float (&Rk)[3][3],
-                            const float* pk, const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
-                            bool zero_acc, const float* c) {
+// the staging: this leg's capsules and body kinematics (real frame)
+H12_DEV void self_stage_geo(int leg, float mu, const float* k01, const float (&Rk)[3][3], const float* pk,
+                            const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf, bool zero_acc,
+                            const float* c) {
   SelfLds& L = self_lds();
   const float sg = leg ? -1.f : 1.f;
   const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
-  {
-    auto g = [&](int f) -> float4& { return L.geo[f][el][leg]; };
-    g(SG_KNEE) = make_float4(k01[0], k01[1], k01[2], mu);  // w: this leg's (sole) dynamic friction coefficient
-    g(SG_KNEE + 1) = make_float4(k01[3], k01[4], k01[5], 0.f);
+  auto g = [&](int f) -> float4& { return L.geo[f][el][leg]; };
+  g(SG_KNEE) = make_float4(k01[0], k01[1], k01[2], mu);  // w: this leg's (sole) dynamic friction coefficient
+  g(SG_KNEE + 1) = make_float4(k01[3], k01[4], k01[5], 0.f);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {  // the rods' ends from the sole plane's offset c (sole_point)
-      float a0[3], a1[3];
-      sole_point(Rf, c, h12m::ROD[r][0], sg, a0);
-      sole_point(Rf, c, h12m::ROD[r][1], sg, a1);
-      g(SG_ROD + 2 * r) = make_float4(a0[0], a0[1], a0[2], 0.f);
-      g(SG_ROD + 2 * r + 1) = make_float4(a1[0], a1[1], a1[2], 0.f);
-    }
-    // world angular velocity (a pseudo-vector: w_real = det(M) M w_lane, det M = sg), origin velocity, origin
-    float w[3], v[3];
-    mv(Rk, vk, w); mv(Rk, vk + 3, v);
-    g(SG_KKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
-    g(SG_KKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
-    g(SG_KKIN + 2) = make_float4(pk[0], sg * pk[1], pk[2], 0.f);
-    mv(Rf, vf, w); mv(Rf, vf + 3, v);
-    g(SG_FKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
-    g(SG_FKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
-    g(SG_FKIN + 2) = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
-    if (zero_acc)
-      for (int b = 0; b < 2; ++b)
-        for (int a = 0; a < 6; ++a) L.acc[0][b][a][el][leg] = 0.f;
-    if (leg == 0 && flags) {
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-      L.slot[rank] = el;
-      L.flags[rank] = flags;
-    }
+  for (int r = 0; r < 4; ++r) {  // the rods' ends from the sole plane's offset c (sole_point)
+    float a0[3], a1[3];
+    sole_point(Rf, c, h12m::ROD[r][0], sg, a0);
+    sole_point(Rf, c, h12m::ROD[r][1], sg, a1);
+    g(SG_ROD + 2 * r) = make_float4(a0[0], a0[1], a0[2], 0.f);
+    g(SG_ROD + 2 * r + 1) = make_float4(a1[0], a1[1], a1[2], 0.f);
+  }
+  // world angular velocity (a pseudo-vector: w_real = det(M) M w_lane, det M = sg), origin velocity, origin
+  float w[3], v[3];
+  mv(Rk, vk, w); mv(Rk, vk + 3, v);
+  g(SG_KKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+  g(SG_KKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
+  g(SG_KKIN + 2) = make_float4(pk[0], sg * pk[1], pk[2], 0.f);
+  mv(Rf, vf, w); mv(Rf, vf + 3, v);
+  g(SG_FKIN) = make_float4(sg * w[0], w[1], sg * w[2], 0.f);
+  g(SG_FKIN + 1) = make_float4(v[0], sg * v[1], v[2], 0.f);
+  g(SG_FKIN + 2) = make_float4(pf[0], sg * pf[1], pf[2], 0.f);
+  if (zero_acc)
+    for (int b = 0; b < 2; ++b)
+      for (int a = 0; a < 6; ++a) L.acc[0][b][a][el][leg] = 0.f;
+}
+// a candidate wave's (act != 0, wave-uniform) job list: each candidate env's slot and bits, ranked by the ballot
+H12_DEV void self_stage_slots(int leg, uint64_t act, int flags) {
+  SelfLds& L = self_lds();
+  if (leg == 0 && flags) {
+    const int el = (threadIdx.x & (BLOCK - 1)) >> 1;
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    L.slot[rank] = el;
+    L.flags[rank] = flags;
   }
   wave_sync();
 }
 // zero_acc false (step_kernel): the physics wave has zeroed this lane's accumulators before R1 (self_acc_zero)
+// early (step_kernel): the staging's LDS writes are issued ahead of the broad phase's tests, which they then overlap
+// (in a wave without candidates they go unread)
 H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
                             const float* vk, const float (&Rf)[3][3], const float* pf, const float* vf,
-                            bool zero_acc = true) {
+                            bool zero_acc = true, bool early = false) {
   float k01[6], c[3];
   int flags;
-  const uint64_t act = self_broad(leg, Rk, pk, Rf, pf, k01, flags, c);
+  self_points(leg, Rk, pk, Rf, pf, k01, c);
+  if (early) self_stage_geo(leg, mu, k01, Rk, pk, vk, Rf, pf, vf, zero_acc, c);
+  const uint64_t act = self_broad(leg, Rf, k01, c, flags);
   if ((threadIdx.x & 63) == 0) self_lds().ncand = __popcll(act);
   if (act == 0) return 0;  // wave-uniform: no candidate pair anywhere in the wave
-  self_stage_geo(leg, mu, act, flags, k01, Rk, pk, vk, Rf, pf, vf, zero_acc, c);
+  if (!early) self_stage_geo(leg, mu, k01, Rk, pk, vk, Rf, pf, vf, zero_acc, c);
+  self_stage_slots(leg, act, flags);
   return act;
 }
 // step_kernel's physics wave before R1 (it waits there for the helper waves): the self wave's accumulators of this
@@ -2044,7 +2057,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
       // broad phase and, in a candidate wave, the staging (after R1 instead, the staging made this wave the last at R2:
       // -3 %, profiles/r5/r5p_*)
-      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5], false);
+      act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5], false, true);
       if constexpr (KNEE_ON_SELF) {
         // the knee capsule's ground contact (the contact wave's without a self wave): the knee origin back at the base
         // position (env-local on terrain, lane frame)
