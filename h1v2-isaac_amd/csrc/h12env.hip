@@ -1243,28 +1243,32 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&R
   self_stage_slots(leg, act, flags);
   return act;
 }
-// step_kernel's physics wave before R1 (it waits there for the helper waves): the self wave's accumulators of this
-// lane's env and leg, zeroed for the inner step's jobs (the previous step's were read before its R2)
+// step_kernel's physics wave before R1 (it waits there for the helper waves): both accumulator sets (self and contact
+// wave) of this lane's env and leg, zeroed for the inner step's jobs (the previous step's were read before its R2)
 H12_DEV void self_acc_zero() {
   SelfLds& L = self_lds();
   const int l = threadIdx.x & (BLOCK - 1);
-  for (int b = 0; b < 2; ++b)
-    for (int a = 0; a < 6; ++a) L.acc[0][b][a][l >> 1][l & 1] = 0.f;
+  for (int set = 0; set < 2; ++set)
+    for (int b = 0; b < 2; ++b)
+      for (int a = 0; a < 6; ++a) L.acc[set][b][a][l >> 1][l & 1] = 0.f;
 }
 
 // The pair jobs of the staged candidate envs: job = (env rank, left capsule i, right capsule j), this lane's jobs
 // g0, g0 + stride, ... (one wave: its live lanes; step_kernel's self + contact waves: 2 x the live lanes).  Each job
 // adds its contact wrenches into both bodies' LDS accumulators (atomics).
-H12_DEV void self_jobs(const KParams& P, int ncand, int g0, int stride, int set) {
-  SelfLds& L = self_lds();
-  // foot-foot fast path (round 5): when every candidate env of the wave has only its feet' bounds near (the common
-  // case), its 16 rod-rod jobs alone are enumerated -- 4 envs per pass of 64 lanes instead of 2 of 25 jobs; the
-  // blocks with several candidate envs set the step's tail (light stamps: without self-collision p95 / max of the
-  // physics loop 22.2 / 23.6 us against 24.2 / 26.7)
+// The job count of the staged candidates (wave-uniform).  Foot-foot fast path (round 5): when every candidate env of
+// the wave has only its feet' bounds near (the common case), its 16 rod-rod jobs alone are enumerated -- 4 envs per
+// pass of 64 lanes instead of 2 of 25 jobs; the blocks with several candidate envs set the step's tail (light stamps:
+// without self-collision p95 / max of the physics loop 22.2 / 23.6 us against 24.2 / 26.7)
+H12_DEV int self_njobs(int ncand, bool& ffonly) {
+  const SelfLds& L = self_lds();
   const int lr = threadIdx.x & 63;
   const int lf = lr < ncand ? L.flags[lr] : 0;
-  const bool ffonly = __ballot(lr < ncand && (lf & 7) != 0) == 0;
-  const int njobs = (ffonly ? 16 : 25) * ncand;
+  ffonly = __ballot(lr < ncand && (lf & 7) != 0) == 0;
+  return (ffonly ? 16 : 25) * ncand;
+}
+H12_DEV void self_jobs(const KParams& P, int njobs, bool ffonly, int g0, int stride, int set) {
+  SelfLds& L = self_lds();
   for (int jb = g0; jb < njobs; jb += stride) {
     int rank, i, j;
     if (ffonly) {
@@ -1334,8 +1338,9 @@ H12_DEV void self_jobs(const KParams& P, int ncand, int g0, int stride, int set)
 
 // Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
 // added to the reported knee / foot contact forces (fr).  act: self_stage's result.  shared (step_kernel): the contact
-// wave runs every other 64-job pass of the inner step it (self_jobs_shared), and its release (L.done > it) is awaited
-// before the accumulators are read.
+// wave runs every other 64-job pass of the inner step it (self_jobs_shared) into its own accumulator set (zeroed with
+// this wave's by the physics wave, self_acc_zero), and when there is such a pass (more jobs than live lanes) its
+// release (L.done > it) is awaited.
 H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&Rk)[3][3], const float* pk,
                          const float (&Rf)[3][3], const float* pf, float* wk, float* wf, Forces& fr,
                          bool shared = false, int it = 0) {
@@ -1348,8 +1353,11 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   const uint64_t live = __ballot(1);
   const int nlive = __popcll(live);
   const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-  self_jobs(P, __popcll(act), me, shared ? 2 * nlive : nlive, 0);
-  if (shared) {  // the contact wave's jobs: its release store follows its atomics (an LDS spin, no barrier)
+  bool ffonly;
+  const int njobs = self_njobs(__popcll(act), ffonly);
+  self_jobs(P, njobs, ffonly, me, shared ? 2 * nlive : nlive, 0);
+  const bool sj = shared && njobs > nlive;  // the contact wave has jobs (self_jobs_shared)
+  if (sj) {  // the contact wave's jobs: its release store follows its atomics (an LDS spin, no barrier)
     // bounded (~2 ms) so that a broken release can only corrupt the wrenches, never hang the GPU
     for (int k = 0; k < (1 << 16) && *reinterpret_cast<volatile int*>(&L.done) <= it; ++k) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
@@ -1380,19 +1388,19 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
 // with several candidate envs set the step's tail: the physics wave waited 1.65 us per launch at R2 in the slowest 5 %
 // of the blocks against 0.13 in the median ones (light stamps, profiles/r5/r5t_*); the contact wave waits ~1.9 us
 // per launch there anyway
+// Only when the jobs outnumber the live lanes (the self wave's first pass): otherwise nothing, no release; the self wave
+// makes the same test (self_finish).  This wave's accumulator set is zeroed by the physics wave (self_acc_zero).
 H12_DEV void self_jobs_shared(const KParams& P, int it) {
   SelfLds& L = self_lds();
   const int ncand = L.ncand;
-  if (ncand) {
-    const int l = threadIdx.x & (BLOCK - 1);
-    for (int b = 0; b < 2; ++b)
-      for (int a = 0; a < 6; ++a) L.acc[1][b][a][l >> 1][l & 1] = 0.f;  // this wave's set, before its atomics
-    wave_sync();
-    const uint64_t live = __ballot(1);
-    const int nlive = __popcll(live);
-    const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-    self_jobs(P, ncand, nlive + me, 2 * nlive, 1);
-  }
+  if (!ncand) return;
+  bool ffonly;
+  const int njobs = self_njobs(ncand, ffonly);
+  const uint64_t live = __ballot(1);
+  const int nlive = __popcll(live);
+  if (njobs <= nlive) return;
+  const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+  self_jobs(P, njobs, ffonly, nlive + me, 2 * nlive, 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if ((threadIdx.x & 63) == 0) *reinterpret_cast<volatile int*>(&L.done) = it + 1;
 }
