@@ -1074,19 +1074,20 @@ H12_DEV bool capsules_near(const float* p1, const float* q1, const float* p2, co
   float d1[3], d2[3], r[3];
   for (int a = 0; a < 3; ++a) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
   const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, r), C = dot3(d1, r), B = dot3(d1, d2);
-  const float den = A * E - B * B, iA = frcp(A);
-  float s, slack = 0.f;
-  if (den > 1e-3f * A * E) {
-    s = fminf(fmaxf((B * F - C * E) * frcp(den), 0.f), 1.f);
-  } else {
-    const float t0 = -C * iA, t1 = (B - C) * iA;
-    const float lo = fmaxf(0.f, fminf(t0, t1)), hi = fminf(1.f, fmaxf(t0, t1));
-    s = fminf(fmaxf(0.5f * (lo + hi), 0.f), 1.f);
-    slack = 0.5f * fmaxf(hi - lo, 0.f) * fsqrt(fmaxf(den, 0.f) * frcp(E)) + 1e-4f;
-  }
-  float t = (B * s + F) * frcp(E);
-  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-C * iA, 0.f), 1.f); }
-  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((B - C) * iA, 0.f), 1.f); }
+  // branch-free (both cases evaluated, then selected): the broad phase runs every inner step, and standing legs
+  // (parallel knees) put both cases in most waves
+  const float den = A * E - B * B, iA = frcp(A), iE = frcp(E);
+  const bool gen = den > 1e-3f * A * E;
+  const float sgen = fminf(fmaxf((B * F - C * E) * frcp(gen ? den : 1.f), 0.f), 1.f);
+  const float t0 = -C * iA, t1 = (B - C) * iA;
+  const float lo = fmaxf(0.f, fminf(t0, t1)), hi = fminf(1.f, fmaxf(t0, t1));
+  const float spar = fminf(fmaxf(0.5f * (lo + hi), 0.f), 1.f);
+  const float slack = gen ? 0.f : 0.5f * fmaxf(hi - lo, 0.f) * fsqrt(fmaxf(den, 0.f) * iE) + 1e-4f;
+  float s = gen ? sgen : spar;
+  float t = (B * s + F) * iE;
+  const float s_lo = fminf(fmaxf(t0, 0.f), 1.f), s_hi = fminf(fmaxf(t1, 0.f), 1.f);
+  s = t < 0.f ? s_lo : (t > 1.f ? s_hi : s);
+  t = fminf(fmaxf(t, 0.f), 1.f);
   const float dv[3] = {r[0] + d1[0] * s - d2[0] * t, r[1] + d1[1] * s - d2[1] * t, r[2] + d1[2] * s - d2[2] * t};
   const float reach = rr + slack;
   return dot3(dv, dv) < reach * reach;
