@@ -2396,11 +2396,12 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   float R0[3][3];
   quat_R(b.quat, R0);
   float ag[6] = {0.f, 0.f, 0.f, -P.g * R0[2][0], -P.g * R0[2][1], -P.g * R0[2][2]};
+  // (lane 1's hand-offs hold zeros here -- the helper wave writes the base body's bias force and the torso contact on
+  // lane 0 only -- so both lanes run this without a branch; the base body's rigid inertia (dmass: an env-level value,
+  // the same in both lanes) is added after the pair sum)
   ImplC ict;  // torso contact linearisation (lane 0)
   float corner[3];
-  ict.beta = ict.gamma = 0.f;
-  if (leg == 0) {
-    ai_add(IA, Rg);
+  {
     for (int i = 0; i < 6; ++i) pAcc[i] += pbase[i];
     torso_corner(R0, corner);
     float t[16];
@@ -2422,6 +2423,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     for (int i = 0; i < 6; ++i) { IB.A[i] = comb(IA.A[i]); IB.C[i] = comb(IA.C[i]); pB[i] = comb(pAcc[i]); }
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) IB.B[i][j] = comb(IA.B[i][j]);
+    ai_add(IB, Rg);
   }
   // branch-free (the fixed base selects afterwards): the pair sums stay in the solve's block, where each DPP swap folds
   // into its add
@@ -2458,14 +2460,13 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     get4(&H.cw1[0][7], threadIdx.x, r[0], 4);  // floats 28..43 of each half: the report at 30..
     get4(&H.cw1[1][7], threadIdx.x, r[1], 4);
     if constexpr (!Feat<K>::terrain) {
+      // without a branch: a sole out of contact reports zero sums (sole_handoff)
       SoleSums ss;
       ss.sb = r[0][2] + r[1][2];
       ss.sg = r[0][3] + r[1][3];
-      if (ss.sb + ss.sg > 0.f) {
-        for (int i = 0; i < 3; ++i) { ss.pb[i] = r[0][4 + i] + r[1][4 + i]; ss.pg[i] = r[0][7 + i] + r[1][7 + i]; }
-        const float Rf[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {r[0][10], r[0][11], r[0][12]}};
-        sole_impl_force_flat(ah, Rf, ss, fr.foot);
-      }
+      for (int i = 0; i < 3; ++i) { ss.pb[i] = r[0][4 + i] + r[1][4 + i]; ss.pg[i] = r[0][7 + i] + r[1][7 + i]; }
+      const float Rf[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {r[0][10], r[0][11], r[0][12]}};
+      sole_impl_force_flat(ah, Rf, ss, fr.foot);
     } else {
 #pragma unroll
       for (int q = 0; q < H12_NFOOT_PTS; ++q) {
