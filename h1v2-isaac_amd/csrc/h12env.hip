@@ -167,6 +167,13 @@ __device__ unsigned long long g_bw[1024][4][16];
   unsigned long long _bw[18] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_readcyclecounter(),       \
                                 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, __builtin_amdgcn_s_memrealtime()}
 #define H12_BW_PARAM , unsigned long long (&_bw)[18]
+// every wave's very first instruction (s_memrealtime; before any kernel-argument load), [block][wave]
+__device__ unsigned long long g_kstart[1024][4];
+#define H12_BW_KSTART()                                                          \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                            \
+      g_kstart[blockIdx.x][threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 // the physics wave's start stamp taken at its entry (its H12_BW_DECL follows the state loads)
 #define H12_BW_ENTRY() const unsigned long long _bw_entry = __builtin_amdgcn_s_memrealtime()
 #define H12_BW_SET_ENTRY() (_bw[17] = _bw_entry)
@@ -202,6 +209,7 @@ __device__ unsigned long long g_bw[1024][4][16];
 #else
 #define H12_BW_DECL (void)0
 #define H12_BW_ENTRY() (void)0
+#define H12_BW_KSTART() (void)0
 #define H12_BW_SET_ENTRY() (void)0
 #define H12_BW_PARAM
 #define H12_BW_ARG
@@ -3634,6 +3642,7 @@ H12_DEV void kernarg_warm() {
 
 template <int K>
 __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
+  H12_BW_KSTART();
   kernarg_warm();
   if (threadIdx.x >= BLOCK) {  // the helper waves (inner_step_hw, helper_wave, contact_wave, self_wave)
     const int nsteps = P.decimation * P.inner;
@@ -5163,6 +5172,11 @@ int h12env_phase_profile(unsigned long long* out16, int clear) {
 int h12env_barrier_waits(unsigned long long* out, int nblocks) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bw), sizeof(unsigned long long) * 64 * (size_t)nblocks));
+  return 0;
+}
+int h12env_kernel_starts(unsigned long long* out, int nblocks) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kstart), sizeof(unsigned long long) * 4 * (size_t)nblocks));
   return 0;
 }
 #endif

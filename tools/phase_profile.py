@@ -88,6 +88,9 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
         bws = []
         has_bw = hasattr(lib, "h12env_barrier_waits")
         bwbuf = (C.c_ulonglong * (64 * waves))()
+        has_ks = hasattr(lib, "h12env_kernel_starts")
+        ksbuf = (C.c_ulonglong * (4 * waves))()
+        kss = []
         for t in range(40):
             env.step(acts[t])
             torch.cuda.synchronize()
@@ -95,6 +98,9 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
             if has_bw:  # light build: per block, role (physics, helper, contact, self) and barrier (S, R1, R2, first S)
                 lib.h12env_barrier_waits(bwbuf, waves)
                 bws.append(np.frombuffer(bwbuf, dtype=np.uint64).reshape(waves, 4, 16).astype(np.float64) / 2370.0)
+            if has_ks:  # every wave's first instruction (s_memrealtime ticks, 100 MHz)
+                lib.h12env_kernel_starts(ksbuf, waves)
+                kss.append(np.frombuffer(ksbuf, dtype=np.uint64).reshape(waves, 4).astype(np.float64) / 100.0)
             full = np.frombuffer(wt, dtype=np.uint64).reshape(waves, 11).astype(np.int64)
             bw.append(full[:, 9:11] / 2370.0)  # barrier-wait cycles -> us at the measured clock
             clk.append((full[:, 8] - full[:, 7]) / np.maximum(1, full[:, 2] - full[:, 0]) * 100.0)  # MHz
@@ -175,6 +181,20 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
                 role: round(float(np.median(St[:, r])), 3) for r, role in enumerate(("physics", "helper", "contact", "self"))}
             res["wave_start_after_first_us_p90"] = {
                 role: round(float(np.quantile(St[:, r], 0.9)), 3) for r, role in enumerate(("physics", "helper", "contact", "self"))}
+            if kss:
+                K = np.concatenate(kss)  # (launches x blocks, 4) us
+                q = lambda x: [round(float(np.quantile(x, p)), 3) for p in (0.05, 0.5, 0.95, 1.0)]
+                n_l = len(kss)
+                Kb = K.min(1).reshape(n_l, -1)
+                res["block_first_instruction_after_first_block_us_q"] = q((Kb - Kb.min(1, keepdims=True)).ravel())
+                res["wave_first_instruction_after_block_first_us_median"] = {
+                    role: round(float(np.median(K[:, r] - K.min(1))), 3)
+                    for r, role in enumerate(("physics", "helper", "contact", "self"))}
+                # role start (slot 15: the physics wave's entry after its argument loads, the other roles' function
+                # start) after the wave's own first instruction
+                res["role_start_after_first_instruction_us_median"] = {
+                    role: round(float(np.median(B[:, r, 15] * 2370.0 / 100.0 - K[:, r])), 3)
+                    for r, role in enumerate(("physics", "helper", "contact", "self"))}
             # who arrives last at barrier F (slot 11: s_memrealtime at the arrival, 100 MHz): per block, each role's
             # arrival after the first one's
             Fa = B[:, :, 11] * 2370.0 / 100.0  # back to realtime ticks, then us
