@@ -1235,7 +1235,7 @@ H12_DEV void self_stage_slots(int leg, uint64_t act, int flags) {
   }
   wave_sync();
 }
-// zero_acc false (step_kernel): the physics wave has zeroed this lane's accumulators before R1 (self_acc_zero)
+// zero_acc false (step_kernel): the helper wave has zeroed this lane's accumulators after the previous R2 (self_acc_zero)
 // early (step_kernel): the staging's LDS writes are issued ahead of the broad phase's tests, which they then overlap
 // (in a wave without candidates they go unread)
 H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
@@ -1252,8 +1252,9 @@ H12_DEV uint64_t self_stage(const KParams& P, int leg, float mu, const float (&R
   self_stage_slots(leg, act, flags);
   return act;
 }
-// step_kernel's physics wave before R1 (it waits there for the helper waves): both accumulator sets (self and contact
-// wave) of this lane's env and leg, zeroed for the inner step's jobs (the previous step's were read before its R2)
+// both accumulator sets (self and contact wave) of this lane's env and leg, zeroed for the next inner step's jobs:
+// step_kernel's helper wave, before its first inner step and after each barrier R2 (the sums were read before it),
+// in its idle wait for barrier S (on the physics wave before R1 they made it the last wave there, r6x_light.json)
 H12_DEV void self_acc_zero() {
   SelfLds& L = self_lds();
   const int l = threadIdx.x & (BLOCK - 1);
@@ -1348,7 +1349,7 @@ H12_DEV void self_jobs(const KParams& P, int njobs, bool ffonly, int g0, int str
 // Self-contact wrenches on this lane's knee (wk) and foot (wf), body coords of the lane frame; their forces are
 // added to the reported knee / foot contact forces (fr).  act: self_stage's result.  shared (step_kernel): the contact
 // wave runs every other 64-job pass of the inner step it (self_jobs_shared) into its own accumulator set (zeroed with
-// this wave's by the physics wave, self_acc_zero), and when there is such a pass (more jobs than live lanes) its
+// this wave's by the helper wave, self_acc_zero), and when there is such a pass (more jobs than live lanes) its
 // release (L.done > it) is awaited.
 H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&Rk)[3][3], const float* pk,
                          const float (&Rf)[3][3], const float* pf, float* wk, float* wf, Forces& fr,
@@ -1398,7 +1399,7 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
 // of the blocks against 0.13 in the median ones (light stamps, profiles/r5/r5t_*); the contact wave waits ~1.9 us
 // per launch there anyway
 // Only when the jobs outnumber the live lanes (the self wave's first pass): otherwise nothing, no release; the self wave
-// makes the same test (self_finish).  This wave's accumulator set is zeroed by the physics wave (self_acc_zero).
+// makes the same test (self_finish).  This wave's accumulator set is zeroed by the helper wave (self_acc_zero).
 H12_DEV void self_jobs_shared(const KParams& P, int it) {
   SelfLds& L = self_lds();
   const int ncand = L.ncand;
@@ -1928,6 +1929,7 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
     H.rnd[k][l] = make_uint4(r[0], r[1], r[2], r[3]);
   };
   Leg lg;
+  if (P.self_coll) self_acc_zero();
   H12_BW_DECL;
   for (int it = 0; it < n_steps; ++it) {
     SYNC_W(it ? 0 : 3);  // S: the state of this inner step
@@ -1966,6 +1968,7 @@ H12_DEV void helper_wave(const KParams& P, int n, int n_steps, uint32_t g, uint3
     SYNC_W(2);  // R2: bias forces (flat: torso contact)
     fuse_early(fc, it, n_steps, l, helper_threads(P));
     if (it < 4) draw(it);
+    if (P.self_coll) self_acc_zero();
   }
   for (int k = n_steps; k < 4; ++k) draw(k);
   H12_BW_STORE();
@@ -2306,7 +2309,6 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
     joint_terms(P, lg, h, tq, dl);
     for (int k = 0; k < NL; ++k) tau[k] = tau_pd[k] + tq[k];
   }
-  if (P.self_coll) self_acc_zero();
   PHX(10);
   SYNC_W(1);  // R1: sole contacts (helper), knee contact (contact wave)
   PHX(8);
