@@ -207,12 +207,12 @@ def cpu_baseline(seconds: float):
     q0 = np.asarray(model.q_default)
     t1 = time.perf_counter()
     for k in range(1000):
-        q_ref = q0 + 0.25 * rng.normal(size=12) * 0.2
+        q_ref = q0 + 0.25 * rng.normal(size=12)  # q_ref = q0 + 0.25 a, a ~ N(0, 1)
         s, _ = O.mujoco_rollout(model, mc, s, q_ref, 20, contact=True, algo=1)
     dt1 = time.perf_counter() - t1
     mujoco = {"value": 1000 / dt1, "unit": "env-steps/s", "cores": 1,
               "sample": "C1: oracle MuJoCo mode (sim2sim semantics), 1 env x 1000 policy steps x 20 substeps, "
-                        f"random q_ref, ground contact ({dt1:.2f} s)"}
+                        f"q_ref = q0 + 0.25 a with a ~ N(0, 1) per policy step, ground contact ({dt1:.2f} s)"}
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "cpus_available": avail,
             "single_env_sim2sim": mujoco,

@@ -295,6 +295,10 @@ struct KParams {
   float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
   int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised
+  // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
+  // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial
+  int* diag;
+  int dbg_norel;          // test hook (H12_TEST_SKIP_SELF_RELEASE=1 at h12env_create): the contact wave never releases
 };
 
 // CaT constraint columns (ConstraintsCfg order, cat_env_cfg.py:336-427) and the scratch rows after them
@@ -1368,9 +1372,11 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   self_jobs(P, njobs, ffonly, me, shared ? 2 * nlive : nlive, 0);
   const bool sj = shared && njobs > nlive;  // the contact wave has jobs (self_jobs_shared)
   if (sj) {  // the contact wave's jobs: its release store follows its atomics (an LDS spin, no barrier)
-    // bounded (~2 ms) so that a broken release can only corrupt the wrenches, never hang the GPU
+    // bounded (~2 ms) so that a broken release can never hang the GPU; a wait that ends at the bound unreleased is
+    // raised in the device diagnostic word, which h12env_check reports (the wrenches of that inner step may be partial)
     for (int k = 0; k < (1 << 16) && *reinterpret_cast<volatile int*>(&L.done) <= it; ++k) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
+    if (*reinterpret_cast<volatile int*>(&L.done) <= it && (threadIdx.x & 63) == 0) atomicOr(P.diag, 1);
   }
   wave_sync();
   // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
@@ -1412,7 +1418,7 @@ H12_DEV void self_jobs_shared(const KParams& P, int it) {
   const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
   self_jobs(P, njobs, ffonly, nlive + me, 2 * nlive, 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) *reinterpret_cast<volatile int*>(&L.done) = it + 1;
+  if ((threadIdx.x & 63) == 0 && !P.dbg_norel) *reinterpret_cast<volatile int*>(&L.done) = it + 1;
 }
 
 H12_DEV void self_contacts(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
@@ -1545,7 +1551,8 @@ H12_DEV void fuse_drain(const FuseCtx& f, int it) {
 // CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the contact wave's
 // R1 hand-off array (free once the last inner step's physics wave has read it)
 typedef float CatLds[H12_NCSTR_COLS + 1][ENVS_PER_BLOCK];
-static_assert(sizeof(CatLds) <= sizeof(HelpLds::cw1), "CaT values fit the contact hand-off array");
+// only the first half: cw1[1] holds the reward inputs (put_rin), written in the same window before barrier L
+static_assert(sizeof(CatLds) <= sizeof(HelpLds::cw1[0]), "CaT values fit the first sole hand-off half");
 H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().cw1[0][0][0]); }
 // Hand-off arrays between the waves of a block: declared as float4 [n4][BLOCK], used FIELD-MAJOR as float [4 n4][BLOCK]
 // (value i of lane l at i * 256 + 4 l bytes): the writes / reads pair into ds_write2_b32 / ds_read2_b32 with two
@@ -1765,7 +1772,7 @@ H12_DEV void knee_handoff(const KParams& P, int l, int leg, const float (&Rk)[3]
 // the lowest corner touches: their heightfield lookups stay off a standing robot's helper wave) --
 // the face whose normal is the box axis closest to the vertical -- add their explicit forces (torso_face), so a torso
 // lying on a face or an edge is carried by that face's corners (oracle contacts(), the same corners in the same
-// order).  Evaluated by helper_torso: the helper wave before R1 on terrain, the contact wave between R1 and R2 on flat
+// order).  Evaluated by helper_torso: the contact wave before R1 on terrain, the helper wave between R1 and R2 on flat
 // ground.
 H12_DEV void torso_corner(const float (&R0)[3][3], float* corner) {
   for (int a = 0; a < 3; ++a) corner[a] = h12m::TORSO_C[a] + (R0[2][a] > 0.f ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
@@ -3642,6 +3649,15 @@ H12_DEV void kernarg_warm() {
       : "memory");
 }
 
+// LDS budget of step_kernel (round 6): the static hand-offs (HelpLds, SelfLds; the same for every feature level K) plus
+// the fused path's dynamic FuseLds must fit the CU's 160 KiB.  A dispatch over the limit is not a HIP error code: the
+// queue aborts (HSA_STATUS_ERROR_INVALID_ALLOCATION) and the next call reports an illegal address (round 5's r7e
+// variant, group_seg_size 166416).  Checked here at compile time and at h12env_create against the compiled kernel's
+// static size and the device's limit (check_step_lds), which refuses the handle with H12_E_STATE instead.
+constexpr size_t LDS_CU_BYTES = 160 * 1024;
+constexpr size_t STEP_LDS_STATIC = sizeof(HelpLds) + sizeof(SelfLds);
+static_assert(STEP_LDS_STATIC + sizeof(FuseLds) <= LDS_CU_BYTES, "step_kernel's static + fused dynamic LDS exceed 160 KiB");
+
 template <int K>
 __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W, StepArgs A) {
   H12_BW_KSTART();
@@ -4318,7 +4334,9 @@ struct Handle {
   uint64_t reset_calls, observe_calls;
   double flops_per_env;
   float* frame;  // [45][n] observation frame scratch between the env kernels and obs_assemble_kernel
-  int* dz_cnt = nullptr;  // 3 rotating deadzone counters (UniformVelocityCommandWithDeadzone)
+  int* dz_cnt = nullptr;  // 3 rotating deadzone counters (UniformVelocityCommandWithDeadzone), then the diagnostic word
+  size_t lds_static = 0;  // step_kernel's static LDS as compiled (hipFuncGetAttributes) and the device's LDS per CU
+  int lds_limit = 0;
   uint64_t dz_step = 0;
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
@@ -4613,6 +4631,30 @@ int feature_level(const KParams& P) {
     }                                                                                                       \
   } while (0)
 
+// step_kernel's LDS against the device (see LDS_CU_BYTES): the compiled kernel's static size plus the fused path's
+// dynamic FuseLds; H12_E_STATE when they exceed the device's LDS per CU
+int check_step_lds(Handle* h) {
+  hipFuncAttributes fa = {};
+  hipError_t e;
+  switch (feature_level(h->P)) {
+    case 0: e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&step_kernel<0>)); break;
+    case 1: e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&step_kernel<1>)); break;
+    default: e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&step_kernel<2>)); break;
+  }
+  if (e != hipSuccess) return set_err(H12_E_HIP, "hipFuncGetAttributes(step_kernel): %s", hipGetErrorString(e));
+  int lim = 0;
+  if (hipDeviceGetAttribute(&lim, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device) != hipSuccess ||
+      lim <= 0)
+    lim = (int)LDS_CU_BYTES;
+  h->lds_static = fa.sharedSizeBytes;
+  h->lds_limit = lim;
+  const size_t dyn = h->fuse ? sizeof(FuseLds) : 0;
+  if (fa.sharedSizeBytes + dyn > (size_t)lim)
+    return set_err(H12_E_STATE, "step_kernel needs %zu B of LDS (%zu static + %zu dynamic), the device has %d per CU",
+                   fa.sharedSizeBytes + dyn, fa.sharedSizeBytes, dyn, lim);
+  return 0;
+}
+
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
@@ -4806,8 +4848,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     delete h;
     return set_err(H12_E_ALLOC, "hipMalloc(frame): %s", hipGetErrorString(e));
   }
-  e = hipMalloc(&h->dz_cnt, 3 * sizeof(int));
-  if (e == hipSuccess) e = hipMemset(h->dz_cnt, 0, 3 * sizeof(int));
+  e = hipMalloc(&h->dz_cnt, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(h->dz_cnt, 0, 4 * sizeof(int));
   const size_t log_bytes = sizeof(float) * LOG_RING * LOG_NPART * (size_t)((n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK);
   if (e == hipSuccess) e = hipMalloc(&h->log_part, log_bytes);
   if (e == hipSuccess) e = hipMemset(h->log_part, 0, log_bytes);
@@ -4818,6 +4860,11 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     return set_err(H12_E_ALLOC, "hipMalloc(dz_cnt): %s", hipGetErrorString(e));
   }
   h->P.dz_cnt = h->dz_cnt;
+  h->P.diag = h->dz_cnt + 3;
+  {
+    const char* nr = getenv("H12_TEST_SKIP_SELF_RELEASE");
+    h->P.dbg_norel = nr && nr[0] == '1';
+  }
   if (h->P.cat) {
     const size_t nn = (size_t)n_envs;
     const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
@@ -4861,6 +4908,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
         return set_err(H12_E_ALLOC, "fused-assembly code table: %s", hipGetErrorString(e));
       }
     }
+  }
+  if (int rc = check_step_lds(h)) {
+    h12env_destroy((h12env*)h);
+    return rc;
   }
   h->env_offset = env_offset;
   h->reset_calls = 0;
@@ -5273,6 +5324,27 @@ int h12env_step_cost(const h12env* hh, double* bytes_per_env, double* flops_per_
   if (bytes_per_env) *bytes_per_env = b0 + b1 - 2.0 * fr;
   if (flops_per_env) *flops_per_env = f0 + f1;
   return 0;
+}
+
+int h12env_step_lds(const h12env* hh, size_t* static_bytes, size_t* dynamic_bytes, size_t* limit_bytes) {
+  const Handle* h = (const Handle*)hh;
+  if (static_bytes) *static_bytes = h ? h->lds_static : STEP_LDS_STATIC;
+  if (dynamic_bytes) *dynamic_bytes = (!h || h->fuse) ? sizeof(FuseLds) : 0;
+  if (limit_bytes) *limit_bytes = h ? (size_t)h->lds_limit : LDS_CU_BYTES;
+  return 0;
+}
+
+int h12env_check(h12env* hh, void* stream) {
+  Handle* h = (Handle*)hh;
+  if (!h) return set_err(H12_E_ARG, "null handle");
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  int d = 0;
+  HIP_TRY(hipMemcpy(&d, h->P.diag, sizeof(int), hipMemcpyDeviceToHost));
+  if (!d) return 0;
+  HIP_TRY(hipMemset(h->P.diag, 0, sizeof(int)));
+  return set_err(H12_E_STATE,
+                 "self-contact: a wait for the contact wave's release ended at its bound (diagnostic 0x%x) since the "
+                 "last check; the self-contact wrenches of that inner step may be partial", (unsigned)d);
 }
 
 int h12env_obs_fused(const h12env* hh) {

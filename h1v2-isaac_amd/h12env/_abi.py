@@ -258,6 +258,10 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_step.restype = C.c_int
     lib.h12env_flush_log.argtypes = [vp, vp]
     lib.h12env_flush_log.restype = C.c_int
+    lib.h12env_step_lds.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+    lib.h12env_step_lds.restype = C.c_int
+    lib.h12env_check.argtypes = [vp, vp]
+    lib.h12env_check.restype = C.c_int
     lib.h12env_obs_fused.argtypes = [vp]
     lib.h12env_obs_fused.restype = C.c_int
     lib.h12env_observe.argtypes = [vp, vp, vp, vp, vp]
@@ -329,5 +333,5 @@ EXPORTED_SYMBOLS = [
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
     "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms", "h12env_eval_self_contacts",
     "h12env_rollout_layout", "h12env_rollout_decode", "h12env_fence_create", "h12env_fence_destroy",
-    "h12env_fence_signal", "h12env_fence_wait",
+    "h12env_fence_signal", "h12env_fence_wait", "h12env_step_lds", "h12env_check",
 ]

@@ -558,7 +558,7 @@ class H12VelocityEnv:
         if rc:
             check(self._lib, rc, "h12env_step")
         log = _LazyLog(self._log_ring, slot, self.max_episode_length_s, self._reward_terms, self._reward_map,
-                       self._cstr_terms, self._log_extra, _LOG_LOOKBACK, self._flush_log)
+                       self._cstr_terms, self._log_extra, _LOG_LOOKBACK, self._flush_and_check)
         self._live_logs[self.common_step_counter] = weakref.ref(log)
         self.extras = {"log": log, "time_outs": self.reset_time_outs}
         obs_out = obs.clone() if self.obs_copy else obs
@@ -674,12 +674,28 @@ class H12VelocityEnv:
         if not self._closed:
             check(self._lib, self._lib.h12env_flush_log(self._h, _raw_stream(self._dev_index)), "h12env_flush_log")
 
+    def check_device(self):
+        """Synchronise and read the library's device diagnostic word (h12env_check): raises H12EnvError when a
+        self-contact wait in the step kernel ended at its bound since the last check (that inner step's self-contact
+        wrenches may be partial; H12EnvError is a RuntimeError).  Called where the host synchronises anyway:
+        episode-log reads and close()."""
+        if not self._closed:
+            check(self._lib, self._lib.h12env_check(self._h, _raw_stream(self._dev_index)), "h12env_check")
+
+    def _flush_and_check(self):
+        self._flush_log()
+        self.check_device()
+
     def close(self):
         if not self._closed:
             self._flush_log()  # logs still referenced (extras) stay complete
             torch.cuda.synchronize(self.device)
+            rc = self._lib.h12env_check(self._h, _raw_stream(self._dev_index))
+            msg = self._lib.h12env_last_error().decode() if rc else ""
             self._lib.h12env_destroy(self._h)
             self._closed = True
+            if rc:
+                raise _abi.H12EnvError(f"h12env_check failed ({rc}): {msg}")
 
     def __del__(self):
         try:

@@ -435,6 +435,17 @@ int h12env_kernel_cost(const h12env* h, int kernel, double* bytes_per_env, doubl
  * h12env_kernel_times synchronises on the last event, returns the summed milliseconds of each kernel and
  * the number of timed steps, and clears the record. */
 int h12env_set_kernel_timing(h12env* h, int enable);
+/* step_kernel's LDS budget (round 6): static hand-off bytes, the fused observation path's dynamic bytes and the
+ * limit per CU.  With h = NULL the values compiled into the library (a compile-time assert holds static + dynamic
+ * <= 160 KiB); with a handle the compiled kernel's static size (hipFuncGetAttributes), the dynamic bytes its step
+ * launches use and the device's LDS per CU -- h12env_create refuses a configuration over the limit with
+ * H12_E_STATE instead of letting the dispatch abort the queue.  No reference counterpart (PhysX sizes its own). */
+int h12env_step_lds(const h12env* h, size_t* static_bytes, size_t* dynamic_bytes, size_t* limit_bytes);
+/* Synchronises the stream and reads / clears the device diagnostic word: H12_E_STATE with a message when a
+ * self-contact wait in step_kernel ended at its bound since the last check (that inner step's self-contact
+ * wrenches may be partial), else 0.  The Python host calls it when it already synchronises (episode-log reads,
+ * close).  No reference counterpart (PhysX reports solver failures through its own error callback). */
+int h12env_check(h12env* h, void* stream);
 int h12env_kernel_times(h12env* h, double* env_ms, double* obs_ms, int* n_steps);
 const char* h12env_last_error(void);
 int h12env_abi_version(void);

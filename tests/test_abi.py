@@ -43,6 +43,23 @@ def test_state_bytes_and_abi():
     assert lib.h12env_state_bytes(4096) == (143 + 3) * 4 * 4096
 
 
+def test_step_kernel_lds_budget():
+    """step_kernel's static LDS hand-offs plus the fused observation path's dynamic FuseLds fit the CU's 160 KiB
+    (h12env_step_lds with no handle: the sizes compiled into the library; a compile-time assert holds the same
+    bound, and h12env_create re-checks it against the compiled kernel and the device).  Round 5's r7e variant
+    went 2.5 KiB over and aborted the queue at dispatch; the margin asserted here is what a hand-off change
+    may still add."""
+    lib = load_library()
+    st, dy, lim = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    assert lib.h12env_step_lds(None, C.byref(st), C.byref(dy), C.byref(lim)) == 0
+    assert lim.value == 160 * 1024
+    assert st.value > 0 and dy.value > 0
+    margin = lim.value - (st.value + dy.value)
+    print(f"step_kernel LDS: {st.value} static + {dy.value} dynamic = {st.value + dy.value} of {lim.value}"
+          f" (margin {margin} B)")
+    assert margin >= 1024, margin
+
+
 def test_config_default_equals_python_cfg():
     lib = load_library()
     c = H12Config()

@@ -178,3 +178,36 @@ def test_self_contact_wrenches_match_oracle(gpu, task):
     assert worst.max() <= BOUND, np.sort(worst)[-10:]
     assert flipped <= 0.01 * hit, flipped
     env.close()
+
+
+def test_self_contact_release_timeout_is_reported(gpu, monkeypatch):
+    """the self wave's wait for the contact wave's release (the shared self-contact jobs of a block with
+    more jobs than lanes) is bounded; a wait that ends at the bound unreleased must surface, not silently leave
+    partial wrenches.  With the test hook H12_TEST_SKIP_SELF_RELEASE=1 the contact wave never releases, so every
+    such inner step ends at the bound: h12env_check (env.check_device) must raise.  The same states without the
+    hook report nothing."""
+    from h12env._abi import H12EnvError
+
+    n = 256
+    for skip in (False, True):
+        if skip:
+            monkeypatch.setenv("H12_TEST_SKIP_SELF_RELEASE", "1")
+        else:
+            monkeypatch.delenv("H12_TEST_SKIP_SELF_RELEASE", raising=False)
+        env = make(n)
+        monkeypatch.delenv("H12_TEST_SKIP_SELF_RELEASE", raising=False)  # read at create only
+        env.reset()
+        rng = np.random.default_rng(44)
+        Fm = crossed_states(env, rng, 1.02, roll=(-0.4, -0.2), qd=0.5)
+        env._fstate.copy_(torch.from_numpy(Fm))
+        a = np.zeros((n, 12), np.float32)
+        a[:, 2] -= 0.5
+        a[:, 8] += 0.5
+        env.step(torch.from_numpy(a).cuda())
+        if skip:
+            with pytest.raises(H12EnvError, match="release"):
+                env.check_device()
+            env.check_device()  # the word is cleared by the read
+        else:
+            env.check_device()
+        env.close()

@@ -75,6 +75,30 @@ PATCHES = {
                ": 0x3fffffff;", 2)],
 }
 PATCHES_HEAD: dict = {
+    # round 6: 16 envs per block on the current kernel (256 blocks at 4096 envs, one per CU, the upper half of every wave
+    # idle): round 4's epb16 re-expressed for the round-5 kernel (four waves, shared self-contact jobs, fused rows)
+    "epb16h": [("constexpr int ENVS_PER_BLOCK = 32;", "constexpr int ENVS_PER_BLOCK = 16;"),
+               ("  const bool active = step_block() * ENVS_PER_BLOCK + (l >> 1) < n;",
+                "  const bool active = (l >> 1) < ENVS_PER_BLOCK && step_block() * ENVS_PER_BLOCK + (l >> 1) < n;", 3),
+               ("      const int he = step_block() * ENVS_PER_BLOCK + (hl >> 1);",
+                "      const int he = (hl >> 1) < ENVS_PER_BLOCK ? step_block() * ENVS_PER_BLOCK + (hl >> 1) : 0x3fffffff;"),
+               ("  const int e = e0 + lane_pair;",
+                "  const int e = lane_pair < ENVS_PER_BLOCK ? e0 + lane_pair : 0x3fffffff;", 3),
+               ("  const int e = blockIdx.x * ENVS_PER_BLOCK + lane_pair;",
+                "  const int e = lane_pair < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + lane_pair : 0x3fffffff;"),
+               ("  const int e = blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1);",
+                "  const int e = (threadIdx.x >> 1) < ENVS_PER_BLOCK ? blockIdx.x * ENVS_PER_BLOCK + (threadIdx.x >> 1) "
+                ": 0x3fffffff;", 2)],
+    # round 6 timing probe (results wrong): the physics wave's three link chains (inertia chain before R2, bias-force
+    # chain and pass 3 after it) over links 3-5 only -- half of the chains' work removed, the best case of splitting
+    # them over two lanes per leg with free exchanges.  "_h" = on the 32-env kernel, "epb16h_half" = on epb16h
+    "chain_half": [("  link_ia<2, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);\n"
+                    "  link_ia<1, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);\n"
+                    "  link_ia<0, true>(P, lg, cs, v, ick, knee_pz, dl, IA, U, Dinv, Ic, h);\n", ""),
+                   ("    link_p_pk<2>(cs, U, Dinv, tau, pb, p, u);\n    link_p_pk<1>(cs, U, Dinv, tau, pb, p, u);\n"
+                    "    link_p_pk<0>(cs, U, Dinv, tau, pb, p, u);\n", ""),
+                   ("  link_pass3_pk<0>(cs, U, Dinv, u, ap, qdd);\n  link_pass3_pk<1>(cs, U, Dinv, u, ap, qdd);\n"
+                    "  link_pass3_pk<2>(cs, U, Dinv, u, ap, qdd);\n", "  qdd[0] = qdd[1] = qdd[2] = 0.f;\n")],
     # probe: the episode sums loaded after the helper wave's loop (is their load the helper's delay at the first S?)
     "epsum_late": [("      if (he < W.n) load_epsum<K>(P, W, he, ep);\n      helper_wave<K>(P, W.n, nsteps, (uint32_t)(A.env_offset + he), A.lo, A.hi, fc);",
                     "      helper_wave<K>(P, W.n, nsteps, (uint32_t)(A.env_offset + he), A.lo, A.hi, fc);\n      if (he < W.n) load_epsum<K>(P, W, he, ep);")],
@@ -87,6 +111,26 @@ PATCHES_HEAD: dict = {
                                          ST_POL);""", """                                         __builtin_amdgcn_make_buffer_rsrc(dst, 0, -1, 0x00020000), j * 16, 0,
                                          0);""")],
 }
+PATCHES_HEAD["epb16h_half"] = PATCHES_HEAD["epb16h"] + PATCHES_HEAD["chain_half"]
+# round 6 timing probe: epb16h_half plus the lane exchanges a two-lanes-per-leg split puts on the chains, as identity
+# double swaps (two dependent DPP lane swaps) of the chains' own values -- per link 16 swaps in the inertia chain (U, C,
+# the shift correction: ~15 values a split hands over once each), 4 in the bias chain, 6 in pass 3
+_XS = ("H12_DEV float xs2(float x) { return pair_swap(pair_swap(x)); }\n"
+       "template <int LINK, bool AV = false, typename UT>\nH12_DEV void link_ia(")
+PATCHES_HEAD["epb16h_halfx"] = PATCHES_HEAD["epb16h_half"] + [
+    ("template <int LINK, bool AV = false, typename UT>\nH12_DEV void link_ia(", _XS),
+    ("  ai_rotate<A>(IA, cs[LINK][0], cs[LINK][1]);\n  ai_shift(IA, h12m::R[LINK]);\n",
+     "  ai_rotate<A>(IA, cs[LINK][0], cs[LINK][1]);\n"
+     "  for (int k = 0; k < 3; ++k) IA.C[k] = xs2(IA.C[k]);\n"
+     "  ai_shift(IA, h12m::R[LINK]);\n"
+     "  for (int k = 0; k < 2; ++k) IA.A[k] = xs2(IA.A[k]);\n"),
+    ("  float D = IA.A[A] + h12m::ARM[LINK]",
+     "  for (int k = 0; k < 3; ++k) Ua[k] = xs2(Ua[k]);\n  float D = IA.A[A] + h12m::ARM[LINK]"),
+    ("  const float ud = uu * Dinv[LINK];\n  f32x2 pa[3], q[3];\n",
+     "  const float ud = xs2(xs2(uu) * Dinv[LINK]);\n  f32x2 pa[3], q[3];\n"),
+    ("  const float x = (u[LINK] - (ua.x + ua.y)) * Dinv[LINK];\n",
+     "  const float x = xs2(xs2(u[LINK] - (xs2(ua.x) + ua.y)) * Dinv[LINK]);\n"),
+]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
