@@ -242,7 +242,27 @@ H12_DEV void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t
 }
 // single-instruction transcendental / reciprocal / sqrt (v_sin, v_cos, v_rcp, v_sqrt: ~1 ulp, no
 // range-reduction or Newton sequences; arguments here are joint angles and positive magnitudes)
-H12_DEV void fsincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+//
+// fsincos (round 6): the hardware sine / cosine with their radial bias removed.  __sinf / __cosf (v_mul by fp32(1/2pi),
+// v_sin_f32 / v_cos_f32) carry two systematic errors on MI355X (tools/probe/hw_trig_table.hip, profiles/r6/r6e_*):
+// the constant fp32(1/2pi) is 4.03e-8 (relative) low, so every angle comes out 4.03e-8 x smaller; and the results lie
+// 3.2e-8 inside the unit circle at every angle (a round-down of ~0.3-0.5 ulp).  The second one shortens every rotated
+// link offset by 3.2e-8 per joint: it is what the fp32 oracle with that error table reproduces as the kernel's signed
+// bias in the sole scenarios (the feet a few 1e-8 m high, weaker support: stance VLIN2 -1.75e-6, z = -144; DESIGN.md
+// section 4, tools/bias_attrib.py); the angle error alone moves nothing measurable there.  So each (sin, cos) pair is
+// put back on the unit circle to first order: d = s^2 + c^2 - 1 from two fma (their one rounding is zero-mean), then
+// (s, c)(1 - d / 2): +5 VALU per call.  fsincos_hw: the uncorrected pair (the self-contact wave's pass 1, where the
+// step's most critical wave before barrier R1 would pay for it and a 3e-8 shift of a leg-leg contact point moves
+// nothing a gate sees).
+H12_DEV void fsincos_hw(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+H12_DEV void fsincos(float x, float* s, float* c) {
+  float sv, cv;
+  fsincos_hw(x, &sv, &cv);
+  const float d = __builtin_fmaf(cv, cv, __builtin_fmaf(sv, sv, -1.f));
+  const float k = -0.5f * d;
+  *s = __builtin_fmaf(sv, k, sv);
+  *c = __builtin_fmaf(cv, k, cv);
+}
 H12_DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 H12_DEV float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 

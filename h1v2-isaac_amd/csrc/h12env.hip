@@ -516,13 +516,21 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   return true;
 }
 
+// The rotation increment r = (cos a, w sin(a) / |w|), a = |w| h / 2, as Taylor polynomials in a^2 (round 6): the
+// hardware sine of these small angles (1e-5 .. 0.05) is +3.7 ulp high on average (profiles/r6/r6d_hw_math_bias.txt),
+// a signed error that turned every orientation increment 3e-7 (relative) too large; the series is exact to fp32 for
+// a <= 0.5 (|w| <= 200 rad/s at h = 5 ms; the truncation error there is 2.4e-11 in sin a / a, 2.7e-10 in cos a) and
+// needs no square root or reciprocal.  w = 0 leaves q as it is (the oracle's rule)
 H12_DEV void quat_integrate(float* q, const float* w, float h) {
-  float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  const float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   if (w2 > 0.f) {
-    float wn = fsqrt(w2);
-    float sh, ch;
-    fsincos(0.5f * wn * h, &sh, &ch);
-    sh *= frcp(wn);
+    const float a2 = w2 * (0.25f * h * h);
+    // sin(a) / a and cos(a) to a^8
+    const float sa = __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, 1.f / 362880.f,
+                                    -1.f / 5040.f), 1.f / 120.f), -1.f / 6.f), 1.f);
+    const float ch = __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, 1.f / 40320.f,
+                                    -1.f / 720.f), 1.f / 24.f), -0.5f), 1.f);
+    const float sh = sa * (0.5f * h);
     float r[4] = {ch, w[0] * sh, w[1] * sh, w[2] * sh};
     float o[4] = {q[0] * r[0] - q[1] * r[1] - q[2] * r[2] - q[3] * r[3],
                   q[0] * r[1] + q[1] * r[0] + q[2] * r[3] - q[3] * r[2],
@@ -758,13 +766,14 @@ H12_DEV void link_p_pk(const float (&cs)[NL][2], const f32x2 (&U)[NL][3], const 
 // velocity as (angular, linear) pairs (link_pass3_pk's transform, the joint rate for qdd), the world rotation's rows 0 / 1
 // as column pairs C[j] = (R_0j, R_1j) with row 2 apart (R2), the position as (p01, p2): a joint rotation turns two
 // columns, one packed op per pair of rows
-template <int LINK>
+template <int LINK, bool HWTRIG = false>
 H12_DEV void link_pass1_pk(const Leg& lg, float (&cs)[NL][2], const f32x2* vp, f32x2 (&V)[NL][3], f32x2 (&C)[3],
                            float (&R2)[3], f32x2& p01, float& p2) {
   constexpr int A = AX[LINK], J = (A + 1) % 3, Q = (A + 2) % 3;
   const float* r = h12m::R[LINK];
   float s, c;
-  fsincos(lg.q[LINK], &s, &c);
+  if constexpr (HWTRIG) fsincos_hw(lg.q[LINK], &s, &c);  // the self-contact wave (fsincos_hw)
+  else fsincos(lg.q[LINK], &s, &c);
   cs[LINK][0] = c;
   cs[LINK][1] = s;
   const float aw[3] = {vp[0].x, vp[1].x, vp[2].x};
@@ -1686,11 +1695,13 @@ H12_DEV void joint_terms(const KParams& P, const Leg& lg, float h, float* tq, fl
 // pass 1 from the state: lane-frame base pose / velocity, then the 6 links' joint sin / cos, spatial velocities
 // and world poses; Rk / pk: the knee's pose, R / p on exit: the foot's.
 // rel: positions relative to the base origin (the self-contact geometry: only differences of body points enter it,
-// and pelvis-relative fp32 points carry the ulp of ~1 m instead of the env's world position)
-template <int K>
+// and pelvis-relative fp32 points carry the ulp of ~1 m instead of the env's world position); HWTRIG: the joint sin /
+// cos without the radial correction (fsincos_hw: the self-contact wave)
+template <int K, bool HWTRIG = false>
 H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, float (&R0)[3][3], float* vb,
                        float* pb0, float (&cs)[NL][2], float (&v)[NL][6], float (&Rk)[3][3], float* pk,
                        float (&R)[3][3], float* p, bool rel = false) {
+  constexpr bool HW = HWTRIG;
   const float sg = leg ? -1.f : 1.f;
   quat_R(b.quat, R0);
   mtv(R0, b.vlin, vb);
@@ -1715,18 +1726,18 @@ H12_DEV void leg_pass1(int leg, const Base& b, const Leg& lg, const float* org, 
   }
   f32x2 p01 = pk2(p[0], p[1]);
   float p2 = p[2];
-  link_pass1_pk<0>(lg, cs, V0, V, C, R2, p01, p2);
-  link_pass1_pk<1>(lg, cs, V[0], V, C, R2, p01, p2);
-  link_pass1_pk<2>(lg, cs, V[1], V, C, R2, p01, p2);
-  link_pass1_pk<3>(lg, cs, V[2], V, C, R2, p01, p2);
+  link_pass1_pk<0, HW>(lg, cs, V0, V, C, R2, p01, p2);
+  link_pass1_pk<1, HW>(lg, cs, V[0], V, C, R2, p01, p2);
+  link_pass1_pk<2, HW>(lg, cs, V[1], V, C, R2, p01, p2);
+  link_pass1_pk<3, HW>(lg, cs, V[2], V, C, R2, p01, p2);
   for (int j = 0; j < 3; ++j) {
     Rk[0][j] = C[j].x;
     Rk[1][j] = C[j].y;
     Rk[2][j] = R2[j];
   }
   pk[0] = p01.x; pk[1] = p01.y; pk[2] = p2;
-  link_pass1_pk<4>(lg, cs, V[3], V, C, R2, p01, p2);
-  link_pass1_pk<5>(lg, cs, V[4], V, C, R2, p01, p2);
+  link_pass1_pk<4, HW>(lg, cs, V[3], V, C, R2, p01, p2);
+  link_pass1_pk<5, HW>(lg, cs, V[4], V, C, R2, p01, p2);
   for (int j = 0; j < 3; ++j) {
     R[0][j] = C[j].x;
     R[1][j] = C[j].y;
@@ -2081,7 +2092,7 @@ H12_DEV void self_wave(const KParams& P, int n, int n_steps, const FuseCtx& fc) 
       float org[3];
       get_state(l, b, lg, org);
       float R0[3][3], vb[3], pb0[3], cs[NL][2], v[NL][6];
-      leg_pass1<K>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
+      leg_pass1<K, true>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);  // pelvis-relative positions
       // broad phase and, in a candidate wave, the staging (after R1 instead, the staging made this wave the last at R2:
       // -3 %, profiles/r5/r5p_*)
       act = self_stage(P, leg, lg.mud, Rk, pk, v[3], R, p, v[5], false, true);

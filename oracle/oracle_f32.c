@@ -17,11 +17,27 @@
 #endif
 
 #include "../include/h12env.h"
-#ifdef H12_F32_HWTRIG
+#if defined(H12_F32_HWTRIG) && !defined(H12_F32_HWTRIG_TABLE)
 /* the kernel's __sinf / __cosf: v_mul_f32 by fp32(1 / 2 pi), then the hardware's sin / cos of that many revolutions
  * (evaluated here exactly, in double, and rounded: the prescale's rounding is the only fp32 error kept) */
 static float hw_sin(float x) { return (float)sin(6.283185307179586 * (double)(x * 0.15915494f)); }
 static float hw_cos(float x) { return (float)cos(6.283185307179586 * (double)(x * 0.15915494f)); }
+#endif
+#ifdef H12_F32_HWTRIG_TABLE
+/* the kernel's __sinf / __cosf as measured: the exact value plus the hardware's mean signed error of the argument's
+ * bin, linearly interpolated between bin centres (hw_trig_err.h, tools/probe/hw_trig_table.hip) */
+#include "hw_trig_err.h"
+static float trig_err(const float* t, float x) {
+  const double u = ((double)x + 3.14159265358979323846) / (2 * 3.14159265358979323846) * H12_TRIG_NB - 0.5;
+  int i = (int)floor(u);
+  const double f = u - i;
+  const int i0 = i < 0 ? 0 : (i > H12_TRIG_NB - 1 ? H12_TRIG_NB - 1 : i);
+  const int i1 = i + 1 < 0 ? 0 : (i + 1 > H12_TRIG_NB - 1 ? H12_TRIG_NB - 1 : i + 1);
+  return (float)((1 - f) * t[i0] + f * t[i1]);
+}
+static float hw_sin(float x) { return (float)(sin((double)x) + trig_err(h12_sin_err, x)); }
+static float hw_cos(float x) { return (float)(cos((double)x) + trig_err(h12_cos_err, x)); }
+#define H12_F32_HWTRIG
 #endif
 #define double float
 #ifdef H12_F32_HWTRIG

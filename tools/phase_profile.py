@@ -150,6 +150,26 @@ def run(tag: str, steps: int, burn: int, envs: int, self_coll: bool) -> dict:
                 grp: {k: round(float(np.median(Lp[sel][:, i])), 2) for i, k in enumerate(names)}
                 for grp, sel in (("waves_with_reset", rw), ("waves_without_reset", ~rw)) if sel.any()}
             res["light_phases_us_median"]["fraction_of_waves_with_reset"] = round(float(rw.mean()), 3)
+        if bws and raw:  # round 6: the block tail -- each block's physics loop against its self-contact candidates
+            # (the self wave's PHN marks: slot 8 = the most candidate envs of an inner step, slot 9 = their sum over the
+            # launch), per launch the slowest block's loop against the median block's
+            Bc = np.asarray(bws)  # (launches, blocks, role, 16) in us of 2370 cycles; the PHN slots hold counts
+            ncmax = np.rint(Bc[:, :, 3, 8] * 2370.0).astype(int)
+            ncsum = np.rint(Bc[:, :, 3, 9] * 2370.0).astype(int)
+            Rw = np.asarray(raw)
+            loop = (Rw[:, :, 3] - Rw[:, :, 0]) / 100.0  # us
+            qq = lambda x: [round(float(np.quantile(x, p)), 2) for p in (0.5, 0.95, 1.0)]  # noqa: E731
+            by = {}
+            for k in range(int(ncmax.max()) + 1):
+                m = ncmax == k
+                if m.any():
+                    by[str(k)] = {"blocks": int(m.sum()), "loop_us_median": round(float(np.median(loop[m])), 2)}
+            res["block_tail"] = {
+                "physics_loop_us_p50_p95_max": qq(loop.ravel()),
+                "per_launch_max_minus_median_us": round(float(np.mean(loop.max(1) - np.median(loop, 1))), 2),
+                "slowest_block_max_candidates_median": float(np.median(ncmax[np.arange(len(loop)), loop.argmax(1)])),
+                "by_max_candidates": by,
+                "candidate_sum_per_launch_p50_p95_max": qq(ncsum.ravel())}
         if bws:  # median over blocks and launches of the us each wave role waited per launch in each barrier kind
             B = np.concatenate(bws)  # (launches x blocks, 4, 4)
             res["barrier_wait_us_per_launch_median"] = {

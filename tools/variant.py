@@ -131,6 +131,12 @@ PATCHES_HEAD["epb16h_halfx"] = PATCHES_HEAD["epb16h_half"] + [
     ("  const float x = (u[LINK] - (ua.x + ua.y)) * Dinv[LINK];\n",
      "  const float x = xs2(xs2(u[LINK] - (xs2(ua.x) + ua.y)) * Dinv[LINK]);\n"),
 ]
+# round 6 timing probe (results wrong): the self-contact pair jobs' LDS float atomics (12 per contact point, up to 16 lanes
+# of one env on the same address in the foot-foot passes) replaced by consuming the values -- what the atomics' address
+# conflicts cost the candidate blocks
+PATCHES_HEAD["self_noatomic"] = [
+    ("        atomicAdd(&al(a), F[a]); atomicAdd(&al(3 + a), m[a]);\n        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(3 + a), -m[a]);\n",
+     "        asm volatile(\"\" :: \"v\"(F[a]), \"v\"(m[a]));\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
