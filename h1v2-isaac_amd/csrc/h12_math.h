@@ -33,11 +33,34 @@ H12_DEV void cross(const float* a, const float* b, float* o) {
 H12_DEV float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 // 3x3 rotation from unit quaternion (w x y z); R maps body -> world
-H12_DEV void quat_R(const float* q, float R[3][3]) {
+// the rotation of q / |q| (round 6): a stored fp32 quaternion is unit only to its rounding, and the one the kernel's own
+// normalisation (rsq) leaves is short by ~2e-8 on average; the unit-quaternion formula then scales the rotation's off-
+// diagonal part by |q|^2 and showed up as a signed bias of lying robots (VLIN2 -3.5e-7, z = -69; the oracle normalises
+// first, quat_to_R).  Writing 2 / |q|^2 for the formula's 2 makes it exact for any |q| (+5 VALU)
+// (every product-sum is an explicit fma: the call sites of the fused and the two-kernel observation paths must round
+// alike, and the compiler's contraction choice may differ between them).  quat_R_unit: the unit-quaternion formula
+// (step_kernel's physics wave after barrier R2, where the reciprocal sat on the step's critical chain: -0.9 % in an
+// interleaved A/B; its R0 only turns gravity and the base velocities, which a |q|^2 - 1 of ~1e-7 moves by as much)
+H12_DEV void quat_R_unit(const float* q, float R[3][3]) {
   float w = q[0], x = q[1], y = q[2], z = q[3];
   R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - w * z); R[0][2] = 2.f * (x * z + w * y);
   R[1][0] = 2.f * (x * y + w * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - w * x);
   R[2][0] = 2.f * (x * z - w * y); R[2][1] = 2.f * (y * z + w * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+H12_DEV void quat_R(const float* q, float R[3][3]) {
+  const float w = q[0], x = q[1], y = q[2], z = q[3];
+  const float F = __builtin_fmaf(w, w, __builtin_fmaf(x, x, __builtin_fmaf(y, y, z * z)));
+  const float t = 2.f * __builtin_amdgcn_rcpf(F);
+  const float xx = x * x, yy = y * y, zz = z * z;
+  R[0][0] = __builtin_fmaf(-t, yy + zz, 1.f);
+  R[0][1] = t * __builtin_fmaf(x, y, -(w * z));
+  R[0][2] = t * __builtin_fmaf(x, z, w * y);
+  R[1][0] = t * __builtin_fmaf(x, y, w * z);
+  R[1][1] = __builtin_fmaf(-t, xx + zz, 1.f);
+  R[1][2] = t * __builtin_fmaf(y, z, -(w * x));
+  R[2][0] = t * __builtin_fmaf(x, z, -(w * y));
+  R[2][1] = t * __builtin_fmaf(y, z, w * x);
+  R[2][2] = __builtin_fmaf(-t, xx + yy, 1.f);
 }
 H12_DEV void mv(const float R[3][3], const float* v, float* o) {
   float t0 = R[0][0] * v[0] + R[0][1] * v[1] + R[0][2] * v[2];
@@ -259,7 +282,7 @@ H12_DEV void fsincos(float x, float* s, float* c) {
   float sv, cv;
   fsincos_hw(x, &sv, &cv);
   const float d = __builtin_fmaf(cv, cv, __builtin_fmaf(sv, sv, -1.f));
-  const float k = -0.5f * d;
+  const float k = -0.5f * d;  // the one rounding (of s^2 - 1) is zero-mean; (1 + d)^(-1/2) = 1 - d / 2 to 1e-15
   *s = __builtin_fmaf(sv, k, sv);
   *c = __builtin_fmaf(cv, k, cv);
 }

@@ -441,7 +441,7 @@ H12_DEV void impl_force(const float* a, const float* p, const float* u, float be
 template <bool ANCHOR, bool TERRAIN, bool EXPL = false>
 H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float* pb, const float* vb,
                             const float* pl, float rad, float* f, float* fw, float* anc, bool was_in, float sg,
-                            const float* org, float mus, float mud, ImplC& ic) {
+                            const float* org, float mus, float mud, ImplC& ic, bool expl_rt = false) {
   ic.beta = 0.f;
   ic.gamma = 0.f;
   float xw[3];
@@ -497,7 +497,7 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
   }
   float Fw[3] = {ft0, ft1, fn}, fl[3], nl[3];
   if constexpr (TERRAIN) { Fw[0] += fn * nrm[0]; Fw[1] += fn * nrm[1]; Fw[2] = fn * nrm[2]; }
-  if (P.impl && !EXPL) {
+  if (P.impl && !EXPL && !expl_rt) {  // expl_rt: EXPL decided per lane (helper_torso's split corners)
     const float h = P.h;
     const float alpha = h * P.cc;
     const float beta = stick ? h * (ANCHOR ? P.fc : P.fc_v) : 0.f;
@@ -1144,6 +1144,19 @@ H12_DEV SelfLds& self_lds() {
   __shared__ SelfLds L;
   return L;
 }
+// The contact wave's release count as an LDS-typed volatile (round 6): through a generic volatile pointer the spin read
+// and the release store compiled to flat_load / flat_store sc0 sc1, and every flat access is followed by an
+// s_waitcnt vmcnt(0) -- each poll of the self wave (and the contact wave after its release) waited for the wave's
+// outstanding row stores to reach memory
+// A workgroup-scope float add on an LDS-typed pointer (ds_add_f32): atomicAdd through the generic reference is an agent-
+// scope atomic, and the memory legalizer put an s_waitcnt vmcnt(0) (the wave's outstanding row stores) ahead of each
+// pass's first one
+H12_DEV void lds_add(float& x, float v) {
+  __hip_atomic_fetch_add((__attribute__((address_space(3))) float*)&x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+H12_DEV volatile __attribute__((address_space(3))) int* self_done() {
+  return (volatile __attribute__((address_space(3))) int*)&self_lds().done;
+}
 
 // Self-contacts, phase 1 (self_stage): broad phase and, when some env of the wave has a candidate pair, the LDS
 // staging of the wave's capsules and body kinematics; returns the wave's candidate mask (0: nothing staged, no
@@ -1352,8 +1365,8 @@ H12_DEV void self_jobs(const KParams& P, int njobs, bool ffonly, int g0, int str
       float m[3];
       cross(x, F, m);
       for (int a = 0; a < 3; ++a) {
-        atomicAdd(&al(a), F[a]); atomicAdd(&al(3 + a), m[a]);
-        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(3 + a), -m[a]);
+        lds_add(al(a), F[a]); lds_add(al(3 + a), m[a]);
+        lds_add(ar(a), -F[a]); lds_add(ar(3 + a), -m[a]);
       }
     }
   }
@@ -1383,9 +1396,9 @@ H12_DEV void self_finish(const KParams& P, int leg, uint64_t act, const float (&
   if (sj) {  // the contact wave's jobs: its release store follows its atomics (an LDS spin, no barrier)
     // bounded (~2 ms) so that a broken release can never hang the GPU; a wait that ends at the bound unreleased is
     // raised in the device diagnostic word, which h12env_check reports (the wrenches of that inner step may be partial)
-    for (int k = 0; k < (1 << 16) && *reinterpret_cast<volatile int*>(&L.done) <= it; ++k) __builtin_amdgcn_s_sleep(1);
+    for (int k = 0; k < (1 << 16) && *self_done() <= it; ++k) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
-    if (*reinterpret_cast<volatile int*>(&L.done) <= it && (threadIdx.x & 63) == 0) atomicOr(P.diag, 1);
+    if (*self_done() <= it && (threadIdx.x & 63) == 0) atomicOr(P.diag, 1);
   }
   wave_sync();
   // ---- own bodies: moment about the body origin, real -> lane frame (force M F; moment sg M T) -> body coords
@@ -1427,7 +1440,7 @@ H12_DEV void self_jobs_shared(const KParams& P, int it) {
   const int me = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
   self_jobs(P, njobs, ffonly, nlive + me, 2 * nlive, 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0 && !P.dbg_norel) *reinterpret_cast<volatile int*>(&L.done) = it + 1;
+  if ((threadIdx.x & 63) == 0 && !P.dbg_norel) *self_done() = it + 1;
 }
 
 H12_DEV void self_contacts(const KParams& P, int leg, float mu, const float (&Rk)[3][3], const float* pk,
@@ -1517,6 +1530,16 @@ struct FuseCtx {
   int row;           // floats per row (45 x history)
   int on;            // whole block, 16-byte aligned, >= 2 physics steps: the spread path; else fuse_late alone
 };
+// One 1-KB LDS-DMA piece (global_load_lds_dwordx4: this lane's 16 B of src into LDS at lds + 16 x lane) written as inline
+// asm (round 6): the compiler tracks a builtin LDS-DMA as a pending LDS write and, unable to tell it apart from the
+// self-contact accumulators, put an s_waitcnt vmcnt(0) ahead of every inner step's first LDS atomic in the self / contact
+// waves -- each job pass waited for the wave's outstanding row stores.  The issuing wave drains its pieces itself
+// (fuse_drain's s_waitcnt before barrier R2 of inner step 1; the reads follow that barrier); a VMEM op the compiler does
+// not count only makes its own vmcnt(k) waits stricter (the counter drains in issue order)
+H12_DEV void lds_dma16(const void* src, const void* lds_chunk) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_chunk;
+  asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(src), "{m0}"(m0) : "memory");
+}
 // helper-wave lane t of nt, after the R2 barrier of inner step it (n_steps in the env step)
 H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
   if (!f.on) return;
@@ -1526,11 +1549,9 @@ H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
     const int w = t >> 6, lane = t & 63, nw = nt >> 6, nch = (f4 + 63) / 64;
     for (int ch = w; ch < nch; ch += nw)
       if (ch * 64 + lane < f4)
-        __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane),
-                                         (__attribute__((address_space(3))) void*)(F.hist + ch * 256), 16, 0, 0);
+        lds_dma16(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane, F.hist + ch * 256);
     for (int ch = w; ch < FUSE_CODE_BYTES / 1024; ch += nw)
-      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const uint4*>(f.code) + ch * 64 + lane),
-                                       (__attribute__((address_space(3))) void*)(F.code + ch * 1024), 16, 0, 0);
+      lds_dma16(reinterpret_cast<const uint4*>(f.code) + ch * 64 + lane, F.code + ch * 1024);
     return;
   }
   // this lane's float4s j = t + k nt, k in its share of the remaining inner steps: every float gets the next-newer
@@ -1856,21 +1877,54 @@ H12_DEV void get_state(int l, Base& b, Leg& lg, float* org) {
 H12_DEV int xcd_block(int b, int nb);
 H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
 
-// The helper wave's torso-box ground contact (lane 0 of each pair): the lowest corner's implicit contact and, while it
-// touches, the face's other corners (torso_face) -> H.torso for the physics wave's base combine after R2.
+// The torso-box ground contact of the helper wave (flat, after R1) or the contact wave (terrain, before R1): the lowest
+// corner's implicit contact and the face's other three corners' explicit ones (torso_face's rule: on terrain only while
+// the lowest corner touches) -> H.torso for the physics wave's base combine after R2.  Round 6: the four corners split
+// over the lane pair -- leg 0 the lowest corner (implicit) and face corner 1, leg 1 face corners 2 and 3 -- as ONE
+// instruction stream (contact_sphere's implicit block switched off per lane): a fallen robot's torso put four full
+// sphere contacts on one lane, and the waves of the blocks holding one were the step's slowest at barrier R2 in 24 of
+// 40 launches (light stamps, profiles/r6/).  Lane 0's hand-off carries the pair's summed reported force and the
+// implicit linearisation; lane 1's its corners' wrench (the physics wave sums the pair's wrenches anyway).  Flat ground
+// only: on terrain the split left env-steps of the Rough / C5 parity tests off the oracle that the harness could not
+// explain (profiles/r6/), so there lane 0 keeps all four corners.
 template <int K>
 H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const float* vb, const float (&R0)[3][3],
                           const float* pb0, const float* org) {
+  constexpr bool T = Feat<K>::terrain;
   float t[16] = {};
+  const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
+  // corner k of the lowest face (k = 0: the lowest corner, torso_corner; 1..3: torso_face's)
+  const float z0 = fabsf(R0[2][0]), z1 = fabsf(R0[2][1]), z2 = fabsf(R0[2][2]);
+  const int an = (z0 >= z1 && z0 >= z2) ? 0 : (z1 >= z2 ? 1 : 2);
+  const int ab = an == 0 ? 1 : 0, ac = an == 2 ? 1 : 2;
+  auto corner_k = [&](int k, float* p) {
+    for (int a = 0; a < 3; ++a) {
+      const bool flip = ((k & 1) && a == ab) || ((k & 2) && a == ac);
+      const bool neg = (R0[2][a] > 0.f) != flip;
+      p[a] = h12m::TORSO_C[a] + (neg ? -h12m::TORSO_H[a] : h12m::TORSO_H[a]);
+    }
+  };
+  ImplC ict;
+  float dummy[2], p[3];
+  bool c = false;
+  if constexpr (T) {  // terrain (the contact wave, before R1): lane 0 alone, the face's corners while the lowest touches
+    if (leg == 0) {
+      corner_k(0, p);
+      c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict);
+      if (c) torso_face<T>(P, R0, pb0, v0, org, t, t + 6);
+    }
+  } else {
+    corner_k(leg ? 2 : 0, p);
+    c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict, leg != 0);
+    corner_k(leg ? 3 : 1, p);
+    ImplC dz;
+    contact_sphere<false, T, true>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, dz);
+  }
+  for (int a = 0; a < 3; ++a) {  // the reported force (|F| feeds the illegal-contact test): the pair's sum on lane 0
+    const float o = pair_swap(t[6 + a]);
+    t[6 + a] = leg ? 0.f : t[6 + a] + o;
+  }
   if (leg == 0) {
-    const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
-    float corner[3];
-    torso_corner(R0, corner);
-    ImplC ict;
-    float dummy[2];
-    const bool c = contact_sphere<false, Feat<K>::terrain>(P, R0, pb0, v0, corner, 0.f, t, t + 6, dummy, false, 1.f,
-                                                           org, P.mus, P.mud, ict);
-    if (c || !Feat<K>::terrain) torso_face<Feat<K>::terrain>(P, R0, pb0, v0, org, t, t + 6);
     t[9] = ict.beta; t[10] = ict.gamma; t[11] = ict.u[0]; t[12] = ict.u[1]; t[13] = ict.u[2];
     t[14] = c ? 1.f : 0.f;
   }
@@ -2422,7 +2476,7 @@ H12_DEV void inner_step_hw(const KParams& P, int leg, Base& b, Leg& lg, const Pd
   for (int i = 0; i < 6; ++i) pAcc[i] *= s6(i, sg);
   // ---- lane 0 adds the base body: rigid inertia, bias force, torso-box contact (helper wave)
   float R0[3][3];
-  quat_R(b.quat, R0);
+  quat_R_unit(b.quat, R0);  // (quat_R_unit: off the critical chain's reciprocal)
   float ag[6] = {0.f, 0.f, 0.f, -P.g * R0[2][0], -P.g * R0[2][1], -P.g * R0[2][2]};
   // (lane 1's hand-offs hold zeros here -- the helper wave writes the base body's bias force and the torso contact on
   // lane 0 only -- so both lanes run this without a branch; the base body's rigid inertia (dmass: an env-level value,
@@ -3626,7 +3680,13 @@ H12_DEV void obs_frame_fused(const KParams& P, const EnvSt& s, int leg, int r, b
     float R[3][3];
     quat_R(s.b.quat, R);
     for (int a = 0; a < 3; ++a) fr[a] = (s.b.wang[a] + nz[a]) * P.oscale[0];
-    for (int a = 0; a < 3; ++a) fr[3 + a] = (-R[2][a] + nz[3 + a]) * P.oscale[1];
+    for (int a = 0; a < 3; ++a) {
+      // the projected gravity rounded on its own, as the two-kernel path stores it (quat_R's products are no longer
+      // exact doublings; contracted into the noise addition they would round differently)
+      float gr = -R[2][a];
+      pin(gr);
+      fr[3 + a] = (gr + nz[3 + a]) * P.oscale[1];
+    }
     for (int a = 0; a < 3; ++a) fr[6 + a] = s.cmd[a] * P.oscale[2];
     F.fill[r] = fill ? 1 : 0;
   }

@@ -46,6 +46,8 @@ class OracleStandIn:
             ccfg.mu_dynamic *= 1.0 - rel
         elif name == "mu_s":  # the static (stick / slip) friction coefficient too SMALL
             ccfg.mu_static *= 1.0 - rel
+        elif name == "gravity":  # gravity too strong (the sole gate's force-balance allowance, gen_sole_bias_gate.py)
+            model.gravity *= 1.0 + rel
         self.core = O.OracleEnv(model, ccfg, n)
         if cfg.scene.terrain.terrain_type == "generator":  # startup state (origins, materials) and the heightfield
             from h12env.startup import apply_to_arrays, startup_state

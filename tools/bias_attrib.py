@@ -98,7 +98,7 @@ class F32StandIn:
         return {"policy": self._obs[0]}, torch.from_numpy(rew), torch.from_numpy(term), torch.from_numpy(trunc), {}
 
 
-def run(lib, name, n, steps):
+def run(lib, name, n, steps, seed=37):
     from forced import ForcedParity
     from h12env import H12FlatEnvCfg
     from scenarios import SOLE_SCENARIOS
@@ -108,9 +108,10 @@ def run(lib, name, n, steps):
     cfg.terminations.base_contact_knees = False
     env = F32StandIn(lib, n, cfg)
     kw = dict(preload=1e-3) if name == "stance" else {}
-    hold = SOLE_SCENARIOS[name](env._model, env.core.F, np.random.default_rng(37), Im=env.core.I, action_scale=0.5, **kw)
-    fp = ForcedParity(env, seed=38)
-    rng = np.random.default_rng(39)
+    hold = SOLE_SCENARIOS[name](env._model, env.core.F, np.random.default_rng(seed), Im=env.core.I, action_scale=0.5,
+                                **kw)
+    fp = ForcedParity(env, seed=seed + 1)
+    rng = np.random.default_rng(seed + 2)
     for _ in range(steps):
         fp.step((hold + rng.normal(size=(n, 12)) * 0.05).astype(np.float32))
     return fp
@@ -122,12 +123,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--scen", default="stance,single_stance,slip")
     ap.add_argument("--json")
+    ap.add_argument("--seed", type=int, default=37)
     ap.add_argument("--variant", default="", help="'' = plain fp32 build, 'hw' = with the kernel's sin / cos prescale")
     a = ap.parse_args()
     lib = f32_lib(a.variant)
     out = {}
     for name in a.scen.split(","):
-        fp = run(lib, name, a.n, a.steps)
+        fp = run(lib, name, a.n, a.steps, a.seed)
         names, m, se = fp.bias_fields()
         kern = json.loads((ROOT / "profiles" / "r5" / f"bias_{name}.json").read_text())
         km, kse = np.array(kern["mean"]), np.array(kern["se"])

@@ -137,6 +137,26 @@ PATCHES_HEAD["epb16h_halfx"] = PATCHES_HEAD["epb16h_half"] + [
 PATCHES_HEAD["self_noatomic"] = [
     ("        atomicAdd(&al(a), F[a]); atomicAdd(&al(3 + a), m[a]);\n        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(3 + a), -m[a]);\n",
      "        asm volatile(\"\" :: \"v\"(F[a]), \"v\"(m[a]));\n")]
+# round 6 bias elimination (correct results, slower math): one single-instruction operation of the kernel replaced by its
+# correctly rounded form, to see which one carries the signed bias left after the fsincos fix (tools/bias_probe.py)
+_ACC = {"acc_rsq": "#define __builtin_amdgcn_rsqf(x) (1.0f / __builtin_sqrtf(x))\n",
+        "acc_rcp": "#define frcp(x) (1.0f / (x))\n",
+        "acc_sqrt": "#define fsqrt(x) __builtin_sqrtf(x)\n",
+        "acc_pre": ("H12_DEV void fsincos_acc(float x, float* s, float* c) {\n"
+                    "  const float y = __builtin_fmaf(x, 0.15915493667125702f, x * 6.4206382e-09f);\n"
+                    "  const float sv = __builtin_amdgcn_sinf(y), cv = __builtin_amdgcn_cosf(y);\n"
+                    "  const float d = __builtin_fmaf(cv, cv, __builtin_fmaf(sv, sv, -1.f));\n"
+                    "  *s = __builtin_fmaf(sv, -0.5f * d, sv);\n  *c = __builtin_fmaf(cv, -0.5f * d, cv);\n}\n"
+                    "#define fsincos(x, s, c) fsincos_acc(x, s, c)\n")}
+for _k, _v in _ACC.items():
+    PATCHES_HEAD[_k] = [("using namespace h12;\n", "using namespace h12;\n" + _v)]
+PATCHES_HEAD["acc_all"] = [("using namespace h12;\n", "using namespace h12;\n" + "".join(_ACC.values()))]
+# round 6 check: the torso corners back on lane 0 alone (the pre-split helper_torso), everything else current
+PATCHES_HEAD["torso_lane0"] = [("  ImplC ict;\n  float dummy[2], p[3];\n  corner_k(leg ? 2 : 0, p);\n  const bool c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict,\n                                          leg != 0);\n  const bool c0 = leg ? pair_swap_i(c ? 1 : 0) != 0 : c;  // the lowest corner's contact (lane 0's)\n  if constexpr (T) {\n    if (!c0)  // leg 1's corner 2 was speculative\n      for (int i = 0; i < 9; ++i) t[i] = 0.f;\n  }\n  if (c0 || !T) {\n    corner_k(leg ? 3 : 1, p);\n    ImplC dz;\n    contact_sphere<false, T, true>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, dz);\n  }\n", '  ImplC ict;\n  float dummy[2], p[3];\n  bool c = false;\n  if (leg == 0) {\n    corner_k(0, p);\n    c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict);\n    if (c || !T) torso_face<T>(P, R0, pb0, v0, org, t, t + 6);\n  }\n')]
+# round 6 block-tail probes (timing only, results wrong): the flat torso contact off the helper wave; the helper waves'
+# drain of the row LDS-DMA before barrier R2 of inner step 1 skipped
+PATCHES_HEAD["no_torso"] = [("      if constexpr (!Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n", "")]
+PATCHES_HEAD["no_drain"] = [("  if (f.on && it == 1) __builtin_amdgcn_s_waitcnt(0);", "  (void)f; (void)it;")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
@@ -161,7 +181,7 @@ def patched(tag: str) -> tuple[str, str]:
     return orig, src
 
 
-def build(tag: str, profile: bool, isa: bool = False) -> Path:
+def build(tag: str, profile: bool, isa: bool = False, light: bool = False) -> Path:
     from h12env.build import ARCH, hipcc
 
     rev = ALL[tag][0] if tag in ALL else (tag.split("@", 1)[1] or None)
@@ -180,7 +200,8 @@ def build(tag: str, profile: bool, isa: bool = False) -> Path:
     out = ROOT / "tools" / "_variants" / f"lib_{tag}.so"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-Xarch_device",
            "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros", "-fPIC", "-shared", "-Wno-unused-function",
-           *(["-DH12_PHASE_PROFILE"] if profile else []), *(["-save-temps"] if isa else []), "-o", str(out),
+           *(["-DH12_PHASE_PROFILE"] if profile or light else []), *(["-DH12_PHASE_LIGHT"] if light else []),
+           *(["-save-temps"] if isa else []), "-o", str(out),
            str(csrc / "h12env.hip")]
     subprocess.run(cmd, check=True, cwd=top)
     if isa:  # the Flat step kernel's static report (tools/kernel_isa.py), as for the product
@@ -205,6 +226,7 @@ if __name__ == "__main__":
     ap.add_argument("tag", help=f"one of {sorted(ALL)}, or <name>@<git revision>: that revision's unpatched "
                     "sources as tools/_variants/lib_<name>.so (the A/B baseline; <name>@ alone: the working tree's)")
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--light", action="store_true", help="the light-stamp profile build (tools/phase_profile.py --tag <tag>)")
     ap.add_argument("--isa", action="store_true", help="print the Flat step kernel's static ISA report")
     a = ap.parse_args()
-    build(a.tag, a.profile, a.isa)
+    build(a.tag, a.profile, a.isa, a.light)
