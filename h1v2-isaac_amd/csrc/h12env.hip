@@ -1541,19 +1541,29 @@ H12_DEV void lds_dma16(const void* src, const void* lds_chunk) {
   asm volatile("global_load_lds_dwordx4 %0, off" : : "v"(src), "{m0}"(m0) : "memory");
 }
 // helper-wave lane t of nt, after the R2 barrier of inner step it (n_steps in the env step)
-H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
+// the rows -> LDS: 1 KB LDS-DMA chunks, issued by each helper wave after barrier R2 of the first inner step (fuse_early)
+// and drained before R2 of inner step 1 (fuse_drain).  The helper waves wait ~0.7 us per launch at that drain (light
+// stamps, profiles/r6/); issued before the first barrier S instead, the chunks delayed the physics wave's state loads:
+// step_kernel +1.1 us (profiles/r6/not_kept/r6n_*)
+H12_DEV void fuse_dma(const FuseCtx& f, int t, int nt) {
   if (!f.on) return;
   FuseLds& F = fuse_lds();
   const int f4 = FUSE_ROWS * f.row / 4;
-  if (it == 0) {  // rows -> LDS: 1 KB LDS-DMA chunks, drained before the next R2 (fuse_drain)
-    const int w = t >> 6, lane = t & 63, nw = nt >> 6, nch = (f4 + 63) / 64;
-    for (int ch = w; ch < nch; ch += nw)
-      if (ch * 64 + lane < f4)
-        lds_dma16(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane, F.hist + ch * 256);
-    for (int ch = w; ch < FUSE_CODE_BYTES / 1024; ch += nw)
-      lds_dma16(reinterpret_cast<const uint4*>(f.code) + ch * 64 + lane, F.code + ch * 1024);
+  const int w = t >> 6, lane = t & 63, nw = nt >> 6, nch = (f4 + 63) / 64;
+  for (int ch = w; ch < nch; ch += nw)
+    if (ch * 64 + lane < f4)
+      lds_dma16(reinterpret_cast<const float4*>(f.src) + ch * 64 + lane, F.hist + ch * 256);
+  for (int ch = w; ch < FUSE_CODE_BYTES / 1024; ch += nw)
+    lds_dma16(reinterpret_cast<const uint4*>(f.code) + ch * 64 + lane, F.code + ch * 1024);
+}
+H12_DEV void fuse_early(const FuseCtx& f, int it, int n_steps, int t, int nt) {
+  if (!f.on) return;
+  if (it == 0) {
+    fuse_dma(f, t, nt);
     return;
   }
+  FuseLds& F = fuse_lds();
+  const int f4 = FUSE_ROWS * f.row / 4;
   // this lane's float4s j = t + k nt, k in its share of the remaining inner steps: every float gets the next-newer
   // slot (+3 in the 3-wide terms, +12 in the 12-wide ones, fuse_code_table); the newest slot's floats get a
   // placeholder that fuse_late overwrites, as it rewrites the rows of resetting envs (after barrier F, when every
@@ -1887,11 +1897,36 @@ H12_DEV int step_block() { return xcd_block(blockIdx.x, gridDim.x); }
 // implicit linearisation; lane 1's its corners' wrench (the physics wave sums the pair's wrenches anyway).  Flat ground
 // only: on terrain the split left env-steps of the Rough / C5 parity tests off the oracle that the harness could not
 // explain (profiles/r6/), so there lane 0 keeps all four corners.
+// the largest distance of a torso-box corner from the base origin (helper_torso's skip test)
+constexpr float TORSO_RMAX = 0.2200f;
+static_assert((h12m::TORSO_C[0] + h12m::TORSO_H[0]) * (h12m::TORSO_C[0] + h12m::TORSO_H[0]) +
+                      (h12m::TORSO_C[1] + h12m::TORSO_H[1]) * (h12m::TORSO_C[1] + h12m::TORSO_H[1]) +
+                      (h12m::TORSO_C[2] + h12m::TORSO_H[2]) * (h12m::TORSO_C[2] + h12m::TORSO_H[2]) <=
+                  TORSO_RMAX * TORSO_RMAX &&
+              h12m::TORSO_C[0] == 0.f && h12m::TORSO_C[1] == 0.f && h12m::TORSO_C[2] >= 0.f,
+              "torso corners within TORSO_RMAX of the base origin");
 template <int K>
 H12_DEV void helper_torso(const KParams& P, int l, int leg, const Base& b, const float* vb, const float (&R0)[3][3],
                           const float* pb0, const float* org) {
   constexpr bool T = Feat<K>::terrain;
   float t[16] = {};
+  if constexpr (!T) {
+    // flat ground: no corner of the box can activate when its lowest point is higher than a step's travel of any
+    // corner (activation needs z_k < -h vn_k <= h (|v| + |w| r_k), r_k <= TORSO_RMAX): the wave skips the contact code
+    // when that holds for all its envs (the upright robots of most blocks; exact, the skipped calls return no force)
+    float zmin = pb0[2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) zmin += R0[2][a] * h12m::TORSO_C[a] - fabsf(R0[2][a]) * h12m::TORSO_H[a];
+    const float v2 = b.vlin[0] * b.vlin[0] + b.vlin[1] * b.vlin[1] + b.vlin[2] * b.vlin[2];
+    const float w2 = b.wang[0] * b.wang[0] + b.wang[1] * b.wang[1] + b.wang[2] * b.wang[2];
+    // (|v| + |w| r)^2 <= 2 (|v|^2 + r^2 |w|^2); margin 1e-4 m for the rounding of zmin
+    const float reach2 = 2.f * P.h * P.h * (v2 + TORSO_RMAX * TORSO_RMAX * w2);
+    const bool clear = zmin > 1e-4f && zmin * zmin > reach2;
+    if (__ballot(!clear) == 0) {
+      put4(help_lds().torso, l, t, 4);
+      return;
+    }
+  }
   const float v0[6] = {b.wang[0], b.wang[1], b.wang[2], vb[0], vb[1], vb[2]};
   // corner k of the lowest face (k = 0: the lowest corner, torso_corner; 1..3: torso_face's)
   const float z0 = fabsf(R0[2][0]), z1 = fabsf(R0[2][1]), z2 = fabsf(R0[2][2]);

@@ -103,9 +103,11 @@ SCEN_GATE = dict(flight=dict(phys=(3e-6, 1.2e-4), rew=(4e-7, 1.5e-5), terms=(2e-
 RUN_GATE = dict(phys=(4.5e-5, 4e-4), rew=(2.5e-6, 5e-5), terms=(1.5e-5, 1.5e-4), obs=(4.5e-5, 4e-4))
 # The sole-contact scenarios (round 5): their absolute-error quantiles sit at the fp32 floor of a sole depth computed
 # from ~1 m positions (p50 ~5.5e-5, the oracle's own conditioning probe ~4e-5) -- gated at 2x the kernel's measured
-# floor -- and the resolving gate is the per-field SIGNED mean error (ForcedParity.bias_violations) against 3x the
-# kernel's own measured fp32 bias + 6 standard errors per field (BIAS_GATE; tools/gen_sole_bias_gate.py from
-# profiles/r5/bias_*.json, the GPU run of test_forced_sole_contact_scenarios under H12_GATE_MEASURE).
+# floor -- and the resolving gate is the per-field SIGNED mean error (ForcedParity.bias_violations) against 6 standard
+# errors + the signed bias of an independent fp32 evaluation of the scenario (round 6: the oracle's source in single
+# precision, and a fifth of what the MI355X sin / cos errors put into it; none of it the kernel's own mean) per field
+# (BIAS_GATE; tools/gen_sole_bias_gate.py from profiles/r6/bias_*.json, the GPU run of
+# test_forced_sole_contact_scenarios under H12_GATE_MEASURE, and profiles/r6/bias_f32*_oracle.json).
 def _sole_gates():
     import json
 

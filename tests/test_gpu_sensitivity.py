@@ -102,7 +102,9 @@ def test_forced_sole_contact_scenarios(gpu, name, task):
     of ~1 m positions, so fp32 rounding of the state moves the one-step map by ~2e-5 here (the conditioning probe)
     and the absolute-error quantiles cannot resolve 1e-5; the SIGNED mean error per physics-state field does
     (ForcedParity.bias_fields: fp32 rounding averages out over the env-steps, a constant parameter error does not)
-    -- forced.BIAS_GATE, per field 3x the kernel's own measured fp32 bias + 6 standard errors, with tests/test_forced_harness.py showing on the CPU that planted errors in the stiction spring
+    -- forced.BIAS_GATE, per field 6 standard errors + the signed bias of an independent fp32 evaluation of the
+    scenario (round 6, tools/gen_sole_bias_gate.py: no term of it is the kernel's own mean), with
+    tests/test_forced_harness.py showing on the CPU that planted errors in the stiction spring
     k_t (1e-4), its damper c_t (1e-3), a sole sphere's x offset (1e-4), the normal spring (1e-4) and, slipping, the
     dynamic friction coefficient (1e-4) cross it."""
     env, fp = run_sole_scenario(name, task=task)
@@ -118,7 +120,8 @@ def test_forced_sole_contact_scenarios(gpu, name, task):
         with open(out, "w") as f:
             json.dump({"names": names, "mean": m.tolist(), "se": se.tolist(), "quantiles": fp.quantiles(),
                        "probe": fp.quantiles("cond")}, f)
-        return
+        env.close()
+        pytest.skip("H12_GATE_MEASURE: floors written, nothing gated")
     fp.check_quantiles(SCEN_GATE[key])
     bad = fp.bias_violations(BIAS_GATE[key])
     assert not bad, (bad, fp.bias(), fp.report())
