@@ -294,7 +294,9 @@ struct KParams {
   float* cpart;           // [H12_NCSTR_COLS][step_kernel blocks] each block's column maxima of the step
   float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
-  int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised
+  int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised, [2] = step_kernel
+                          // blocks done with their CaT hand-off this launch (cat_fold); from [64] on: each env chunk's
+                          // still (no_move-active) envs as a 32-bit mask (cat_cstill)
   // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
   // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial
   int* diag;
@@ -3755,6 +3757,106 @@ H12_DEV void kernarg_warm() {
       : "memory");
 }
 
+// CaT fold (round 6): the last step_kernel block's helper wave, once every block's hand-off is out (the agent-scope
+// counter, step_kernel): the running maxima (CaT.add, constraint_manager.py:42-78) from the blocks' column maxima and the
+// still envs in ascending order (constraints.no_move hands env i the row of the (i mod m)-th still env,
+// constraints.py:202-238) from the blocks' masks -- what the one-block cat_reduce_kernel launch did (7.1 us per step).
+// Every load of the hand-off is an sc1 (agent-scope relaxed) load, as the hand-off's rule asks.
+H12_DEV int* cat_ccount(const KParams& P) { return P.cmeta + 2; }
+H12_DEV uint32_t* cat_cstill(const KParams& P) { return reinterpret_cast<uint32_t*>(P.cmeta + 64); }
+template <typename T>
+H12_DEV T ld_sc1(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+H12_DEV void cat_fold(const KParams& P, int n) {
+  const int lane = threadIdx.x & 63;
+  const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  // the still envs: lane l owns the env chunks [l q, l q + q), an exclusive prefix of the counts over the lanes
+  const int q = (nb + 63) / 64, c0 = min(nb, lane * q), c1 = min(nb, c0 + q);
+  int cnt = 0;
+  for (int c = c0; c < c1; ++c) cnt += __popc(ld_sc1(&cat_cstill(P)[c]));
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  const int m = __shfl(incl, 63, 64);
+  int off = incl - cnt;
+  for (int c = c0; c < c1; ++c)
+    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) P.clist[off++] = c * ENVS_PER_BLOCK + __builtin_ctz(b);
+  // the column maxima: lane l < 56 takes the column pair l % 28 of the blocks b = l / 28 (mod 2); 8-B sc1 loads of the
+  // [block][56] rows, 32 in flight per batch; then the two block phases combined
+  static_assert(H12_NCSTR_COLS == 56, "28 column pairs, two block phases on 56 lanes");
+  const int pr = lane % 28, ph = lane / 28;
+  float mx0 = CAT_NEG, mx1 = CAT_NEG;
+  if (lane < 56) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(P.cpart) + pr;
+    for (int b0 = ph; b0 < nb; b0 += 64) {
+      uint64_t w[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) w[k] = ld_sc1(src + (size_t)min(b0 + 2 * k, nb - 1) * 28);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const float lo = __uint_as_float((uint32_t)w[k]), hi = __uint_as_float((uint32_t)(w[k] >> 32));
+        const bool ok = b0 + 2 * k < nb;
+        mx0 = ok ? fmaxf(mx0, lo) : mx0;
+        mx1 = ok ? fmaxf(mx1, hi) : mx1;
+      }
+    }
+  }
+  mx0 = fmaxf(mx0, __shfl(mx0, min(lane + 28, 63), 64));
+  mx1 = fmaxf(mx1, __shfl(mx1, min(lane + 28, 63), 64));
+  // lane col (< 56) takes its column from lane col / 2
+  const float a0 = __shfl(mx0, lane >> 1, 64), a1 = __shfl(mx1, lane >> 1, 64);
+  if (lane < H12_NCSTR_COLS) {
+    float cm = (lane & 1) ? a1 : a0;
+    const bool nm = lane >= C_COL0[H12_C_NO_MOVE] && lane < C_COL0[H12_C_NO_MOVE + 1];
+    if (nm && m == 0) cm = 0.f;  // constraints.no_move returns zeros when no env is still
+    cm = fmaxf(cm, 1e-6f);       // constraint.max(dim=0).clamp(min=1e-6)
+    const float old = P.crun[lane];
+    const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
+    P.crun[lane] = run;
+    P.crun[H12_NCSTR_COLS + lane] = 1.f / run;
+  }
+  if (lane == 0) {
+    P.cmeta[0] = m;
+    P.cmeta[1] = 1;
+    __hip_atomic_store(cat_ccount(P), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's count
+  }
+}
+
+// CaT hand-off (round 6): step_kernel's contact wave, after barrier L (it idles there until barrier F): this block's
+// column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs only) as one [block][56] row and
+// its still envs as a mask, sc1 stores waited for, then one agent-scope add per block; true on the block whose add came
+// last, which folds every block's (cat_fold, after its rows) -- the cross-workgroup hand-off of MI355X_MICROARCH.md
+// (stores and loads all sc1, one atomic per workgroup, the last adder loads after its add returned).  The one-block
+// cat_reduce_kernel launch it replaces took 7.1 us per step (rocprofv3, profiles/r6/)
+H12_DEV void cat_handoff(const KParams& P, int n) {
+  const int col = threadIdx.x & 63;
+  const int ne = min(ENVS_PER_BLOCK, n - step_block() * ENVS_PER_BLOCK);
+  const CatLds& cv = cat_lds();
+  if (col < H12_NCSTR_COLS) {
+    const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
+    float m = CAT_NEG;
+#pragma unroll
+    for (int j = 0; j < ENVS_PER_BLOCK; ++j) {  // unrolled: the LDS reads issue back to back
+      const float x = cv[col][j];
+      const bool ok = j < ne && (!nm || cv[CAT_ROW_NOMOVE][j] != 0.f);
+      m = ok ? fmaxf(m, x) : m;
+    }
+    __hip_atomic_store(&P.cpart[(size_t)blockIdx.x * H12_NCSTR_COLS + col], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t still = (uint32_t)__ballot(col < ENVS_PER_BLOCK && col < ne && cv[CAT_ROW_NOMOVE][col] != 0.f);
+  if (col == 0) __hip_atomic_store(&cat_cstill(P)[step_block()], still, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// ... after the wave's s_waitcnt vmcnt(0) (the stores above have completed): the block's add.  The returned count is
+// only looked at after barrier F and the rows (cat_is_last), so its round trip overlaps them
+H12_DEV int cat_arrive(const KParams& P) {
+  int old = -1;
+  if ((threadIdx.x & 63) == 0) old = __hip_atomic_fetch_add(cat_ccount(P), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return old;
+}
+H12_DEV bool cat_is_last(int old) { return __shfl(old, 0, 64) == (int)gridDim.x - 1; }
+
 // LDS budget of step_kernel (round 6): the static hand-offs (HelpLds, SelfLds; the same for every feature level K) plus
 // the fused path's dynamic FuseLds must fit the CU's 160 KiB.  A dispatch over the limit is not a HIP error code: the
 // queue aborts (HSA_STATUS_ERROR_INVALID_ALLOCATION) and the next call reports an illegal address (round 5's r7e
@@ -3788,24 +3890,6 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
       {
         __syncthreads();  // L: the final state and the reward inputs (and CaT constraint values)
-        if (Feat<K>::ext && P.cat) {
-          // CaT: this block's column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs
-          // only), one value per column and block -- cat_reduce_kernel folds the blocks
-          const int col = threadIdx.x - BLOCK;
-          const int ne = min(ENVS_PER_BLOCK, W.n - step_block() * ENVS_PER_BLOCK);
-          if (col < H12_NCSTR_COLS) {
-            const CatLds& cv = cat_lds();
-            const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
-            float m = CAT_NEG;
-#pragma unroll
-            for (int j = 0; j < ENVS_PER_BLOCK; ++j) {  // unrolled: the LDS reads issue back to back
-              const float x = cv[col][j];
-              const bool ok = j < ne && (!nm || cv[CAT_ROW_NOMOVE][j] != 0.f);
-              m = ok ? fmaxf(m, x) : m;
-            }
-            P.cpart[(size_t)col * gridDim.x + blockIdx.x] = m;
-          }
-        }
       }
       // ---- rewards on the pre-reset state (mdp_terms: the 12 Flat / 20 extended terms), the episode sums, the reward
       // output and the episode-log values of the resetting envs -- the physics wave's until round 4: it resets and
@@ -3879,12 +3963,20 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       else self_wave<K>(P, W.n, nsteps, fc);
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
       __syncthreads();  // L (the helper's final sole contact state is in LDS)
+      const bool cat_w = Feat<K>::ext && P.cat && threadIdx.x < 3 * BLOCK;  // the contact wave: the CaT hand-off
+      if (cat_w) cat_handoff(P, W.n);
+      int cat_old = -1;
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);
+        if (cat_w) cat_old = cat_arrive(P);
         H12_BW_F_ARRIVAL();
         __syncthreads();  // F
         fuse_late(P, A, fc, W.n, ft, fnt);
+      } else if (cat_w) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        cat_old = cat_arrive(P);
       }
+      if (cat_w && cat_is_last(cat_old)) cat_fold(P, W.n);
     }
     PH_HELPER_END();
     return;
@@ -4123,68 +4215,6 @@ __global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, Te
   if (Feat<K>::ext && P.cat) cat_constraints<false, false>(P, W, e, leg, s, tau, fmax_foot, term, R, s.eplen);
 }
 
-
-// CaT: the running maxima (CaT.add, constraint_manager.py:42-78) and the compacted list of still envs in
-// ascending order (constraints.no_move hands env i the row of the (i mod m)-th still env,
-// constraints.py:202-238).  One block; per 1024-env chunk a ballot prefix in each wave and one LDS pass over
-// the wave totals.  The column maxima (CaT.add: constraint.max(dim=0)) fold step_kernel's per-block maxima
-// (cpart, formed by its helper wave from LDS: no separate pass over the [col][n] scratch).
-constexpr int CAT_RBLOCK = 1024;
-__global__ void __launch_bounds__(CAT_RBLOCK) cat_reduce_kernel(KParams P, int n) {
-  __shared__ int s_wsum[CAT_RBLOCK / 64];
-  __shared__ int s_base;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_base = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < n; c0 += CAT_RBLOCK) {
-    const int i = c0 + tid;
-    const bool f = i < n && P.cscr[(size_t)CAT_ROW_NOMOVE * n + i] != 0.f;
-    const unsigned long long b = __ballot(f);
-    const int below = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wsum[wave] = __popcll(b);
-    __syncthreads();
-    int off = s_base;
-    for (int w = 0; w < wave; ++w) off += s_wsum[w];
-    if (f) P.clist[off + below] = i;
-    __syncthreads();
-    if (tid == 0) {
-      int t = 0;
-      for (int w = 0; w < CAT_RBLOCK / 64; ++w) t += s_wsum[w];
-      s_base += t;
-    }
-    __syncthreads();
-  }
-  const int m = s_base;
-  // the column maxima: 16 threads per column fold step_kernel's per-block maxima, then a 16-lane shuffle
-  __shared__ float s_cm[H12_NCSTR_COLS];
-  static_assert(H12_NCSTR_COLS * 16 <= CAT_RBLOCK, "16 threads per column");
-  {
-    const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-    const int col = tid >> 4, sub = tid & 15;
-    float mx = CAT_NEG;
-    if (col < H12_NCSTR_COLS)
-      for (int b = sub; b < nb; b += 16) mx = fmaxf(mx, P.cpart[(size_t)col * nb + b]);
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-    if (sub == 0 && col < H12_NCSTR_COLS) s_cm[col] = mx;
-  }
-  __syncthreads();
-  if (tid < H12_NCSTR_COLS) {
-    float cm = s_cm[tid];
-    const bool nm = tid >= C_COL0[H12_C_NO_MOVE] && tid < C_COL0[H12_C_NO_MOVE + 1];
-    if (nm && m == 0) cm = 0.f;  // constraints.no_move returns zeros when no env is still
-    cm = fmaxf(cm, 1e-6f);       // constraint.max(dim=0).clamp(min=1e-6)
-    const float old = P.crun[tid];
-    const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
-    P.crun[tid] = run;
-    P.crun[H12_NCSTR_COLS + tid] = 1.f / run;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    P.cmeta[0] = m;
-    P.cmeta[1] = 1;
-  }
-}
 
 // CaT, last: per env, p = min_p + clamp(c / running_max, 0, 1) (max_p - min_p) on violated columns, the max over
 // all columns scales the reward (CaTEnv.step, cat_env.py:148-153) and is returned as dones (1 where the env
@@ -4974,8 +5004,10 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
   if (h->P.cat) {
     const size_t nn = (size_t)n_envs;
     const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-    const size_t bytes_cat = sizeof(float) * CAT_ROWS * nn + sizeof(float) * H12_NCSTR_COLS * nbk +
-                             sizeof(float) * 2 * H12_NCSTR_COLS + sizeof(int) * nn + sizeof(int) * 4;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };  // every section 256-B aligned (cat_fold's 8-B loads)
+    const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * H12_NCSTR_COLS * nbk) +
+                             al(sizeof(float) * 2 * H12_NCSTR_COLS) + al(sizeof(int) * nn) + 256 +
+                             al(sizeof(uint32_t) * nbk);
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
     if (e != hipSuccess) {
@@ -4986,11 +5018,11 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
       return set_err(H12_E_ALLOC, "hipMalloc(CaT buffers): %s", hipGetErrorString(e));
     }
     char* q = (char*)h->cat_mem;
-    h->P.cscr = (float*)q; q += sizeof(float) * CAT_ROWS * nn;
-    h->P.cpart = (float*)q; q += sizeof(float) * H12_NCSTR_COLS * nbk;
-    h->P.crun = (float*)q; q += sizeof(float) * 2 * H12_NCSTR_COLS;
-    h->P.clist = (int*)q; q += sizeof(int) * nn;
-    h->P.cmeta = (int*)q;
+    h->P.cscr = (float*)q; q += al(sizeof(float) * CAT_ROWS * nn);
+    h->P.cpart = (float*)q; q += al(sizeof(float) * H12_NCSTR_COLS * nbk);
+    h->P.crun = (float*)q; q += al(sizeof(float) * 2 * H12_NCSTR_COLS);
+    h->P.clist = (int*)q; q += al(sizeof(int) * nn);
+    h->P.cmeta = (int*)q;  // 64 ints of meta, then the still masks (cat_ccount, cat_cstill)
   }
   h->device = device;
   if (h->P.task == H12_TASK_FLAT) {
@@ -5134,8 +5166,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   HIP_TRY(hipGetLastError());
   if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
   if (h->P.cat) {
-    hipLaunchKernelGGL(cat_reduce_kernel, dim3(1), dim3(CAT_RBLOCK), 0, st, h->P, h->W.n);
-    HIP_TRY(hipGetLastError());
+    // (the running maxima and the still list were folded by step_kernel's last block, cat_fold)
     static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
     CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
     hipLaunchKernelGGL(cat_prob_kernel, dim3((h->W.n + CAT_PBLOCK - 1) / CAT_PBLOCK), dim3(CAT_PBLOCK), 0, st, h->P,

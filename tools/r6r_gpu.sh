@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/r6r_tests.txt 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r6r_tests.txt; exit 1; }
+tail -1 gpurun_out/r6r_tests.txt
+for r in 1 2; do
+  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 1000 > gpurun_out/r6r_new$r.json 2>/dev/null || { echo "bench failed"; exit 1; }
+  H12ENV_LIB=$PWD/tools/_variants/lib_r6lds.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 1000 > gpurun_out/r6r_old$r.json 2>/dev/null || { echo "bench old failed"; exit 1; }
+  for v in new old; do tail -1 gpurun_out/r6r_$v$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('flat $v', round(d['value']/1e6,2), round(d['ms_per_step']*1e3,2), 'step_kernel', round(d['roofline']['kernel_ms_avg']*1e3,2))"; done
+done

@@ -135,7 +135,7 @@ PATCHES_HEAD["epb16h_halfx"] = PATCHES_HEAD["epb16h_half"] + [
 # of one env on the same address in the foot-foot passes) replaced by consuming the values -- what the atomics' address
 # conflicts cost the candidate blocks
 PATCHES_HEAD["self_noatomic"] = [
-    ("        atomicAdd(&al(a), F[a]); atomicAdd(&al(3 + a), m[a]);\n        atomicAdd(&ar(a), -F[a]); atomicAdd(&ar(3 + a), -m[a]);\n",
+    ("        lds_add(al(a), F[a]); lds_add(al(3 + a), m[a]);\n        lds_add(ar(a), -F[a]); lds_add(ar(3 + a), -m[a]);\n",
      "        asm volatile(\"\" :: \"v\"(F[a]), \"v\"(m[a]));\n")]
 # round 6 bias elimination (correct results, slower math): one single-instruction operation of the kernel replaced by its
 # correctly rounded form, to see which one carries the signed bias left after the fsincos fix (tools/bias_probe.py)
@@ -151,8 +151,6 @@ _ACC = {"acc_rsq": "#define __builtin_amdgcn_rsqf(x) (1.0f / __builtin_sqrtf(x))
 for _k, _v in _ACC.items():
     PATCHES_HEAD[_k] = [("using namespace h12;\n", "using namespace h12;\n" + _v)]
 PATCHES_HEAD["acc_all"] = [("using namespace h12;\n", "using namespace h12;\n" + "".join(_ACC.values()))]
-# round 6 check: the torso corners back on lane 0 alone (the pre-split helper_torso), everything else current
-PATCHES_HEAD["torso_lane0"] = [("  ImplC ict;\n  float dummy[2], p[3];\n  corner_k(leg ? 2 : 0, p);\n  const bool c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict,\n                                          leg != 0);\n  const bool c0 = leg ? pair_swap_i(c ? 1 : 0) != 0 : c;  // the lowest corner's contact (lane 0's)\n  if constexpr (T) {\n    if (!c0)  // leg 1's corner 2 was speculative\n      for (int i = 0; i < 9; ++i) t[i] = 0.f;\n  }\n  if (c0 || !T) {\n    corner_k(leg ? 3 : 1, p);\n    ImplC dz;\n    contact_sphere<false, T, true>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, dz);\n  }\n", '  ImplC ict;\n  float dummy[2], p[3];\n  bool c = false;\n  if (leg == 0) {\n    corner_k(0, p);\n    c = contact_sphere<false, T>(P, R0, pb0, v0, p, 0.f, t, t + 6, dummy, false, 1.f, org, P.mus, P.mud, ict);\n    if (c || !T) torso_face<T>(P, R0, pb0, v0, org, t, t + 6);\n  }\n')]
 # round 6 block-tail probes (timing only, results wrong): the flat torso contact off the helper wave; the helper waves'
 # drain of the row LDS-DMA before barrier R2 of inner step 1 skipped
 PATCHES_HEAD["no_torso"] = [("      if constexpr (!Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n", "")]
