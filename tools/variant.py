@@ -155,6 +155,36 @@ PATCHES_HEAD["acc_all"] = [("using namespace h12;\n", "using namespace h12;\n" +
 # drain of the row LDS-DMA before barrier R2 of inner step 1 skipped
 PATCHES_HEAD["no_torso"] = [("      if constexpr (!Feat<K>::terrain) helper_torso<K>(P, l, leg, b, vb, R0, pb0, org);\n", "")]
 PATCHES_HEAD["no_drain"] = [("  if (f.on && it == 1) __builtin_amdgcn_s_waitcnt(0);", "  (void)f; (void)it;")]
+# round 6 private-segment fix B (measured, not kept: profiles/r6/not_kept/private_segment_ab.txt): the StepArgs output
+# pointers re-read after the physics loop through an opaque kernarg-segment pointer, so the entry's 16-dword StepArgs
+# s_load is not live across the loop; and the probe on top of it (timing only): a never-taken dynamically indexed
+# private array that gives the step kernel a private segment again, with real scratch instructions
+_LATE = """constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+constexpr size_t STEP_ARGS_KOFF = align_up(align_up(sizeof(KParams), alignof(Workspace)) + sizeof(Workspace), alignof(StepArgs));
+H12_DEV const __attribute__((address_space(4))) StepArgs& late_step_args() {
+  auto p = (const __attribute__((address_space(4))) StepArgs*)(
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + STEP_ARGS_KOFF);
+  asm volatile("" : "+s"(p));
+  return *p;
+}
+"""
+PATCHES_HEAD["late_step_args"] = [
+    ("H12_DEV void kernarg_warm() {", _LATE + "H12_DEV void kernarg_warm() {"),
+    ("      if (he < W.n) {\n        if (hleg == 0) A.rew[he] = r;", "      const auto& AL = late_step_args();\n"
+     "      if (he < W.n) {\n        if (hleg == 0) AL.rew[he] = r;"),
+    ("      if (lv) A.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;",
+     "      if (lv) AL.log_part[(size_t)v * gridDim.x + blockIdx.x] = lacc;"),
+    ("    if (leg == 0) {\n      A.term[e] = (uint8_t)term;\n      A.trunc[e] = (uint8_t)tout;\n    }\n"
+     "    if (A.applied_torque)\n      for (int k = 0; k < NL; ++k) A.applied_torque[",
+     "    const auto& AL = late_step_args();\n    if (leg == 0) {\n      AL.term[e] = (uint8_t)term;\n"
+     "      AL.trunc[e] = (uint8_t)tout;\n    }\n    if (AL.applied_torque)\n"
+     "      for (int k = 0; k < NL; ++k) AL.applied_torque["),
+    ("    if (A.foot_force) A.foot_force[2 * e + leg] = flast_foot;",
+     "    if (AL.foot_force) AL.foot_force[2 * e + leg] = flast_foot;")]
+PATCHES_HEAD["scratch_pad"] = PATCHES_HEAD["late_step_args"] + [
+    ("  H12_BW_KSTART();\n  kernarg_warm();\n",
+     "  H12_BW_KSTART();\n  kernarg_warm();\n  if (P.dbg_norel == 0x5eed) {\n    volatile int pad[17];\n"
+     "    pad[threadIdx.x % 17] = (int)threadIdx.x;\n    P.diag[0] = pad[(threadIdx.x + 1) % 17];\n  }\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
