@@ -291,12 +291,13 @@ struct KParams {
   float cvlim[NL], celim[NL];  // joint velocity / effort limits (leg-symmetric)
   float c_ff, c_nm_dz, c_nm_v, c_or, c_h, c_hstd, c_clr, c_clr_dz;
   float* cscr;            // [CAT_ROWS][n] raw constraints of the step (+ no_move flag, pre-reset episode length)
-  float* cpart;           // [H12_NCSTR_COLS][step_kernel blocks] each block's column maxima of the step
   float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
   int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised, [2] = step_kernel
-                          // blocks done with their CaT hand-off this launch (cat_fold); from [64] on: each env chunk's
-                          // still (no_move-active) envs as a 32-bit mask (cat_cstill)
+                          // blocks done with their CaT hand-off this launch (cat_fold); [4..5] = the published fold
+                          // (epoch << 32 | m, cat_pub); [8..63] = the step's column maxima as order-preserving integer
+                          // encodings, maxed by every block (cat_cmax); from [64] on: each env chunk's still
+                          // (no_move-active) envs as a 32-bit mask (cat_cstill)
   // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
   // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial
   int* diag;
@@ -1592,7 +1593,10 @@ H12_DEV void fuse_drain(const FuseCtx& f, int it) {
 
 // CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the contact wave's
 // R1 hand-off array (free once the last inner step's physics wave has read it)
-typedef float CatLds[H12_NCSTR_COLS + 1][ENVS_PER_BLOCK];
+typedef float CatLds[H12_NCSTR_COLS + 5][ENVS_PER_BLOCK];
+// rows past the values: CAT_ROW_EPLEN; CAT_LROW_EPOCH (the fold epoch this block waits past, its bits in [0]);
+// CAT_LROW_RINV, +1: the running maxima's reciprocals once folded (cat_prob_inline)
+constexpr int CAT_LROW_EPOCH = H12_NCSTR_COLS + 2, CAT_LROW_RINV = H12_NCSTR_COLS + 3;
 // only the first half: cw1[1] holds the reward inputs (put_rin), written in the same window before barrier L
 static_assert(sizeof(CatLds) <= sizeof(HelpLds::cw1[0]), "CaT values fit the first sole hand-off half");
 H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().cw1[0][0][0]); }
@@ -2961,7 +2965,7 @@ H12_DEV void cat_constraints(const KParams& P, const Workspace& W, int e, int le
   auto put = [&](int row, float v) {
     S[(size_t)row * n + e] = v;
     if constexpr (LDS) {
-      if (row <= CAT_ROW_NOMOVE) cat_lds()[row][e & (ENVS_PER_BLOCK - 1)] = v;
+      if (row <= CAT_ROW_EPLEN) cat_lds()[row][e & (ENVS_PER_BLOCK - 1)] = v;
     }
   };
   const float sg = leg ? -1.f : 1.f;
@@ -3619,13 +3623,17 @@ struct StepArgs {
   float* applied_torque;
   float* foot_force;
   const uint8_t* reset_mask;
-  const float* q_ref;  // physics-only hook
+  union {
+    const float* q_ref;  // physics_kernel: the physics-only hook's joint targets
+    float* cstr_prob;    // step_kernel with cat_inline: CaT's termination probabilities (h12env_outputs.cstr_prob), or null
+  };
   float* frame;        // [45][n] noise-free observation frame scratch (handle-owned)
   int64_t env_offset;
   uint32_t lo, hi;
   int n_substeps;
   int dz_slot;  // deadzone counter read this step (P.dz_cnt[dz_slot]); +1 is counted into, +2 zeroed
   int fuse;     // the observation rows are assembled inside step_kernel (FuseCtx; dynamic LDS)
+  int cat_inline;  // CaT: step_kernel also applies the probabilities (cat_prob_inline; the grid is resident)
   const uint8_t* fuse_code;  // fuse_code_table of the handle's history length
   float* frame_out;         // (n, 45) noisy scaled frames as they enter the history (fused path), or null
 };
@@ -3757,18 +3765,40 @@ H12_DEV void kernarg_warm() {
       : "memory");
 }
 
-// CaT fold (round 6): the last step_kernel block's helper wave, once every block's hand-off is out (the agent-scope
-// counter, step_kernel): the running maxima (CaT.add, constraint_manager.py:42-78) from the blocks' column maxima and the
-// still envs in ascending order (constraints.no_move hands env i the row of the (i mod m)-th still env,
-// constraints.py:202-238) from the blocks' masks -- what the one-block cat_reduce_kernel launch did (7.1 us per step).
-// Every load of the hand-off is an sc1 (agent-scope relaxed) load, as the hand-off's rule asks.
+// CaT fold (round 6): the contact wave of the last step_kernel block to arrive, once every block's hand-off is out (the
+// agent-scope counter, cat_arrive): the running maxima (CaT.add, constraint_manager.py:42-78) from the column maxima
+// every block maxed in, and the still envs in ascending order (constraints.no_move hands env i the row of the
+// (i mod m)-th still env, constraints.py:202-238) from the blocks' masks -- what the one-block cat_reduce_kernel launch
+// did (7.1 us per step).  Every load of the hand-off is an sc1 (agent-scope relaxed) load, as the hand-off's rule asks;
+// with cat_inline the fold is published (cat_pub) once its stores have completed.
 H12_DEV int* cat_ccount(const KParams& P) { return P.cmeta + 2; }
 H12_DEV uint32_t* cat_cstill(const KParams& P) { return reinterpret_cast<uint32_t*>(P.cmeta + 64); }
 template <typename T>
 H12_DEV T ld_sc1(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-H12_DEV void cat_fold(const KParams& P, int n) {
+template <typename T>
+H12_DEV void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// the published fold (cat_inline): epoch << 32 | m, one 8-B word -- the epoch +1 per fold, stored after the fold's other
+// stores completed; the blocks wait past the epoch they read before their own arrival (no block can read the new one
+// early: the fold needs every arrival), and the word that ends the wait carries m
+H12_DEV unsigned long long* cat_pub(const KParams& P) { return reinterpret_cast<unsigned long long*>(P.cmeta + 4); }
+// the column maxima: float -> unsigned with the same order (sign bit flipped for >= 0, all bits for < 0), so every
+// block's maxima go in with one unsigned atomic max per column (exact, order-free); 0 (below every encoding) = none
+H12_DEV unsigned* cat_cmax(const KParams& P) { return reinterpret_cast<unsigned*>(P.cmeta + 8); }
+H12_DEV unsigned cat_enc(float f) {
+  const unsigned b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+H12_DEV float cat_dec(unsigned u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
+H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
   const int lane = threadIdx.x & 63;
   const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  static_assert(H12_NCSTR_COLS <= 56, "the column maxima fit cmeta[8..63]");
+  // the column maxima (lane col), read and reset for the next step (the blocks' atomic maxima, cat_handoff)
+  float cmx = CAT_NEG;
+  if (lane < H12_NCSTR_COLS) {
+    cmx = cat_dec(ld_sc1(cat_cmax(P) + lane));
+    st_sc1(cat_cmax(P) + lane, 0u);
+  }
   // the still envs: lane l owns the env chunks [l q, l q + q), an exclusive prefix of the counts over the lanes
   const int q = (nb + 63) / 64, c0 = min(nb, lane * q), c1 = min(nb, c0 + q);
   int cnt = 0;
@@ -3782,58 +3812,52 @@ H12_DEV void cat_fold(const KParams& P, int n) {
   const int m = __shfl(incl, 63, 64);
   int off = incl - cnt;
   for (int c = c0; c < c1; ++c)
-    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) P.clist[off++] = c * ENVS_PER_BLOCK + __builtin_ctz(b);
-  // the column maxima: lane l < 56 takes the column pair l % 28 of the blocks b = l / 28 (mod 2); 8-B sc1 loads of the
-  // [block][56] rows, 32 in flight per batch; then the two block phases combined
-  static_assert(H12_NCSTR_COLS == 56, "28 column pairs, two block phases on 56 lanes");
-  const int pr = lane % 28, ph = lane / 28;
-  float mx0 = CAT_NEG, mx1 = CAT_NEG;
-  if (lane < 56) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(P.cpart) + pr;
-    for (int b0 = ph; b0 < nb; b0 += 64) {
-      uint64_t w[32];
-#pragma unroll
-      for (int k = 0; k < 32; ++k) w[k] = ld_sc1(src + (size_t)min(b0 + 2 * k, nb - 1) * 28);
-#pragma unroll
-      for (int k = 0; k < 32; ++k) {
-        const float lo = __uint_as_float((uint32_t)w[k]), hi = __uint_as_float((uint32_t)(w[k] >> 32));
-        const bool ok = b0 + 2 * k < nb;
-        mx0 = ok ? fmaxf(mx0, lo) : mx0;
-        mx1 = ok ? fmaxf(mx1, hi) : mx1;
-      }
-    }
-  }
-  mx0 = fmaxf(mx0, __shfl(mx0, min(lane + 28, 63), 64));
-  mx1 = fmaxf(mx1, __shfl(mx1, min(lane + 28, 63), 64));
-  // lane col (< 56) takes its column from lane col / 2
-  const float a0 = __shfl(mx0, lane >> 1, 64), a1 = __shfl(mx1, lane >> 1, 64);
+    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) st_sc1(&P.clist[off++], c * ENVS_PER_BLOCK + __builtin_ctz(b));
   if (lane < H12_NCSTR_COLS) {
-    float cm = (lane & 1) ? a1 : a0;
+    float cm = cmx;
     const bool nm = lane >= C_COL0[H12_C_NO_MOVE] && lane < C_COL0[H12_C_NO_MOVE + 1];
     if (nm && m == 0) cm = 0.f;  // constraints.no_move returns zeros when no env is still
     cm = fmaxf(cm, 1e-6f);       // constraint.max(dim=0).clamp(min=1e-6)
     const float old = P.crun[lane];
     const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
-    P.crun[lane] = run;
-    P.crun[H12_NCSTR_COLS + lane] = 1.f / run;
+    st_sc1(&P.crun[lane], run);
+    st_sc1(&P.crun[H12_NCSTR_COLS + lane], 1.f / run);
   }
   if (lane == 0) {
-    P.cmeta[0] = m;
-    P.cmeta[1] = 1;
-    __hip_atomic_store(cat_ccount(P), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's count
+    st_sc1(&P.cmeta[0], m);
+    st_sc1(&P.cmeta[1], 1);
+    st_sc1(cat_ccount(P), 0);  // the next launch's count
+  }
+  if (inl) {  // every store above has completed, then the epoch: the blocks' cat_prob_inline may read them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      st_sc1(cat_pub(P), (unsigned long long)(__float_as_uint(cat_lds()[CAT_LROW_EPOCH][0]) + 1u) << 32 | (unsigned)m);
   }
 }
 
 // CaT hand-off (round 6): step_kernel's contact wave, after barrier L (it idles there until barrier F): this block's
-// column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs only) as one [block][56] row and
-// its still envs as a mask, sc1 stores waited for, then one agent-scope add per block; true on the block whose add came
-// last, which folds every block's (cat_fold, after its rows) -- the cross-workgroup hand-off of MI355X_MICROARCH.md
-// (stores and loads all sc1, one atomic per workgroup, the last adder loads after its add returned).  The one-block
-// cat_reduce_kernel launch it replaces took 7.1 us per step (rocprofv3, profiles/r6/)
-H12_DEV void cat_handoff(const KParams& P, int n) {
+// column maxima (CaT.add's constraint.max(dim=0); no_move columns over the still envs only) into the step's maxima with
+// one agent-scope atomic max per column (a [block][56] row for the fold to read took 2-3 more memory round trips on its
+// critical path), its still envs as an sc1-stored mask, all waited for, then one agent-scope add per block (cat_arrive);
+// the block whose add came last folds (cat_fold) -- the cross-workgroup hand-off of MI355X_MICROARCH.md (stores, atomics
+// and loads all agent scope, one arrival atomic per workgroup, the last adder loads after its add returned).  The
+// one-block cat_reduce_kernel launch it replaces took 7.1 us per step (rocprofv3, profiles/r6/)
+H12_DEV unsigned cat_handoff(const KParams& P, int n, bool inl) {
   const int col = threadIdx.x & 63;
   const int ne = min(ENVS_PER_BLOCK, n - step_block() * ENVS_PER_BLOCK);
   const CatLds& cv = cat_lds();
+  // cat_inline: the fold epoch before this block's arrival (in flight until the arrival's vmcnt(0)), and the still
+  // envs' no_move rows again as sc1 stores (cat_prob_inline reads them across blocks: constraints.no_move's remap)
+  const unsigned e0 = inl && col == 0 ? (unsigned)(ld_sc1(cat_pub(P)) >> 32) : 0u;
+  if (inl) {
+    constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NMC = C_COL0[H12_C_NO_MOVE + 1] - NM0;
+    const int j = col & (ENVS_PER_BLOCK - 1);
+    if (j < ne && cv[CAT_ROW_NOMOVE][j] != 0.f) {
+      const size_t e = (size_t)step_block() * ENVS_PER_BLOCK + j;
+      for (int k = col / ENVS_PER_BLOCK; k < NMC; k += 64 / ENVS_PER_BLOCK)
+        st_sc1(&P.cscr[(size_t)(NM0 + k) * n + e], cv[NM0 + k][j]);
+    }
+  }
   if (col < H12_NCSTR_COLS) {
     const bool nm = col >= C_COL0[H12_C_NO_MOVE] && col < C_COL0[H12_C_NO_MOVE + 1];
     float m = CAT_NEG;
@@ -3843,10 +3867,11 @@ H12_DEV void cat_handoff(const KParams& P, int n) {
       const bool ok = j < ne && (!nm || cv[CAT_ROW_NOMOVE][j] != 0.f);
       m = ok ? fmaxf(m, x) : m;
     }
-    __hip_atomic_store(&P.cpart[(size_t)blockIdx.x * H12_NCSTR_COLS + col], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(cat_cmax(P) + col, cat_enc(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint32_t still = (uint32_t)__ballot(col < ENVS_PER_BLOCK && col < ne && cv[CAT_ROW_NOMOVE][col] != 0.f);
   if (col == 0) __hip_atomic_store(&cat_cstill(P)[step_block()], still, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return e0;
 }
 // ... after the wave's s_waitcnt vmcnt(0) (the stores above have completed): the block's add.  The returned count is
 // only looked at after barrier F and the rows (cat_is_last), so its round trip overlaps them
@@ -3856,6 +3881,122 @@ H12_DEV int cat_arrive(const KParams& P) {
   return old;
 }
 H12_DEV bool cat_is_last(int old) { return __shfl(old, 0, 64) == (int)gridDim.x - 1; }
+
+// CaT's episode statistics of the resetting envs (cat_prob_inline, cat_prob_kernel): L[k][j] holds env j's
+// value k of one step_kernel block (k < NCSTR: the violation sum over the episode length, then the probability sum;
+// zero for envs that do not reset), summed in env order by lane k and added to the block's partial slot -- the same
+// order on both paths (float atomics from one instruction, the round-5 form, summed in an order the two paths did not
+// share).  `any`: some env of the block resets (else nothing to add).
+H12_DEV void cat_log_block(uint32_t cmask, const float (*L)[ENVS_PER_BLOCK], int k, bool any, float* log_part,
+                           int log_nb, int slot) {
+  if (!any || !log_part || k >= 2 * H12_NCSTR || !((cmask >> (k % H12_NCSTR)) & 1u)) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < ENVS_PER_BLOCK; ++j) sum += L[k][j];
+  float& d = log_part[(size_t)(LOG_NSTEP + k) * log_nb + slot];
+  d = d + sum;
+}
+constexpr int CAT_WAIT_POLLS = 1 << 18;
+// step_kernel's KParams read through the kernarg segment pointer (its first argument, offset 0) instead of the by-value
+// parameter: code that indexes the parameter in a way the compiler cannot resolve (here the new CaT functions' loads,
+// merged into selects of addresses) makes it copy all 856 B of KParams to scratch first
+H12_DEV const __attribute__((address_space(4))) KParams& kparams4() {
+  return *(const __attribute__((address_space(4))) KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+constexpr int cat_col_term(int col) {
+  int t = 0;
+  while (C_COL0[t + 1] <= col) ++t;
+  return t;
+}
+// one env's probabilities (the leg-0 lane of a pair): the reward factor 1 - p_max, the dones' probability, the
+// constraint sums, and its episode statistics into lg (zero unless it resets)
+H12_DEV float cat_prob_env(const Workspace& W, const StepArgs& A, int he, int j, bool reset, const float* vs,
+                           const float* vp, int src, const float* rinv, float* lg) {
+  const auto& P = kparams4();
+  const CatLds& cv = cat_lds();
+  constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NM1 = C_COL0[H12_C_NO_MOVE + 1];
+  float nmv[NM1 - NM0];
+#pragma unroll
+  for (int k = 0; k < NM1 - NM0; ++k) nmv[k] = src >= 0 ? ld_sc1(&P.cscr[(size_t)(NM0 + k) * W.n + src]) : 0.f;
+  // one flat loop over the columns (constant trip count: fully unrolled, every index static -- the nested form left
+  // a dynamic KParams index that made the compiler copy KParams to scratch); max is exact, so the order is free
+  float pt[H12_NCSTR];
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) pt[t] = 0.f;
+#pragma unroll
+  for (int col = 0; col < H12_NCSTR_COLS; ++col) {
+    const int t = cat_col_term(col);
+    const bool on_t = (P.cmask >> t) & 1u;
+    const float c = (col >= NM0 && col < NM1) ? nmv[col - NM0] : cv[col][j];
+    const float p = P.cminp + fminf(fmaxf(c * rinv[col], 0.f), 1.f) * (P.cmaxp[t] - P.cminp);
+    pt[t] = fmaxf(pt[t], (on_t && c > 0.f) ? p : 0.f);
+  }
+  float pmax = 0.f;
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) pmax = fmaxf(pmax, pt[t]);
+  if (A.cstr_prob) A.cstr_prob[he] = reset ? 1.f : pmax;
+  const float inv_len = 1.f / cv[CAT_ROW_EPLEN][j];
+  const int n = W.n;
+#pragma unroll
+  for (int t = 0; t < H12_NCSTR; ++t) {
+    lg[t] = lg[H12_NCSTR + t] = 0.f;
+    if (!((P.cmask >> t) & 1u)) continue;  // (the sums of an inactive term stay as they are)
+    float a = vs[t] + (pt[t] > 0.f ? 1.f : 0.f), b = vp[t] + pt[t];
+    if (reset) {
+      lg[t] = a * inv_len;
+      lg[H12_NCSTR + t] = b * inv_len;
+      a = b = 0.f;
+    }
+    W.F[(size_t)(H12_F_CSTR_SUM + t) * n + he] = a;
+    W.F[(size_t)(H12_F_CSTR_P + t) * n + he] = b;
+  }
+  float keep = 1.f - pmax;  // pinned as in cat_prob_kernel (the same rounding on both paths)
+  pin(keep);
+  return keep;
+}
+// CaT probabilities inside step_kernel (round 6, A.cat_inline: the whole grid is resident, h12env_create checks it):
+// cat_prob_kernel's per-env step (below) by the helper wave after barrier F, once the last block's fold is published --
+// the running maxima's reciprocals, the still list and the still envs' no_move rows (all sc1) -- for env he (the leg-0
+// lane of each pair, `on`); the env's own constraint values and episode length come from the block's LDS copy.
+// Returns the reward factor 1 - p_max.  The wait is bounded (~20 ms): at the bound it raises bit 2 of the device
+// diagnostic word (h12env_check) and goes on with what it has.
+H12_DEV float cat_prob_inline(const Workspace& W, const StepArgs& A, int he, int j, bool on, bool reset,
+                              const float* vs, const float* vp) {
+  const auto& P = kparams4();
+  const int lane = threadIdx.x & 63;
+  CatLds& cv = cat_lds();
+  int m0 = 0;
+  if (lane == 0) {
+    const unsigned e0 = __float_as_uint(cv[CAT_LROW_EPOCH][0]);
+    int k = 0;
+    // sc1 polls (an acquire per poll would invalidate this CU's caches every time), one acquire fence after: the loads
+    // below stay after the poll that saw the new epoch
+    const auto pub = reinterpret_cast<unsigned long long*>(P.cmeta + 4);
+    unsigned long long w;
+    while (((w = ld_sc1(pub)) >> 32) == e0 && ++k < CAT_WAIT_POLLS) __builtin_amdgcn_s_sleep(2);
+    if (k == CAT_WAIT_POLLS) atomicOr(P.diag, 2);
+    m0 = (int)(unsigned)w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int m = __shfl(m0, 0, 64);
+  // the still list's entry and the reciprocals in one round trip
+  const int src = on && m > 0 ? ld_sc1(&P.clist[he % m]) : -1;
+  float* rinv = &cv[CAT_LROW_RINV][0];  // two rows: 64 floats
+  if (lane < H12_NCSTR_COLS) rinv[lane] = ld_sc1(&P.crun[H12_NCSTR_COLS + lane]);
+  wave_sync();
+  float keep = 1.f;
+  float lg[2 * H12_NCSTR] = {};
+  if (on) keep = cat_prob_env(W, A, he, j, reset, vs, vp, src, rinv, lg);
+  // the block's episode statistics: the value rows reused (every lane has read its values)
+  const bool any = __ballot(on && reset) != 0;
+  wave_sync();
+  if (any && (lane & 1) == 0)
+#pragma unroll
+    for (int k = 0; k < 2 * H12_NCSTR; ++k) cv[k][j] = lg[k];
+  wave_sync();
+  cat_log_block(P.cmask, cv, lane, any, A.log_part, gridDim.x, step_block());  // the envs' block: cat_prob_kernel's slot
+  return keep;
+}
 
 // LDS budget of step_kernel (round 6): the static hand-offs (HelpLds, SelfLds; the same for every feature level K) plus
 // the fused path's dynamic FuseLds must fit the CU's 160 KiB.  A dispatch over the limit is not a HIP error code: the
@@ -3896,6 +4037,16 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       // observes meanwhile (light stamps: sensor + rewards were ~1.0 us of its post-loop 3.7 us)
       constexpr int NT = Feat<K>::ext ? H12_NREW : H12_NREW_FLAT;
       float r = 0.f;
+      bool hreset = false;
+      // cat_inline: the env's constraint sums, loaded now (their round trip overlaps the rewards and barrier F)
+      const bool cat_on = Feat<K>::ext && A.cat_inline && he < W.n && hleg == 0;
+      float cvs[H12_NCSTR], cvp[H12_NCSTR];
+      if (cat_on)
+#pragma unroll
+        for (int t = 0; t < H12_NCSTR; ++t) {
+          cvs[t] = W.F[(size_t)(H12_F_CSTR_SUM + t) * W.n + he];
+          cvp[t] = W.F[(size_t)(H12_F_CSTR_P + t) * W.n + he];
+        }
       if (he < W.n) {
         EnvSt rs;
         float org[3];
@@ -3917,6 +4068,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
           ep[t] += v;
         }
         const bool reset = ri.term || ri.tout;
+        hreset = reset;
         // episode log: the resetting envs' sums go to LDS and lane v below adds value v over the block into this block's
         // own partial slot (value-major [LOG_NPART][blocks]; one shared accumulator made every wave's atomics queue on
         // the same L2 lines: +4.2 us per step).  The assembly kernel that follows folds the partials into log_acc
@@ -3952,6 +4104,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
         __syncthreads();                // F: the physics wave's noisy frames and refill flags
         fuse_late(P, A, fc, W.n, ft, fnt);
       }
+      if (Feat<K>::ext && A.cat_inline) r *= cat_prob_inline(W, A, he, hl >> 1, cat_on, hreset, cvs, cvp);
       // the reward and the episode sums last: their stores issued before barrier F held the vmcnt(0) ahead of it
       if (he < W.n) {
         if (hleg == 0) A.rew[he] = r;
@@ -3964,11 +4117,21 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
       if (A.fuse) fuse_stage(P, A, fc, W.n, ft, fnt);
       __syncthreads();  // L (the helper's final sole contact state is in LDS)
       const bool cat_w = Feat<K>::ext && P.cat && threadIdx.x < 3 * BLOCK;  // the contact wave: the CaT hand-off
-      if (cat_w) cat_handoff(P, W.n);
+      const bool cat_inl = Feat<K>::ext && A.cat_inline;  // (only with A.fuse: barrier F orders the epoch's LDS copy)
+      unsigned cat_e0 = 0;
+      if (cat_w) cat_e0 = cat_handoff(P, W.n, cat_inl);
       int cat_old = -1;
       if (A.fuse) {
         __builtin_amdgcn_s_waitcnt(0);
-        if (cat_w) cat_old = cat_arrive(P);
+        if (cat_w) {
+          cat_old = cat_arrive(P);
+          // cat_inline: every block's helper wave waits for the fold, so the last block folds at once, while its
+          // physics wave resets and observes (off that wave's way to barrier F)
+          if (cat_inl) {
+            if ((threadIdx.x & 63) == 0) cat_lds()[CAT_LROW_EPOCH][0] = __uint_as_float(cat_e0);
+            if (cat_is_last(cat_old)) cat_fold(P, W.n, true);
+          }
+        }
         H12_BW_F_ARRIVAL();
         __syncthreads();  // F
         fuse_late(P, A, fc, W.n, ft, fnt);
@@ -3976,7 +4139,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         cat_old = cat_arrive(P);
       }
-      if (cat_w && cat_is_last(cat_old)) cat_fold(P, W.n);
+      if (cat_w && !cat_inl && cat_is_last(cat_old)) cat_fold(P, W.n, false);
     }
     PH_HELPER_END();
     return;
@@ -4229,9 +4392,12 @@ struct CatArgs {
 };
 constexpr int CAT_PBLOCK = 64;
 __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspace W, CatArgs A) {
+  static_assert(CAT_PBLOCK == 2 * ENVS_PER_BLOCK, "one wave: two step_kernel blocks' envs");
+  __shared__ float Lg[2][2 * H12_NCSTR][ENVS_PER_BLOCK];  // the episode statistics of both step blocks (cat_log_block)
   const int n = W.n;
   const int i = blockIdx.x * CAT_PBLOCK + threadIdx.x;
-  if (i >= n) return;
+  const bool valid = i < n;
+  const int ii = valid ? i : n - 1;  // (the tail lanes compute on a real env and write nothing)
   const float* S = P.cscr;
   // every load is issued up front (one memory round trip for the env's own rows and statistics, one more
   // for the no_move rows of the remapped env), then branch-free arithmetic
@@ -4239,16 +4405,16 @@ __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspa
   constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NM1 = C_COL0[H12_C_NO_MOVE + 1];
 #pragma unroll
   for (int col = 0; col < H12_NCSTR_COLS; ++col)
-    if (col < NM0 || col >= NM1) cv[col] = S[(size_t)col * n + i];
+    if (col < NM0 || col >= NM1) cv[col] = S[(size_t)col * n + ii];
 #pragma unroll
   for (int t = 0; t < H12_NCSTR; ++t) {
-    vs[t] = W.F[(size_t)(H12_F_CSTR_SUM + t) * n + i];
-    vp[t] = W.F[(size_t)(H12_F_CSTR_P + t) * n + i];
+    vs[t] = W.F[(size_t)(H12_F_CSTR_SUM + t) * n + ii];
+    vp[t] = W.F[(size_t)(H12_F_CSTR_P + t) * n + ii];
   }
-  const float len = S[(size_t)CAT_ROW_EPLEN * n + i];
+  const float len = S[(size_t)CAT_ROW_EPLEN * n + ii];
   const int m = P.cmeta[0];
-  const int src = m > 0 ? P.clist[i % m] : -1;
-  const int srow = src >= 0 ? src : i;
+  const int src = m > 0 ? P.clist[ii % m] : -1;
+  const int srow = src >= 0 ? src : ii;
 #pragma unroll
   for (int col = NM0; col < NM1; ++col) cv[col] = src >= 0 ? S[(size_t)col * n + srow] : 0.f;
   float pmax = 0.f;
@@ -4266,24 +4432,37 @@ __global__ void __launch_bounds__(CAT_PBLOCK) cat_prob_kernel(KParams P, Workspa
     }
     pmax = fmaxf(pmax, pt[t]);
   }
-  A.rew[i] *= 1.f - pmax;
-  const bool reset = A.term[i] || A.trunc[i];
-  if (A.cstr_prob) A.cstr_prob[i] = reset ? 1.f : pmax;
+  // the factor pinned: r * (1 - p) left to the compiler became fma(-p, r, r) in one kernel and not the other
+  float keep = 1.f - pmax;
+  pin(keep);
+  const bool reset = valid && (A.term[ii] || A.trunc[ii]);
+  if (valid) {
+    A.rew[i] *= keep;
+    if (A.cstr_prob) A.cstr_prob[i] = reset ? 1.f : pmax;
+  }
   const float inv_len = 1.f / len;
+  const int g = threadIdx.x / ENVS_PER_BLOCK, j = threadIdx.x % ENVS_PER_BLOCK;
 #pragma unroll
   for (int t = 0; t < H12_NCSTR; ++t) {
+    Lg[g][t][j] = Lg[g][H12_NCSTR + t][j] = 0.f;
     if (!((P.cmask >> t) & 1u)) continue;
     float a = vs[t] + (pt[t] > 0.f ? 1.f : 0.f), b = vp[t] + pt[t];
     if (reset) {
-      if (A.log_part) {  // this block's partial slots (see step_kernel's episode log)
-        atomicAdd(&A.log_part[(size_t)(LOG_NSTEP + t) * A.log_nb + blockIdx.x], a * inv_len);
-        atomicAdd(&A.log_part[(size_t)(LOG_NSTEP + H12_NCSTR + t) * A.log_nb + blockIdx.x], b * inv_len);
-      }
+      Lg[g][t][j] = a * inv_len;
+      Lg[g][H12_NCSTR + t][j] = b * inv_len;
       a = b = 0.f;
     }
-    W.F[(size_t)(H12_F_CSTR_SUM + t) * n + i] = a;
-    W.F[(size_t)(H12_F_CSTR_P + t) * n + i] = b;
+    if (valid) {
+      W.F[(size_t)(H12_F_CSTR_SUM + t) * n + i] = a;
+      W.F[(size_t)(H12_F_CSTR_P + t) * n + i] = b;
+    }
   }
+  // the episode statistics per step_kernel block, summed in env order (the order cat_prob_inline sums in)
+  const uint64_t rs = __ballot(reset);
+  wave_sync();
+  const int slot = blockIdx.x * 2 + g;
+  if (slot < A.log_nb)
+    cat_log_block(P.cmask, Lg[g], j, ((rs >> (g * ENVS_PER_BLOCK)) & 0xffffffffull) != 0, A.log_part, A.log_nb, slot);
 }
 
 template <int K>
@@ -4473,6 +4652,7 @@ struct Handle {
   int* dz_cnt = nullptr;  // 3 rotating deadzone counters (UniformVelocityCommandWithDeadzone), then the diagnostic word
   size_t lds_static = 0;  // step_kernel's static LDS as compiled (hipFuncGetAttributes) and the device's LDS per CU
   int lds_limit = 0;
+  bool cat_inline = false;  // CaT's probabilities inside step_kernel (cat_prob_inline; check_cat_inline)
   uint64_t dz_step = 0;
   void* cat_mem = nullptr;  // CaT buffers (scratch, column keys, running maxima, no_move list, meta)
   bool timing = false;
@@ -4791,6 +4971,28 @@ int check_step_lds(Handle* h) {
   return 0;
 }
 
+// CaT with the fused rows: step_kernel applies the probabilities itself (cat_prob_inline) when its whole grid is
+// resident -- every block's helper wave waits for the last block's fold, so a block that could not start until another
+// ended would wait for ever (bounded, and reported by h12env_check, but wrong) -- else cat_prob_kernel follows as before.
+// H12_CAT_INLINE=0 at h12env_create asks for the two-kernel path.
+void check_cat_inline(Handle* h) {
+  h->cat_inline = false;
+  if (!h->P.cat || !h->fuse) return;
+  const char* ci = getenv("H12_CAT_INLINE");
+  if (ci && ci[0] == '0') return;
+  int per_cu = 0, cus = 0;
+  const int threads = (h->P.self_coll ? 4 : 3) * BLOCK;
+  hipError_t e;
+  switch (feature_level(h->P)) {
+    case 0: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<0>, threads, sizeof(FuseLds)); break;
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<1>, threads, sizeof(FuseLds)); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<2>, threads, sizeof(FuseLds)); break;
+  }
+  if (e != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+    return;
+  h->cat_inline = (long long)per_cu * cus >= (long long)n_blocks(h);
+}
+
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
 int launch_assemble(const Handle* h, const float* obs_prev, float* obs, const uint8_t* fill_a, const uint8_t* fill_b,
                     const uint8_t* sel, int reset_mode, uint32_t lo, uint32_t hi, hipStream_t stream,
@@ -5005,9 +5207,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     const size_t nn = (size_t)n_envs;
     const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };  // every section 256-B aligned (cat_fold's 8-B loads)
-    const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * H12_NCSTR_COLS * nbk) +
-                             al(sizeof(float) * 2 * H12_NCSTR_COLS) + al(sizeof(int) * nn) + 256 +
-                             al(sizeof(uint32_t) * nbk);
+    const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * 2 * H12_NCSTR_COLS) +
+                             al(sizeof(int) * nn) + 256 + al(sizeof(uint32_t) * nbk);
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
     if (e != hipSuccess) {
@@ -5019,7 +5220,6 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     }
     char* q = (char*)h->cat_mem;
     h->P.cscr = (float*)q; q += al(sizeof(float) * CAT_ROWS * nn);
-    h->P.cpart = (float*)q; q += al(sizeof(float) * H12_NCSTR_COLS * nbk);
     h->P.crun = (float*)q; q += al(sizeof(float) * 2 * H12_NCSTR_COLS);
     h->P.clist = (int*)q; q += al(sizeof(int) * nn);
     h->P.cmeta = (int*)q;  // 64 ints of meta, then the still masks (cat_ccount, cat_cstill)
@@ -5051,6 +5251,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     h12env_destroy((h12env*)h);
     return rc;
   }
+  check_cat_inline(h);
   h->env_offset = env_offset;
   h->reset_calls = 0;
   h->observe_calls = 0;
@@ -5156,6 +5357,8 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
   A.fuse = h->fuse && ((((uintptr_t)obs_prev | (uintptr_t)out->obs) & 15u) == 0);
   A.frame_out = out->frame_out;
   A.fuse_code = h->fuse_code;
+  A.cat_inline = h->cat_inline && A.fuse;
+  if (A.cat_inline) A.cstr_prob = out->cstr_prob;
   // timing: pair 0 = step_kernel, pair 1 = the second kernel (a flushed fold above, the assembly kernel below, or
   // an empty pair)
   hipEvent_t k0, k1;
@@ -5165,7 +5368,7 @@ int h12env_step(h12env* hh, const float* actions, const float* obs_prev, const h
             A.fuse ? sizeof(FuseLds) : 0, st, h->P, h->W, A);
   HIP_TRY(hipGetLastError());
   if (out->log_acc) h->log_pos = (h->log_pos + 1) % LOG_RING;
-  if (h->P.cat) {
+  if (h->P.cat && !A.cat_inline) {
     // (the running maxima and the still list were folded by step_kernel's last block, cat_fold)
     static_assert(CAT_PBLOCK >= ENVS_PER_BLOCK, "cat_prob_kernel's blocks fit the partial slots of step_kernel's");
     CatArgs C = {out->rew, out->terminated, out->truncated, out->cstr_prob, part, n_blocks(h)};
@@ -5479,9 +5682,18 @@ int h12env_check(h12env* hh, void* stream) {
   HIP_TRY(hipMemcpy(&d, h->P.diag, sizeof(int), hipMemcpyDeviceToHost));
   if (!d) return 0;
   HIP_TRY(hipMemset(h->P.diag, 0, sizeof(int)));
+  if (d & 1)
+    return set_err(H12_E_STATE,
+                   "self-contact: a wait for the contact wave's release ended at its bound (diagnostic 0x%x) since the "
+                   "last check; the self-contact wrenches of that inner step may be partial", (unsigned)d);
   return set_err(H12_E_STATE,
-                 "self-contact: a wait for the contact wave's release ended at its bound (diagnostic 0x%x) since the "
-                 "last check; the self-contact wrenches of that inner step may be partial", (unsigned)d);
+                 "CaT: a block's wait for the last block's fold ended at its bound (diagnostic 0x%x) since the last "
+                 "check; that step's constraint probabilities may be stale", (unsigned)d);
+}
+
+int h12env_cat_inline(const h12env* hh) {
+  const Handle* h = (const Handle*)hh;
+  return h && h->cat_inline ? 1 : 0;
 }
 
 int h12env_obs_fused(const h12env* hh) {

@@ -264,6 +264,9 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_check.restype = C.c_int
     lib.h12env_obs_fused.argtypes = [vp]
     lib.h12env_obs_fused.restype = C.c_int
+    if hasattr(lib, "h12env_cat_inline"):  # (a round-5 library, loaded as an A/B baseline, lacks it)
+        lib.h12env_cat_inline.argtypes = [vp]
+        lib.h12env_cat_inline.restype = C.c_int
     lib.h12env_observe.argtypes = [vp, vp, vp, vp, vp]
     lib.h12env_observe.restype = C.c_int
     lib.h12env_set_terrain.argtypes = [vp, vp, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, vp, C.c_int, C.c_int]
@@ -328,7 +331,7 @@ def check(lib, rc: int, what: str):
 
 EXPORTED_SYMBOLS = [
     "h12env_config_default", "h12env_state_bytes", "h12env_create", "h12env_destroy", "h12env_reset",
-    "h12env_step", "h12env_flush_log", "h12env_obs_fused", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
+    "h12env_step", "h12env_flush_log", "h12env_obs_fused", "h12env_cat_inline", "h12env_observe", "h12env_step_physics", "h12env_field_ptr", "h12env_num_envs", "h12env_step_cost",
     "h12env_last_error", "h12env_abi_version", "h12env_sizeof_struct", "h12env_kernel_cost",
     "h12env_set_kernel_timing", "h12env_kernel_times", "h12env_set_terrain", "h12env_obs_dim",
     "h12env_set_reward_weights", "h12env_set_constraint_max_p", "h12env_eval_terms", "h12env_eval_self_contacts",

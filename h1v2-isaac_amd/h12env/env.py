@@ -715,6 +715,12 @@ class H12VelocityEnv:
         cost pairs is then the deferred episode-log fold, else the observation assembly kernel."""
         return bool(self._lib.h12env_obs_fused(self._h))
 
+    @property
+    def cat_inline(self) -> bool:
+        """CaT: step() applies the constraint probabilities inside the env kernel (h12env_cat_inline), with no
+        separate probability kernel after it."""
+        return hasattr(self._lib, "h12env_cat_inline") and bool(self._lib.h12env_cat_inline(self._h))
+
     def kernel_cost(self, kernel: int):
         """(compulsory HBM bytes, counted FLOPs) per env of kernel 0 (env step) or 1 (obs assembly, or the log fold
         per step on the fused path)."""

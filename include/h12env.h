@@ -347,6 +347,11 @@ int h12env_flush_log(h12env* h, void* stream);
  * CaT -- with 16-byte aligned obs / obs_prev; environment variable H12_FUSE_OBS=0 at h12env_create selects the two-kernel
  * path), else 0.  Results are bit-identical either way; the kernel timing / cost pairs name different kernels. */
 int h12env_obs_fused(const h12env* h);
+/* (ABI 9, round 6) 1 when a CaT handle's h12env_step applies the constraint probabilities inside the env kernel (the
+ * fused path, with the kernel's whole grid resident on the device; environment variable H12_CAT_INLINE=0 at
+ * h12env_create selects the two-kernel path), else 0.  Results are bit-identical either way.  Replaces the separate
+ * probability pass of CaT.compute (biped_tasks/utils/cat/cat_env.py:95-193, constraint_manager.py:126-269). */
+int h12env_cat_inline(const h12env* h);
 /* ObservationManager.compute() outside step(): appends one frame of the current state to every
  * env's history (obs_prev -> obs, may alias); fill_mask[i] != 0 fills env i's history with the frame
  * (the first push after a reset).  fill_mask may be NULL. */

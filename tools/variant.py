@@ -185,6 +185,24 @@ PATCHES_HEAD["scratch_pad"] = PATCHES_HEAD["late_step_args"] + [
     ("  H12_BW_KSTART();\n  kernarg_warm();\n",
      "  H12_BW_KSTART();\n  kernarg_warm();\n  if (P.dbg_norel == 0x5eed) {\n    volatile int pad[17];\n"
      "    pad[threadIdx.x % 17] = (int)threadIdx.x;\n    P.diag[0] = pad[(threadIdx.x + 1) % 17];\n  }\n")]
+# round 6 CaT in-kernel probabilities, timing probes (results wrong): the helper waves skip the wait for the fold's
+# epoch; or they wait but skip the per-env probability chain after it
+PATCHES_HEAD["cat_nowait"] = [("    while (((w = ld_sc1(pub)) >> 32) == e0 && ++k < CAT_WAIT_POLLS) __builtin_amdgcn_s_sleep(2);\n",
+                               "    w = ld_sc1(pub); (void)e0;\n")]
+PATCHES_HEAD["cat_nochain"] = [("  if (on) keep = cat_prob_env(W, A, he, j, reset, vs, vp, src, rinv, lg);\n",
+                                "  (void)vs; (void)vp; (void)src; (void)reset;\n")]
+# ... and the floor: no hand-off, fold, wait or probabilities at all (the constraint values are still computed)
+PATCHES_HEAD["cat_floor"] = [
+    ("      const bool cat_w = Feat<K>::ext && P.cat && threadIdx.x < 3 * BLOCK;", "      const bool cat_w = false;"),
+    ("      if (Feat<K>::ext && A.cat_inline) r *= cat_prob_inline(W, A, he, hl >> 1, cat_on, hreset, cvs, cvp);\n", "")]
+# ... the fold after barrier F (the non-last blocks do not wait for their add's return before F), before the rows;
+# and the hand-off without the still envs' no_move row stores (results wrong: timing of that part)
+PATCHES_HEAD["cat_fold_after_f"] = [
+    ("            if (cat_is_last(cat_old)) cat_fold(P, W.n, true);\n", ""),
+    ("        __syncthreads();  // F\n        fuse_late(P, A, fc, W.n, ft, fnt);\n      } else if (cat_w) {",
+     "        __syncthreads();  // F\n        if (cat_w && cat_inl && cat_is_last(cat_old)) cat_fold(P, W.n, true);\n"
+     "        fuse_late(P, A, fc, W.n, ft, fnt);\n      } else if (cat_w) {")]
+PATCHES_HEAD["cat_no_nmrows"] = [("        st_sc1(&P.cscr[(size_t)(NM0 + k) * n + e], cv[NM0 + k][j]);\n", "        (void)e;\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
