@@ -299,7 +299,8 @@ struct KParams {
                           // encodings, maxed by every block (cat_cmax); from [64] on: each env chunk's still
                           // (no_move-active) envs as a 32-bit mask (cat_cstill)
   // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
-  // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial
+  // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial;
+  // bit 1 = a CaT wait for the last block's fold ended at its bound (cat_prob_inline)
   int* diag;
   int dbg_norel;          // test hook (H12_TEST_SKIP_SELF_RELEASE=1 at h12env_create): the contact wave never releases
 };
@@ -3958,7 +3959,7 @@ H12_DEV float cat_prob_env(const Workspace& W, const StepArgs& A, int he, int j,
 // cat_prob_kernel's per-env step (below) by the helper wave after barrier F, once the last block's fold is published --
 // the running maxima's reciprocals, the still list and the still envs' no_move rows (all sc1) -- for env he (the leg-0
 // lane of each pair, `on`); the env's own constraint values and episode length come from the block's LDS copy.
-// Returns the reward factor 1 - p_max.  The wait is bounded (~20 ms): at the bound it raises bit 2 of the device
+// Returns the reward factor 1 - p_max.  The wait is bounded (~20 ms): at the bound it raises bit 1 of the device
 // diagnostic word (h12env_check) and goes on with what it has.
 H12_DEV float cat_prob_inline(const Workspace& W, const StepArgs& A, int he, int j, bool on, bool reset,
                               const float* vs, const float* vp) {

@@ -448,7 +448,8 @@ int h12env_set_kernel_timing(h12env* h, int enable);
 int h12env_step_lds(const h12env* h, size_t* static_bytes, size_t* dynamic_bytes, size_t* limit_bytes);
 /* Synchronises the stream and reads / clears the device diagnostic word: H12_E_STATE with a message when a
  * self-contact wait in step_kernel ended at its bound since the last check (that inner step's self-contact
- * wrenches may be partial), else 0.  The Python host calls it when it already synchronises (episode-log reads,
+ * wrenches may be partial), or (round 6) a CaT block's wait for the last block's fold did (that step's constraint
+ * probabilities may be stale), else 0.  The Python host calls it when it already synchronises (episode-log reads,
  * close).  No reference counterpart (PhysX reports solver failures through its own error callback). */
 int h12env_check(h12env* h, void* stream);
 int h12env_kernel_times(h12env* h, double* env_ms, double* obs_ms, int* n_steps);
