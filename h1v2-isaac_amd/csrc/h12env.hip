@@ -291,11 +291,13 @@ struct KParams {
   float cvlim[NL], celim[NL];  // joint velocity / effort limits (leg-symmetric)
   float c_ff, c_nm_dz, c_nm_v, c_or, c_h, c_hstd, c_clr, c_clr_dz;
   float* cscr;            // [CAT_ROWS][n] raw constraints of the step (+ no_move flag, pre-reset episode length)
-  float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals
+  float* crun;            // [2][H12_NCSTR_COLS] running maxima (CaT.running_maxes) and their reciprocals; 512 B after
+                          // it, cat_inline's published fold (cat_cpub: no field of its own -- one more kernel argument
+                          // shifted step_kernel's kernarg layout and measured 0.7 % slower on the Flat window)
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
   int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised, [2] = step_kernel
-                          // blocks done with their CaT hand-off this launch (cat_fold); [4..5] = the published fold
-                          // (epoch << 32 | m, cat_pub); [8..63] = the step's column maxima as order-preserving integer
+                          // blocks done with their CaT hand-off this launch (cat_fold); [8..63] = the step's column
+                          // maxima as order-preserving integer
                           // encodings, maxed by every block (cat_cmax); from [64] on: each env chunk's still
                           // (no_move-active) envs as a 32-bit mask (cat_cstill)
   // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
@@ -3771,17 +3773,25 @@ H12_DEV void kernarg_warm() {
 // every block maxed in, and the still envs in ascending order (constraints.no_move hands env i the row of the
 // (i mod m)-th still env, constraints.py:202-238) from the blocks' masks -- what the one-block cat_reduce_kernel launch
 // did (7.1 us per step).  Every load of the hand-off is an sc1 (agent-scope relaxed) load, as the hand-off's rule asks;
-// with cat_inline the fold is published (cat_pub) once its stores have completed.
+// with cat_inline the fold's outputs also go out as epoch-tagged words (cpub).
 H12_DEV int* cat_ccount(const KParams& P) { return P.cmeta + 2; }
 H12_DEV uint32_t* cat_cstill(const KParams& P) { return reinterpret_cast<uint32_t*>(P.cmeta + 64); }
 template <typename T>
 H12_DEV T ld_sc1(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T>
 H12_DEV void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// the published fold (cat_inline): epoch << 32 | m, one 8-B word -- the epoch +1 per fold, stored after the fold's other
-// stores completed; the blocks wait past the epoch they read before their own arrival (no block can read the new one
-// early: the fold needs every arrival), and the word that ends the wait carries m
-H12_DEV unsigned long long* cat_pub(const KParams& P) { return reinterpret_cast<unsigned long long*>(P.cmeta + 4); }
+// the published fold (cat_inline): every value the blocks read after the fold is an 8-B word tagged with the fold's
+// epoch (epoch << 32 | value; +1 per fold), so a word is its own "ready" flag -- no store-completion wait and no
+// separate flag store in the fold, and the waiters poll the very words they need.  A block reads the epoch (the m
+// word's tag) before its own arrival, so it cannot see the next one early: the fold needs every arrival.
+// cat_cpub: every word (epoch << 32 | value): [0, 56) the reciprocals, [56] m, [64 + k] the k-th still env
+constexpr int CPUB_M = 56, CPUB_LIST = 64;
+constexpr size_t CPUB_OFF = 512;  // after crun (2 x 56 floats, its section 256-B aligned: h12env_create)
+static_assert(2 * H12_NCSTR_COLS * sizeof(float) <= CPUB_OFF, "crun fits ahead of the published fold");
+H12_DEV unsigned long long* cat_cpub(const float* crun) {
+  return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(const_cast<float*>(crun)) + CPUB_OFF);
+}
+H12_DEV unsigned long long cat_tag(unsigned epoch, unsigned v) { return (unsigned long long)epoch << 32 | v; }
 // the column maxima: float -> unsigned with the same order (sign bit flipped for >= 0, all bits for < 0), so every
 // block's maxima go in with one unsigned atomic max per column (exact, order-free); 0 (below every encoding) = none
 H12_DEV unsigned* cat_cmax(const KParams& P) { return reinterpret_cast<unsigned*>(P.cmeta + 8); }
@@ -3792,6 +3802,7 @@ H12_DEV unsigned cat_enc(float f) {
 H12_DEV float cat_dec(unsigned u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
 H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
   const int lane = threadIdx.x & 63;
+  const unsigned e1 = inl ? __float_as_uint(cat_lds()[CAT_LROW_EPOCH][0]) + 1u : 0u;  // this fold's epoch
   const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
   static_assert(H12_NCSTR_COLS <= 56, "the column maxima fit cmeta[8..63]");
   // the column maxima (lane col), read and reset for the next step (the blocks' atomic maxima, cat_handoff)
@@ -3813,7 +3824,11 @@ H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
   const int m = __shfl(incl, 63, 64);
   int off = incl - cnt;
   for (int c = c0; c < c1; ++c)
-    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) st_sc1(&P.clist[off++], c * ENVS_PER_BLOCK + __builtin_ctz(b));
+    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) {
+      const int env = c * ENVS_PER_BLOCK + __builtin_ctz(b);
+      if (inl) st_sc1(&cat_cpub(P.crun)[CPUB_LIST + off++], cat_tag(e1, (unsigned)env));
+      else st_sc1(&P.clist[off++], env);
+    }
   if (lane < H12_NCSTR_COLS) {
     float cm = cmx;
     const bool nm = lane >= C_COL0[H12_C_NO_MOVE] && lane < C_COL0[H12_C_NO_MOVE + 1];
@@ -3823,16 +3838,13 @@ H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
     const float run = P.cmeta[1] ? P.ctau * old + (1.f - P.ctau) * cm : cm;
     st_sc1(&P.crun[lane], run);
     st_sc1(&P.crun[H12_NCSTR_COLS + lane], 1.f / run);
+    if (inl) st_sc1(&cat_cpub(P.crun)[lane], cat_tag(e1, __float_as_uint(1.f / run)));
   }
   if (lane == 0) {
     st_sc1(&P.cmeta[0], m);
     st_sc1(&P.cmeta[1], 1);
     st_sc1(cat_ccount(P), 0);  // the next launch's count
-  }
-  if (inl) {  // every store above has completed, then the epoch: the blocks' cat_prob_inline may read them
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
-      st_sc1(cat_pub(P), (unsigned long long)(__float_as_uint(cat_lds()[CAT_LROW_EPOCH][0]) + 1u) << 32 | (unsigned)m);
+    if (inl) st_sc1(&cat_cpub(P.crun)[CPUB_M], cat_tag(e1, (unsigned)m));
   }
 }
 
@@ -3849,7 +3861,7 @@ H12_DEV unsigned cat_handoff(const KParams& P, int n, bool inl) {
   const CatLds& cv = cat_lds();
   // cat_inline: the fold epoch before this block's arrival (in flight until the arrival's vmcnt(0)), and the still
   // envs' no_move rows again as sc1 stores (cat_prob_inline reads them across blocks: constraints.no_move's remap)
-  const unsigned e0 = inl && col == 0 ? (unsigned)(ld_sc1(cat_pub(P)) >> 32) : 0u;
+  const unsigned e0 = inl && col == 0 ? (unsigned)(ld_sc1(&cat_cpub(P.crun)[CPUB_M]) >> 32) : 0u;
   if (inl) {
     constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NMC = C_COL0[H12_C_NO_MOVE + 1] - NM0;
     const int j = col & (ENVS_PER_BLOCK - 1);
@@ -3966,24 +3978,35 @@ H12_DEV float cat_prob_inline(const Workspace& W, const StepArgs& A, int he, int
   const auto& P = kparams4();
   const int lane = threadIdx.x & 63;
   CatLds& cv = cat_lds();
-  int m0 = 0;
-  if (lane == 0) {
-    const unsigned e0 = __float_as_uint(cv[CAT_LROW_EPOCH][0]);
-    int k = 0;
-    // sc1 polls (an acquire per poll would invalidate this CU's caches every time), one acquire fence after: the loads
-    // below stay after the poll that saw the new epoch
-    const auto pub = reinterpret_cast<unsigned long long*>(P.cmeta + 4);
-    unsigned long long w;
-    while (((w = ld_sc1(pub)) >> 32) == e0 && ++k < CAT_WAIT_POLLS) __builtin_amdgcn_s_sleep(2);
-    if (k == CAT_WAIT_POLLS) atomicOr(P.diag, 2);
-    m0 = (int)(unsigned)w;
+  // lanes 0-55 poll their reciprocal's word, lane 56 the m word, until every one carries this step's epoch (sc1
+  // loads with a short sleep between rounds; bounded, ~20 ms); then each env lane its still-list entry
+  const unsigned e1 = __float_as_uint(cv[CAT_LROW_EPOCH][0]) + 1u;
+  const bool pl = lane <= CPUB_M;
+  unsigned long long w = 0;
+  bool ok = !pl;
+  int k = 0;
+  for (; k < CAT_WAIT_POLLS; ++k) {
+    if (!ok) {
+      w = ld_sc1(&cat_cpub(P.crun)[lane]);
+      ok = (unsigned)(w >> 32) == e1;
+    }
+    if (__ballot(!ok) == 0) break;
+    __builtin_amdgcn_s_sleep(2);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int m = __shfl(m0, 0, 64);
-  // the still list's entry and the reciprocals in one round trip
-  const int src = on && m > 0 ? ld_sc1(&P.clist[he % m]) : -1;
+  const int m = __shfl((int)(unsigned)w, CPUB_M, 64);
+  int src = -1;
+  if (on && m > 0) {
+    const unsigned long long* le = &cat_cpub(P.crun)[CPUB_LIST + he % m];
+    unsigned long long v = ld_sc1(le);
+    for (; (unsigned)(v >> 32) != e1 && k < CAT_WAIT_POLLS; ++k) {
+      __builtin_amdgcn_s_sleep(2);
+      v = ld_sc1(le);
+    }
+    src = (int)(unsigned)v;
+  }
+  if (__ballot(k >= CAT_WAIT_POLLS) != 0 && lane == 0) atomicOr(P.diag, 2);
   float* rinv = &cv[CAT_LROW_RINV][0];  // two rows: 64 floats
-  if (lane < H12_NCSTR_COLS) rinv[lane] = ld_sc1(&P.crun[H12_NCSTR_COLS + lane]);
+  if (lane < H12_NCSTR_COLS) rinv[lane] = __uint_as_float((unsigned)w);
   wave_sync();
   float keep = 1.f;
   float lg[2 * H12_NCSTR] = {};
@@ -5209,7 +5232,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };  // every section 256-B aligned (cat_fold's 8-B loads)
     const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * 2 * H12_NCSTR_COLS) +
-                             al(sizeof(int) * nn) + 256 + al(sizeof(uint32_t) * nbk);
+                             al(sizeof(unsigned long long) * (CPUB_LIST + nn)) + al(sizeof(int) * nn) + 256 +
+                             al(sizeof(uint32_t) * nbk);
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
     if (e != hipSuccess) {
@@ -5222,6 +5246,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     char* q = (char*)h->cat_mem;
     h->P.cscr = (float*)q; q += al(sizeof(float) * CAT_ROWS * nn);
     h->P.crun = (float*)q; q += al(sizeof(float) * 2 * H12_NCSTR_COLS);
+    static_assert((sizeof(float) * 2 * H12_NCSTR_COLS + 255) / 256 * 256 == CPUB_OFF, "cat_cpub follows crun's section");
+    q += al(sizeof(unsigned long long) * (CPUB_LIST + nn));
     h->P.clist = (int*)q; q += al(sizeof(int) * nn);
     h->P.cmeta = (int*)q;  // 64 ints of meta, then the still masks (cat_ccount, cat_cstill)
   }

@@ -204,6 +204,9 @@ PATCHES_HEAD["cat_fold_after_f"] = [
      "        fuse_late(P, A, fc, W.n, ft, fnt);\n      } else if (cat_w) {")]
 PATCHES_HEAD["cat_no_nmrows"] = [("        st_sc1(&P.cscr[(size_t)(NM0 + k) * n + e], cv[NM0 + k][j]);\n", "        (void)e;\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
+# the CaT probes were measured on commit 306df83's kernel (profiles/r6/cat_inline_ab.txt)
+for _k in ("cat_nowait", "cat_nochain", "cat_floor", "cat_fold_after_f", "cat_no_nmrows"):
+    ALL[_k] = ("306df83", ALL[_k][1])
 SOURCES = ("h1v2-isaac_amd/csrc/h12env.hip", "h1v2-isaac_amd/csrc/h12_math.h", "h1v2-isaac_amd/csrc/h12_model_gen.h",
            "include/h12env.h")
 
