@@ -1596,10 +1596,12 @@ H12_DEV void fuse_drain(const FuseCtx& f, int it) {
 
 // CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the contact wave's
 // R1 hand-off array (free once the last inner step's physics wave has read it)
-typedef float CatLds[H12_NCSTR_COLS + 5][ENVS_PER_BLOCK];
+constexpr int CAT_LDS_EXTRA = 13;
+typedef float CatLds[H12_NCSTR_COLS + CAT_LDS_EXTRA][ENVS_PER_BLOCK];
 // rows past the values: CAT_ROW_EPLEN; CAT_LROW_EPOCH (the fold epoch this block waits past, its bits in [0]);
-// CAT_LROW_RINV, +1: the running maxima's reciprocals once folded (cat_prob_inline)
-constexpr int CAT_LROW_EPOCH = H12_NCSTR_COLS + 2, CAT_LROW_RINV = H12_NCSTR_COLS + 3;
+// CAT_LROW_RINV, +1: the running maxima's reciprocals once folded; CAT_LROW_PRE .. +7: the blocks' still prefixes
+// (cat_prob_inline)
+constexpr int CAT_LROW_EPOCH = H12_NCSTR_COLS + 2, CAT_LROW_RINV = H12_NCSTR_COLS + 3, CAT_LROW_PRE = H12_NCSTR_COLS + 5;
 // only the first half: cw1[1] holds the reward inputs (put_rin), written in the same window before barrier L
 static_assert(sizeof(CatLds) <= sizeof(HelpLds::cw1[0]), "CaT values fit the first sole hand-off half");
 H12_DEV CatLds& cat_lds() { return *reinterpret_cast<CatLds*>(&help_lds().cw1[0][0][0]); }
@@ -3784,12 +3786,20 @@ H12_DEV void st_sc1(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HI
 // epoch (epoch << 32 | value; +1 per fold), so a word is its own "ready" flag -- no store-completion wait and no
 // separate flag store in the fold, and the waiters poll the very words they need.  A block reads the epoch (the m
 // word's tag) before its own arrival, so it cannot see the next one early: the fold needs every arrival.
-// cat_cpub: every word (epoch << 32 | value): [0, 56) the reciprocals, [56] m, [64 + k] the k-th still env
+// cat_cpub: every word (epoch << 32 | value): [0, 56) the reciprocals, [56] m, [64 + b] the still envs in blocks
+// before block b (the exclusive prefix of the blocks' still counts); then, as floats, the blocks' still envs' no_move
+// rows compacted by the hand-off, [block][12][32] (cat_rows: env i's remapped row -- the (i mod m)-th still env's --
+// is found from the prefixes, one load round trip shorter than a still list)
 constexpr int CPUB_M = 56, CPUB_LIST = 64;
+constexpr int CAT_NMC = C_COL0[H12_C_NO_MOVE + 1] - C_COL0[H12_C_NO_MOVE];
+H12_DEV int cat_nbpad(int n) { return ((n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK + 31) / 32 * 32; }
 constexpr size_t CPUB_OFF = 512;  // after crun (2 x 56 floats, its section 256-B aligned: h12env_create)
 static_assert(2 * H12_NCSTR_COLS * sizeof(float) <= CPUB_OFF, "crun fits ahead of the published fold");
 H12_DEV unsigned long long* cat_cpub(const float* crun) {
   return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(const_cast<float*>(crun)) + CPUB_OFF);
+}
+H12_DEV float* cat_rows(const float* crun, int n) {
+  return reinterpret_cast<float*>(cat_cpub(crun) + CPUB_LIST + cat_nbpad(n));
 }
 H12_DEV unsigned long long cat_tag(unsigned epoch, unsigned v) { return (unsigned long long)epoch << 32 | v; }
 // the column maxima: float -> unsigned with the same order (sign bit flipped for >= 0, all bits for < 0), so every
@@ -3812,9 +3822,16 @@ H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
     st_sc1(cat_cmax(P) + lane, 0u);
   }
   // the still envs: lane l owns the env chunks [l q, l q + q), an exclusive prefix of the counts over the lanes
+  // (the masks loaded once: at most 4 chunks per lane -- cat_inline grids have <= 256 blocks, the fallback's larger
+  // ones loop)
   const int q = (nb + 63) / 64, c0 = min(nb, lane * q), c1 = min(nb, c0 + q);
+  uint32_t mk[4] = {};
   int cnt = 0;
-  for (int c = c0; c < c1; ++c) cnt += __popc(ld_sc1(&cat_cstill(P)[c]));
+  for (int c = c0; c < c1; ++c) {
+    const uint32_t b = ld_sc1(&cat_cstill(P)[c]);
+    if (c - c0 < 4) mk[c - c0] = b;
+    cnt += __popc(b);
+  }
   int incl = cnt;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3823,12 +3840,18 @@ H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
   }
   const int m = __shfl(incl, 63, 64);
   int off = incl - cnt;
-  for (int c = c0; c < c1; ++c)
-    for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) {
-      const int env = c * ENVS_PER_BLOCK + __builtin_ctz(b);
-      if (inl) st_sc1(&cat_cpub(P.crun)[CPUB_LIST + off++], cat_tag(e1, (unsigned)env));
-      else st_sc1(&P.clist[off++], env);
+  if (inl) {  // the blocks' prefixes
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (c0 + i < c1) {
+        st_sc1(&cat_cpub(P.crun)[CPUB_LIST + c0 + i], cat_tag(e1, (unsigned)off));
+        off += __popc(mk[i]);
+      }
     }
+  } else {  // the still list (cat_prob_kernel)
+    for (int c = c0; c < c1; ++c)
+      for (uint32_t b = ld_sc1(&cat_cstill(P)[c]); b; b &= b - 1u) st_sc1(&P.clist[off++], c * ENVS_PER_BLOCK + __builtin_ctz(b));
+  }
   if (lane < H12_NCSTR_COLS) {
     float cm = cmx;
     const bool nm = lane >= C_COL0[H12_C_NO_MOVE] && lane < C_COL0[H12_C_NO_MOVE + 1];
@@ -3862,13 +3885,15 @@ H12_DEV unsigned cat_handoff(const KParams& P, int n, bool inl) {
   // cat_inline: the fold epoch before this block's arrival (in flight until the arrival's vmcnt(0)), and the still
   // envs' no_move rows again as sc1 stores (cat_prob_inline reads them across blocks: constraints.no_move's remap)
   const unsigned e0 = inl && col == 0 ? (unsigned)(ld_sc1(&cat_cpub(P.crun)[CPUB_M]) >> 32) : 0u;
-  if (inl) {
-    constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NMC = C_COL0[H12_C_NO_MOVE + 1] - NM0;
+  if (inl) {  // compacted: the block's r-th still env at [block][k][r]
+    constexpr int NM0 = C_COL0[H12_C_NO_MOVE];
     const int j = col & (ENVS_PER_BLOCK - 1);
-    if (j < ne && cv[CAT_ROW_NOMOVE][j] != 0.f) {
-      const size_t e = (size_t)step_block() * ENVS_PER_BLOCK + j;
-      for (int k = col / ENVS_PER_BLOCK; k < NMC; k += 64 / ENVS_PER_BLOCK)
-        st_sc1(&P.cscr[(size_t)(NM0 + k) * n + e], cv[NM0 + k][j]);
+    const uint32_t sm = (uint32_t)__ballot(col < ENVS_PER_BLOCK && col < ne && cv[CAT_ROW_NOMOVE][col] != 0.f);
+    if ((sm >> j) & 1u) {
+      const int r = __popc(sm & ((1u << j) - 1u));
+      float* rows = cat_rows(P.crun, n) + (size_t)step_block() * CAT_NMC * ENVS_PER_BLOCK + r;
+      for (int k = col / ENVS_PER_BLOCK; k < CAT_NMC; k += 64 / ENVS_PER_BLOCK)
+        st_sc1(&rows[k * ENVS_PER_BLOCK], cv[NM0 + k][j]);
     }
   }
   if (col < H12_NCSTR_COLS) {
@@ -3924,13 +3949,13 @@ constexpr int cat_col_term(int col) {
 // one env's probabilities (the leg-0 lane of a pair): the reward factor 1 - p_max, the dones' probability, the
 // constraint sums, and its episode statistics into lg (zero unless it resets)
 H12_DEV float cat_prob_env(const Workspace& W, const StepArgs& A, int he, int j, bool reset, const float* vs,
-                           const float* vp, int src, const float* rinv, float* lg) {
+                           const float* vp, const float* srow, const float* rinv, float* lg) {
   const auto& P = kparams4();
   const CatLds& cv = cat_lds();
   constexpr int NM0 = C_COL0[H12_C_NO_MOVE], NM1 = C_COL0[H12_C_NO_MOVE + 1];
   float nmv[NM1 - NM0];
 #pragma unroll
-  for (int k = 0; k < NM1 - NM0; ++k) nmv[k] = src >= 0 ? ld_sc1(&P.cscr[(size_t)(NM0 + k) * W.n + src]) : 0.f;
+  for (int k = 0; k < NM1 - NM0; ++k) nmv[k] = srow ? ld_sc1(&srow[k * ENVS_PER_BLOCK]) : 0.f;
   // one flat loop over the columns (constant trip count: fully unrolled, every index static -- the nested form left
   // a dynamic KParams index that made the compiler copy KParams to scratch); max is exact, so the order is free
   float pt[H12_NCSTR];
@@ -3978,39 +4003,53 @@ H12_DEV float cat_prob_inline(const Workspace& W, const StepArgs& A, int he, int
   const auto& P = kparams4();
   const int lane = threadIdx.x & 63;
   CatLds& cv = cat_lds();
-  // lanes 0-55 poll their reciprocal's word, lane 56 the m word, until every one carries this step's epoch (sc1
-  // loads with a short sleep between rounds; bounded, ~20 ms); then each env lane its still-list entry
+  // the wave polls the words it needs -- lanes 0-55 their reciprocal's, lane 56 m's, every lane up to four block
+  // prefixes -- until each carries this step's epoch (sc1 loads, a short sleep between rounds; bounded, ~20 ms)
   const unsigned e1 = __float_as_uint(cv[CAT_LROW_EPOCH][0]) + 1u;
-  const bool pl = lane <= CPUB_M;
-  unsigned long long w = 0;
-  bool ok = !pl;
+  const int nb = (W.n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  static_assert(CAT_LROW_PRE + 8 <= H12_NCSTR_COLS + CAT_LDS_EXTRA, "256 block prefixes in the CaT rows");
+  const unsigned long long* pub = cat_cpub(P.crun);
+  unsigned long long w[5] = {};
+  uint32_t need = 0;
+  if (lane <= CPUB_M) need |= 1u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < nb) need |= 2u << i;
   int k = 0;
   for (; k < CAT_WAIT_POLLS; ++k) {
-    if (!ok) {
-      w = ld_sc1(&cat_cpub(P.crun)[lane]);
-      ok = (unsigned)(w >> 32) == e1;
-    }
-    if (__ballot(!ok) == 0) break;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if ((need >> i) & 1u) {
+        w[i] = ld_sc1(i == 0 ? &pub[lane] : &pub[CPUB_LIST + lane + 64 * (i - 1)]);
+        if ((unsigned)(w[i] >> 32) == e1) need &= ~(1u << i);
+      }
+    if (__ballot(need != 0) == 0) break;
     __builtin_amdgcn_s_sleep(2);
   }
-  const int m = __shfl((int)(unsigned)w, CPUB_M, 64);
-  int src = -1;
-  if (on && m > 0) {
-    const unsigned long long* le = &cat_cpub(P.crun)[CPUB_LIST + he % m];
-    unsigned long long v = ld_sc1(le);
-    for (; (unsigned)(v >> 32) != e1 && k < CAT_WAIT_POLLS; ++k) {
-      __builtin_amdgcn_s_sleep(2);
-      v = ld_sc1(le);
-    }
-    src = (int)(unsigned)v;
-  }
-  if (__ballot(k >= CAT_WAIT_POLLS) != 0 && lane == 0) atomicOr(P.diag, 2);
+  if (k == CAT_WAIT_POLLS && lane == 0) atomicOr(P.diag, 2);
+  const int m = __shfl((int)(unsigned)w[0], CPUB_M, 64);
   float* rinv = &cv[CAT_LROW_RINV][0];  // two rows: 64 floats
-  if (lane < H12_NCSTR_COLS) rinv[lane] = __uint_as_float((unsigned)w);
+  if (lane < H12_NCSTR_COLS) rinv[lane] = __uint_as_float((unsigned)w[0]);
+  int* pre = reinterpret_cast<int*>(&cv[CAT_LROW_PRE][0]);  // the blocks' prefixes, 8 rows: 256 ints
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < nb) pre[lane + 64 * i] = (int)(unsigned)w[1 + i];
   wave_sync();
   float keep = 1.f;
   float lg[2 * H12_NCSTR] = {};
-  if (on) keep = cat_prob_env(W, A, he, j, reset, vs, vp, src, rinv, lg);
+  // env he's remapped row: the (he mod m)-th still env, in the last block whose prefix is <= he mod m
+  const float* srow = nullptr;
+  if (on && m > 0) {
+    const int kk = he % m;
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= kk) lo = mid;
+      else hi = mid - 1;
+    }
+    srow = cat_rows(P.crun, W.n) + (size_t)lo * CAT_NMC * ENVS_PER_BLOCK + (kk - pre[lo]);
+  }
+  if (on) keep = cat_prob_env(W, A, he, j, reset, vs, vp, srow, rinv, lg);
   // the block's episode statistics: the value rows reused (every lane has read its values)
   const bool any = __ballot(on && reset) != 0;
   wave_sync();
@@ -5014,7 +5053,8 @@ void check_cat_inline(Handle* h) {
   }
   if (e != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
     return;
-  h->cat_inline = (long long)per_cu * cus >= (long long)n_blocks(h);
+  // (and at most 256 blocks: the waiting wave reads four block prefixes per lane, cat_prob_inline)
+  h->cat_inline = (long long)per_cu * cus >= (long long)n_blocks(h) && n_blocks(h) <= 256;
 }
 
 // obs_assemble_kernel after an env kernel on the same stream (history blocks + frame blocks)
@@ -5232,7 +5272,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     const size_t nbk = (nn + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };  // every section 256-B aligned (cat_fold's 8-B loads)
     const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * 2 * H12_NCSTR_COLS) +
-                             al(sizeof(unsigned long long) * (CPUB_LIST + nn)) + al(sizeof(int) * nn) + 256 +
+                             al(sizeof(unsigned long long) * (CPUB_LIST + (nbk + 31) / 32 * 32) +
+                                sizeof(float) * CAT_NMC * ENVS_PER_BLOCK * nbk) + al(sizeof(int) * nn) + 256 +
                              al(sizeof(uint32_t) * nbk);
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
@@ -5247,7 +5288,8 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     h->P.cscr = (float*)q; q += al(sizeof(float) * CAT_ROWS * nn);
     h->P.crun = (float*)q; q += al(sizeof(float) * 2 * H12_NCSTR_COLS);
     static_assert((sizeof(float) * 2 * H12_NCSTR_COLS + 255) / 256 * 256 == CPUB_OFF, "cat_cpub follows crun's section");
-    q += al(sizeof(unsigned long long) * (CPUB_LIST + nn));
+    q += al(sizeof(unsigned long long) * (CPUB_LIST + (nbk + 31) / 32 * 32) +
+            sizeof(float) * CAT_NMC * ENVS_PER_BLOCK * nbk);
     h->P.clist = (int*)q; q += al(sizeof(int) * nn);
     h->P.cmeta = (int*)q;  // 64 ints of meta, then the still masks (cat_ccount, cat_cstill)
   }

@@ -21,6 +21,11 @@ for t in range(3):
     bad = torch.nonzero(dr > 0).flatten()
     print(f"t={t} obs_eq={torch.equal(oa['policy'], ob['policy'])} rew ndiff={int((dr > 0).sum())} max={dr.max().item():.3e}"
           f" prob ndiff={int((dt > 0).sum())} max={dt.max().item():.3e} first={bad[:12].tolist()}")
+    from h12env._abi import F as FIELDS
+    for key in ("CSTR_SUM", "CSTR_P"):
+        o, c = FIELDS[key]
+        da = (a._fstate[o:o + c] != b._fstate[o:o + c])
+        print("  ", key, "per term ndiff", da.sum(dim=1).tolist())
     if len(bad):
         i = bad[:4]
         print("  ra", ra[i].tolist(), "rb", rb[i].tolist())
