@@ -1597,7 +1597,9 @@ H12_DEV void fuse_drain(const FuseCtx& f, int it) {
 // CaT, after the physics loop: the step's raw constraint values and the no_move flag [col][env], in the contact wave's
 // R1 hand-off array (free once the last inner step's physics wave has read it)
 constexpr int CAT_LDS_EXTRA = 13;
-typedef float CatLds[H12_NCSTR_COLS + CAT_LDS_EXTRA][ENVS_PER_BLOCK];
+// rows of 33: the contact wave's hand-off reads a column per lane (lane col, row col) -- with rows of 32 floats every
+// other lane hit the same bank (28-way conflicts per read)
+typedef float CatLds[H12_NCSTR_COLS + CAT_LDS_EXTRA][ENVS_PER_BLOCK + 1];
 // rows past the values: CAT_ROW_EPLEN; CAT_LROW_EPOCH (the fold epoch this block waits past, its bits in [0]);
 // CAT_LROW_RINV, +1: the running maxima's reciprocals once folded; CAT_LROW_PRE .. +7: the blocks' still prefixes
 // (cat_prob_inline)
@@ -3925,7 +3927,8 @@ H12_DEV bool cat_is_last(int old) { return __shfl(old, 0, 64) == (int)gridDim.x 
 // zero for envs that do not reset), summed in env order by lane k and added to the block's partial slot -- the same
 // order on both paths (float atomics from one instruction, the round-5 form, summed in an order the two paths did not
 // share).  `any`: some env of the block resets (else nothing to add).
-H12_DEV void cat_log_block(uint32_t cmask, const float (*L)[ENVS_PER_BLOCK], int k, bool any, float* log_part,
+template <int S>
+H12_DEV void cat_log_block(uint32_t cmask, const float (*L)[S], int k, bool any, float* log_part,
                            int log_nb, int slot) {
   if (!any || !log_part || k >= 2 * H12_NCSTR || !((cmask >> (k % H12_NCSTR)) & 1u)) return;
   float sum = 0.f;
