@@ -296,9 +296,9 @@ struct KParams {
                           // shifted step_kernel's kernarg layout and measured 0.7 % slower on the Flat window)
   int* clist;             // [n] no_move-active envs in ascending order (the reference's row remap)
   int* cmeta;             // [0] = number of no_move-active envs, [1] = running maxima initialised, [2] = step_kernel
-                          // blocks done with their CaT hand-off this launch (cat_fold); [8..63] = the step's column
-                          // maxima as order-preserving integer
-                          // encodings, maxed by every block (cat_cmax); from [64] on: each env chunk's still
+                          // blocks done with their CaT hand-off this launch (cat_fold); [64, 64 + 8 x 56) = the step's
+                          // column maxima (eight sets) as order-preserving integer
+                          // encodings, maxed by every block (cat_cmax); from [64 + 448] on: each env chunk's still
                           // (no_move-active) envs as a 32-bit mask (cat_cstill)
   // device diagnostic word (handle-owned, read and cleared by h12env_check): bit 0 = a self-contact wait for the
   // contact wave's release ended at its bound (self_finish), so that inner step's self-contact wrenches may be partial;
@@ -3778,8 +3778,9 @@ H12_DEV void kernarg_warm() {
 // (i mod m)-th still env, constraints.py:202-238) from the blocks' masks -- what the one-block cat_reduce_kernel launch
 // did (7.1 us per step).  Every load of the hand-off is an sc1 (agent-scope relaxed) load, as the hand-off's rule asks;
 // with cat_inline the fold's outputs also go out as epoch-tagged words (cpub).
+constexpr int CAT_META_INTS = 64 + 8 * H12_NCSTR_COLS;  // meta, then the eight column-maxima sets (cat_cmax)
 H12_DEV int* cat_ccount(const KParams& P) { return P.cmeta + 2; }
-H12_DEV uint32_t* cat_cstill(const KParams& P) { return reinterpret_cast<uint32_t*>(P.cmeta + 64); }
+H12_DEV uint32_t* cat_cstill(const KParams& P) { return reinterpret_cast<uint32_t*>(P.cmeta + CAT_META_INTS); }
 template <typename T>
 H12_DEV T ld_sc1(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T>
@@ -3806,7 +3807,12 @@ H12_DEV float* cat_rows(const float* crun, int n) {
 H12_DEV unsigned long long cat_tag(unsigned epoch, unsigned v) { return (unsigned long long)epoch << 32 | v; }
 // the column maxima: float -> unsigned with the same order (sign bit flipped for >= 0, all bits for < 0), so every
 // block's maxima go in with one unsigned atomic max per column (exact, order-free); 0 (below every encoding) = none
-H12_DEV unsigned* cat_cmax(const KParams& P) { return reinterpret_cast<unsigned*>(P.cmeta + 8); }
+// eight sets of them, one per XCD slot of the block (blockIdx.x mod 8): 16 blocks per address instead of 128, the
+// fold takes the max of the eight
+constexpr int CAT_CMAX_SETS = 8;
+H12_DEV unsigned* cat_cmax(const KParams& P, int set) {
+  return reinterpret_cast<unsigned*>(P.cmeta + 64) + set * H12_NCSTR_COLS;
+}
 H12_DEV unsigned cat_enc(float f) {
   const unsigned b = __float_as_uint(f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -3816,12 +3822,19 @@ H12_DEV void cat_fold(const KParams& P, int n, bool inl) {
   const int lane = threadIdx.x & 63;
   const unsigned e1 = inl ? __float_as_uint(cat_lds()[CAT_LROW_EPOCH][0]) + 1u : 0u;  // this fold's epoch
   const int nb = (n + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-  static_assert(H12_NCSTR_COLS <= 56, "the column maxima fit cmeta[8..63]");
   // the column maxima (lane col), read and reset for the next step (the blocks' atomic maxima, cat_handoff)
   float cmx = CAT_NEG;
   if (lane < H12_NCSTR_COLS) {
-    cmx = cat_dec(ld_sc1(cat_cmax(P) + lane));
-    st_sc1(cat_cmax(P) + lane, 0u);
+    unsigned u[CAT_CMAX_SETS];
+#pragma unroll
+    for (int x = 0; x < CAT_CMAX_SETS; ++x) u[x] = ld_sc1(cat_cmax(P, x) + lane);
+    unsigned um = 0u;
+#pragma unroll
+    for (int x = 0; x < CAT_CMAX_SETS; ++x) {
+      um = max(um, u[x]);
+      st_sc1(cat_cmax(P, x) + lane, 0u);
+    }
+    cmx = cat_dec(um);
   }
   // the still envs: lane l owns the env chunks [l q, l q + q), an exclusive prefix of the counts over the lanes
   // (the masks loaded once: at most 4 chunks per lane -- cat_inline grids have <= 256 blocks, the fallback's larger
@@ -3907,7 +3920,8 @@ H12_DEV unsigned cat_handoff(const KParams& P, int n, bool inl) {
       const bool ok = j < ne && (!nm || cv[CAT_ROW_NOMOVE][j] != 0.f);
       m = ok ? fmaxf(m, x) : m;
     }
-    __hip_atomic_fetch_max(cat_cmax(P) + col, cat_enc(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(cat_cmax(P, blockIdx.x % CAT_CMAX_SETS) + col, cat_enc(m), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint32_t still = (uint32_t)__ballot(col < ENVS_PER_BLOCK && col < ne && cv[CAT_ROW_NOMOVE][col] != 0.f);
   if (col == 0) __hip_atomic_store(&cat_cstill(P)[step_block()], still, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5276,7 +5290,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };  // every section 256-B aligned (cat_fold's 8-B loads)
     const size_t bytes_cat = al(sizeof(float) * CAT_ROWS * nn) + al(sizeof(float) * 2 * H12_NCSTR_COLS) +
                              al(sizeof(unsigned long long) * (CPUB_LIST + (nbk + 31) / 32 * 32) +
-                                sizeof(float) * CAT_NMC * ENVS_PER_BLOCK * nbk) + al(sizeof(int) * nn) + 256 +
+                                sizeof(float) * CAT_NMC * ENVS_PER_BLOCK * nbk) + al(sizeof(int) * nn) + al(sizeof(int) * CAT_META_INTS) +
                              al(sizeof(uint32_t) * nbk);
     e = hipMalloc(&h->cat_mem, bytes_cat);
     if (e == hipSuccess) e = hipMemset(h->cat_mem, 0, bytes_cat);
@@ -5294,7 +5308,7 @@ int h12env_create(const h12env_model* model, const h12env_config* cfg, int n_env
     q += al(sizeof(unsigned long long) * (CPUB_LIST + (nbk + 31) / 32 * 32) +
             sizeof(float) * CAT_NMC * ENVS_PER_BLOCK * nbk);
     h->P.clist = (int*)q; q += al(sizeof(int) * nn);
-    h->P.cmeta = (int*)q;  // 64 ints of meta, then the still masks (cat_ccount, cat_cstill)
+    h->P.cmeta = (int*)q;  // CAT_META_INTS ints of meta and column maxima, then the still masks (cat_ccount, cat_cstill)
   }
   h->device = device;
   if (h->P.task == H12_TASK_FLAT) {
