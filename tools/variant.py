@@ -203,6 +203,11 @@ PATCHES_HEAD["cat_fold_after_f"] = [
      "        __syncthreads();  // F\n        if (cat_w && cat_inl && cat_is_last(cat_old)) cat_fold(P, W.n, true);\n"
      "        fuse_late(P, A, fc, W.n, ft, fnt);\n      } else if (cat_w) {")]
 PATCHES_HEAD["cat_no_nmrows"] = [("        st_sc1(&P.cscr[(size_t)(NM0 + k) * n + e], cv[NM0 + k][j]);\n", "        (void)e;\n")]
+# round 6 side-rod cost probe (timing only, results wrong): every sole_contacts_flat call evaluates one more sphere (its
+# last one again) -- the work the side rods' front ends would add to each of the two sole waves
+PATCHES_HEAD["siderod_probe"] = [("#pragma unroll\n  for (int q = Q0; q < Q1; ++q) {\n    float r[3];\n",
+                                  "#pragma unroll\n  for (int qq = Q0; qq <= Q1; ++qq) {\n    const int q = qq < Q1 ? qq : Q1 - 1;\n"
+                                  "    float r[3];\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 # the CaT probes were measured on commit 306df83's kernel (profiles/r6/cat_inline_ab.txt)
 for _k in ("cat_nowait", "cat_nochain", "cat_floor", "cat_fold_after_f", "cat_no_nmrows"):
