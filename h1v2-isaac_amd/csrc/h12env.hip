@@ -385,6 +385,22 @@ H12_DEV float ground_local(const KParams& P, const float* org, float xl, float y
 struct Base {               // shared floating base, REAL coordinates (identical in both lanes)
   float pos[3], quat[4], vlin[3], wang[3];
 };
+// A diverged floating base (round 6): any component of the base's angular velocity above 200 rad/s or of its linear
+// velocity above 50 m/s, or not finite, terminates the episode like an illegal contact (the env resets in the same
+// step).  The penalty contacts can blow up (a base spinning at 100+ rad/s for a few steps, then 1e5 rad/s and NaN in
+// a random-action Rsl / CaT run at 8192 envs; PhysX's contact solver does not); IsaacLab has no such term -- DESIGN.md
+// section 9.  Integer compares on the magnitudes' bits: NaN / inf sort above every finite threshold, and no
+// finite-math assumption can fold them away.  The oracle applies the same rule (orc_mdp_terms).
+constexpr float H12_DIV_W = 200.f, H12_DIV_V = 50.f;
+template <typename B>
+H12_DEV bool base_diverged(const B& b) {
+  bool d = false;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    d = d || (__float_as_uint(b.wang[a]) & 0x7fffffffu) > __float_as_uint(H12_DIV_W) ||
+        (__float_as_uint(b.vlin[a]) & 0x7fffffffu) > __float_as_uint(H12_DIV_V);
+  return d;
+}
 struct Leg {                // this lane's leg in the lane frame (mirrored for the right leg)
   float q[NL], qd[NL];
   float anc[H12_NFOOT_PTS][2];
@@ -526,16 +542,17 @@ H12_DEV bool contact_sphere(const KParams& P, const float Rb[3][3], const float*
 // hardware sine of these small angles (1e-5 .. 0.05) is +3.7 ulp high on average (profiles/r6/r6d_hw_math_bias.txt),
 // a signed error that turned every orientation increment 3e-7 (relative) too large; the series is exact to fp32 for
 // a <= 0.5 (|w| <= 200 rad/s at h = 5 ms; the truncation error there is 2.4e-11 in sin a / a, 2.7e-10 in cos a) and
-// needs no square root or reciprocal.  w = 0 leaves q as it is (the oracle's rule)
+// needs no square root or reciprocal.  (Far beyond that range -- a diverging state -- the polynomials can overflow; such
+// a base is terminated by base_diverged at the end of the env step.)  w = 0 leaves q as it is (the oracle's rule)
 H12_DEV void quat_integrate(float* q, const float* w, float h) {
   const float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   if (w2 > 0.f) {
     const float a2 = w2 * (0.25f * h * h);
     // sin(a) / a and cos(a) to a^8
     const float sa = __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, 1.f / 362880.f,
-                                    -1.f / 5040.f), 1.f / 120.f), -1.f / 6.f), 1.f);
+                              -1.f / 5040.f), 1.f / 120.f), -1.f / 6.f), 1.f);
     const float ch = __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, __builtin_fmaf(a2, 1.f / 40320.f,
-                                    -1.f / 720.f), 1.f / 24.f), -0.5f), 1.f);
+                              -1.f / 720.f), 1.f / 24.f), -0.5f), 1.f);
     const float sh = sa * (0.5f * h);
     float r[4] = {ch, w[0] * sh, w[1] * sh, w[2] * sh};
     float o[4] = {q[0] * r[0] - q[1] * r[1] - q[2] * r[2] - q[3] * r[3],
@@ -4299,7 +4316,7 @@ __global__ void __launch_bounds__(4 * BLOCK) step_kernel(KParams P, Workspace W,
     // ---- terminations: time_out, illegal_contact (pair-combined)
     PH(2);
     const bool tout = s.eplen >= P.max_len;
-    int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
+    int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr) || base_diverged(s.b);
     const int term = ill | pair_swap_i(ill);
     // ---- rewards on the pre-reset state: the helper wave's (round 5), while this wave resets and observes -- the final
     // state and the terms' other inputs to LDS
@@ -4442,7 +4459,7 @@ __global__ void __launch_bounds__(BLOCK) terms_kernel(KParams P, Workspace W, Te
   }
   const float fmax_foot = T.fmax[5 * (size_t)e + leg], fmax_knee = T.fmax[5 * (size_t)e + 2 + leg];
   const float fmax_torso = T.fmax[5 * (size_t)e + 4];
-  int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr);
+  int ill = (P.ill_knees && fmax_knee > P.cthr) || (P.ill_torso && fmax_torso > P.cthr) || base_diverged(s.b);
   const int term = ill | pair_swap_i(ill);
   float R[3][3];
   quat_R(s.b.quat, R);

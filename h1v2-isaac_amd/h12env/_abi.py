@@ -258,10 +258,11 @@ def load_library(path: str | os.PathLike | None = None):
     lib.h12env_step.restype = C.c_int
     lib.h12env_flush_log.argtypes = [vp, vp]
     lib.h12env_flush_log.restype = C.c_int
-    lib.h12env_step_lds.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
-    lib.h12env_step_lds.restype = C.c_int
-    lib.h12env_check.argtypes = [vp, vp]
-    lib.h12env_check.restype = C.c_int
+    if hasattr(lib, "h12env_step_lds"):  # round 6 (a round-5 library, loaded as an A/B baseline, lacks these)
+        lib.h12env_step_lds.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        lib.h12env_step_lds.restype = C.c_int
+        lib.h12env_check.argtypes = [vp, vp]
+        lib.h12env_check.restype = C.c_int
     lib.h12env_obs_fused.argtypes = [vp]
     lib.h12env_obs_fused.restype = C.c_int
     if hasattr(lib, "h12env_cat_inline"):  # (a round-5 library, loaded as an A/B baseline, lacks it)

@@ -679,7 +679,7 @@ class H12VelocityEnv:
         self-contact wait in the step kernel ended at its bound since the last check (that inner step's self-contact
         wrenches may be partial; H12EnvError is a RuntimeError).  Called where the host synchronises anyway:
         episode-log reads and close()."""
-        if not self._closed:
+        if not self._closed and hasattr(self._lib, "h12env_check"):
             check(self._lib, self._lib.h12env_check(self._h, _raw_stream(self._dev_index)), "h12env_check")
 
     def _flush_and_check(self):
@@ -690,7 +690,7 @@ class H12VelocityEnv:
         if not self._closed:
             self._flush_log()  # logs still referenced (extras) stay complete
             torch.cuda.synchronize(self.device)
-            rc = self._lib.h12env_check(self._h, _raw_stream(self._dev_index))
+            rc = self._lib.h12env_check(self._h, _raw_stream(self._dev_index)) if hasattr(self._lib, "h12env_check") else 0
             msg = self._lib.h12env_last_error().decode() if rc else ""
             self._lib.h12env_destroy(self._h)
             self._closed = True

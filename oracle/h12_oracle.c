@@ -1493,6 +1493,11 @@ int orc_mdp_terms(const h12env_model* m, const h12env_config* c, const orc_term_
   int term = 0;
   if (c->illegal_contact_knees && (in->fmax_knee[0] > c->contact_threshold || in->fmax_knee[1] > c->contact_threshold)) term = 1;
   if (c->illegal_contact_torso && in->fmax_torso > c->contact_threshold) term = 1;
+  /* a diverged floating base terminates as well (round 6; the kernel's base_diverged: a component of the base's angular
+   * velocity above 200 rad/s or of its linear velocity above 50 m/s, or not finite) -- no reference counterpart: PhysX
+   * does not blow up where the penalty contacts can */
+  for (int a = 0; a < 3; ++a)
+    if (!(fabs((double)in->p.wang[a]) <= 200.0) || !(fabs((double)in->p.vlin[a]) <= 50.0)) term = 1;
   /* rewards (pre-reset state) */
   m3 R;
   quat_to_R(in->p.quat, R);

@@ -38,13 +38,14 @@ def _make(n, inline):
     return env
 
 
-@pytest.mark.parametrize("n", [4096, 300])
-def test_cat_inline_equals_two_kernel_path(gpu, n):
+@pytest.mark.parametrize("n,steps", [(4096, 30), (300, 30), (8192, 200)])
+def test_cat_inline_equals_two_kernel_path(gpu, n, steps):
+    """(8192 envs: 256 blocks, one per CU -- the largest grid the inline path takes; 200 steps.)"""
     a_env, b_env = _make(n, True), _make(n, False)
     assert a_env.cat_inline and not b_env.cat_inline
     gen = torch.Generator(device="cpu").manual_seed(11)
     resets = 0
-    for t in range(30):
+    for t in range(steps):
         # small actions on some envs keep them still under a zero command (no_move's remap)
         act = torch.randn(n, 12, generator=gen) * (0.02 if t % 3 == 0 else 0.4)
         act = act.to(gpu)

@@ -208,6 +208,11 @@ PATCHES_HEAD["cat_no_nmrows"] = [("        st_sc1(&P.cscr[(size_t)(NM0 + k) * n 
 PATCHES_HEAD["siderod_probe"] = [("#pragma unroll\n  for (int q = Q0; q < Q1; ++q) {\n    float r[3];\n",
                                   "#pragma unroll\n  for (int qq = Q0; qq <= Q1; ++qq) {\n    const int q = qq < Q1 ? qq : Q1 - 1;\n"
                                   "    float r[3];\n")]
+# round 6 NaN hunt (rsl / cat at 8192 envs, tools/probe/determinism.py): the self-contact wave's pass 1 with the corrected
+# joint sin / cos; the radial correction off everywhere
+PATCHES_HEAD["nan_selfcorr"] = [("leg_pass1<K, true>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);",
+                                 "leg_pass1<K, false>(leg, b, lg, org, R0, vb, pb0, cs, v, Rk, pk, R, p, true);")]
+PATCHES_HEAD["nan_nocorr"] = [("using namespace h12;\n", "using namespace h12;\n#define fsincos(x, s, c) fsincos_hw(x, s, c)\n")]
 ALL = {**{k: (R4_BASE, v) for k, v in PATCHES.items()}, **{k: (None, v) for k, v in PATCHES_HEAD.items()}}
 # the CaT probes were measured on commit 306df83's kernel (profiles/r6/cat_inline_ab.txt)
 for _k in ("cat_nowait", "cat_nochain", "cat_floor", "cat_fold_after_f", "cat_no_nmrows"):
